@@ -1,0 +1,139 @@
+/*
+ * qtts_hip.h - thin C-ABI between the C host (qwen_tts.c, main.c) and the
+ * MI355X (gfx950) HIP implementation of the Qwen3-TTS hot path.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int error codes
+ * (0 = ok, <0 = error with a message on stderr).  No HIP or torch types.
+ * "dev" pointers below are device (HBM) addresses; "host" pointers are
+ * ordinary process memory.  `stream` arguments are hipStream_t passed as
+ * void* (NULL = the default stream).
+ *
+ * Two layers:
+ *   1. Model-level entry points used by the C host's decode loop
+ *      (qwen_tts.c) - they replace the compute of
+ *        qwen_tts_talker_prefill / qwen_tts_talker_forward   (c/qwen_tts.h:483-486,
+ *                                                            c/qwen_tts_talker.c:254-533)
+ *        qwen_tts_subtalker_generate                         (c/qwen_tts.h:489-494,
+ *                                                            c/qwen_tts_talker.c:539-736)
+ *        the per-frame loop body of qwen_tts_generate       (c/qwen_tts.c:1282-1373)
+ *        qwen_tts_codec_decode                               (c/qwen_tts.h:497-502,
+ *                                                            c/qwen_tts_codec.c:581-749)
+ *   2. Kernel-level entry points on device buffers, one per kernel_* of
+ *      c/qwen_tts_kernels.h the hot path uses, so each HIP kernel is parity
+ *      tested against the CPU oracle in isolation.
+ */
+#ifndef QTTS_HIP_H
+#define QTTS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qtts_dev qtts_dev_t;
+
+/* Model dimensions (same meaning as qwen_tts_config_t, c/qwen_tts.h:84-144). */
+typedef struct {
+    int H, I, L, NH, KV, HD, TH, TV, V, G;   /* talker */
+    int Hs, Is, Ls, NHs, KVs, HDs, Vs;       /* sub-talker (code predictor) */
+    float eps, theta;                        /* talker_rms_norm_eps / talker_rope_theta */
+    int cq, ccb, ccbdim, chid, clat, clayers, cheads, ckv, cinter, cwin, cdec;  /* codec */
+    int rates[4], ratios[2];
+    float ceps;
+    int pad_id, bos_id, eos_id;
+} qtts_dims_t;
+
+/* Generation parameters (qwen_tts_ctx_t fields, c/qwen_tts.h:420-430). */
+typedef struct {
+    float temperature, top_p, repetition_penalty;
+    int top_k;
+    float st_temperature, st_top_p;
+    int st_top_k;
+    int fixed_codec_tokens;
+    int seed;
+} qtts_gen_params_t;
+
+/* ---- device + model ---- */
+int qtts_hip_device_count(void);
+/* Creates the device model on HIP device `device` (selects it for the
+ * calling thread).  Returns NULL on error. */
+qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device);
+void qtts_dev_destroy(qtts_dev_t *dev);
+/* Hands one checkpoint tensor (by its safetensors name) to the device.
+ * dtype: 0 = F32, 1 = BF16, 2 = F16.  Tensors the hot path does not use are
+ * ignored.  Packing (fused [q;k;v], gate|up row quads), bf16 -> f32 of
+ * norms/biases, codebook = embedding_sum / max(usage, 1e-5) and SnakeBeta
+ * pre-exponentiation (c/qwen_tts.c:481-489, 577-602) happen here. */
+int qtts_dev_put_tensor(qtts_dev_t *dev, const char *name, const void *host, int dtype,
+                        const int64_t *shape, int ndim);
+/* Validates that every required tensor arrived (reports the first missing
+ * one like c/qwen_tts.c:381-427) and builds RoPE tables. */
+int qtts_dev_finalize(qtts_dev_t *dev);
+/* Device bytes currently allocated for weights / state. */
+size_t qtts_dev_bytes(const qtts_dev_t *dev, int which /*0 weights, 1 state*/);
+
+/* ---- generation (batch of nb utterances in lock-step frames) ---- */
+/* Allocates state for nb slots, max_frames frames (KV capacity = max_prefill
+ * + max_frames), resets counters / RNG, (re)captures the frame graphs. */
+int qtts_dev_begin(qtts_dev_t *dev, int nb, int max_frames, int max_prefill, const qtts_gen_params_t *p);
+/* Prompt for slot b (layout built by the host, c/qwen_tts.c:1147-1243):
+ *   text_ids[n_text]  text tokens to embed+project (text_embedding -> fc1 ->
+ *                     SiLU -> fc2, c/qwen_tts.c:823-847)
+ *   plan[5*nplan]     per output row {text row, codec id or -1,
+ *                     0 = prefill / 1 = trailing, b, slot}
+ *   p_len, n_trailing prefill / trailing lengths; pad_row = text row of tts_pad */
+int qtts_dev_prompt(qtts_dev_t *dev, int b, const int *text_ids, int n_text, const int *plan, int nplan,
+                    int p_len, int n_trailing, int pad_row);
+/* Talker prefill of all nb slots (leaves each slot's last raw hidden). */
+int qtts_dev_prefill(qtts_dev_t *dev);
+/* Enqueues frame `step` (step 0: codec_head on the prefill hidden; step > 0:
+ * talker forward first): sample group 0 -> sub-talker 15 groups -> next
+ * input embedding.  Asynchronous (one HIP graph launch). */
+int qtts_dev_frame(qtts_dev_t *dev, int step);
+/* Waits for the queued work; stopped[b] = 1 once slot b drew EOS
+ * (non-fixed mode); n_gen[b] frames stored; stop_step[b] as in the
+ * reference's "Stop: eos at step N". */
+int qtts_dev_poll(qtts_dev_t *dev, int *stopped, int *n_gen, int *stop_step);
+/* Copies slot b's codes [n_gen][G] to host. */
+int qtts_dev_get_codes(qtts_dev_t *dev, int b, int *host_codes, int max_frames);
+/* Codec decode of slot b's generated codes (device-resident) into a malloc'd
+ * host buffer of T*1920 samples (caller frees). */
+float *qtts_dev_codec_slot(qtts_dev_t *dev, int b, int T, int *out_samples);
+
+/* ---- host-pointer stage wrappers (oracle-level tests, c/qwen_tts.h:483-502) ---- */
+int qtts_dev_talker_prefill_host(qtts_dev_t *dev, const float *embeds, int n, float *hidden_out);
+int qtts_dev_talker_forward_host(qtts_dev_t *dev, const float *embed, float *logits, float *hidden_out);
+int qtts_dev_subtalker_host(qtts_dev_t *dev, const float *hidden, int first_code, int *out_codes);
+float *qtts_dev_codec_decode_host(qtts_dev_t *dev, const int *codes, int T, int *out_samples);
+
+/* ---- kernel-level entry points (device buffers) ---- */
+/* kernel_matvec_bf16 (c/qwen_tts_kernels.c:95): out[b*rows + r] = sum_c A[r,c] x[b*cols + c] */
+int qtts_hip_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_dev, int rows, int cols,
+                         int batch, void *stream);
+/* kernel_rms_norm fused as a GEMV prologue; exported standalone for tests:
+ * out = rmsnorm(x) @ A^T  (c/qwen_tts_kernels.c:27 + :95) */
+int qtts_hip_rmsnorm_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_dev, const float *w_dev,
+                                 float eps, int rows, int cols, int batch, void *stream);
+/* kernel_sample_top_k (c/qwen_tts_kernels.c:407) on `batch` logit rows; rng_bits
+ * holds the float-bit xorshift state per row (updated in place). */
+int qtts_hip_sample_top_k(int *out_dev, const float *logits_dev, int vocab, int top_k, float top_p,
+                          float temperature, uint32_t *rng_bits_dev, int batch, void *stream);
+/* kernel_causal_conv1d (c/qwen_tts_kernels.c:659): [ci, L] -> [co, L] */
+int qtts_hip_causal_conv1d(float *out_dev, const float *in_dev, const float *w_dev, const float *b_dev, int ci,
+                           int co, int k, int L, int dilation, int groups, void *stream);
+/* kernel_transposed_conv1d (c/qwen_tts_kernels.c:873): [ci, L] -> [co, L*stride] */
+int qtts_hip_transposed_conv1d(float *out_dev, const float *in_dev, const float *w_dev, const float *b_dev,
+                               int ci, int co, int k, int stride, int L, void *stream);
+/* kernel_snake_beta (c/qwen_tts_kernels.c:251), alpha/inv_beta pre-processed */
+int qtts_hip_snake_beta(float *out_dev, const float *x_dev, const float *alpha_dev, const float *inv_beta_dev,
+                        int channels, int length, void *stream);
+/* glibc-exact expf replica used by the sampler (for the libm cross-check test) */
+int qtts_hip_expf_glibc(float *out_dev, const float *in_dev, int n, void *stream);
+int qtts_hip_sync(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QTTS_HIP_H */

@@ -1,0 +1,216 @@
+/*
+ * qwen_tts.h - public C API of the MI355X (gfx950) Qwen3-TTS hot path.
+ *
+ * Drop-in for the reference header c/qwen_tts.h: the same constants, the
+ * same qwen_tts_config_t, the same public functions with the same
+ * signatures, ownership and error behaviour (c/qwen_tts.h:448-502), and a
+ * qwen_tts_ctx_t keeping every field name the reference CLI reads or writes
+ * (config, generation parameters, progress callback, perf counters,
+ * talker_kv_len; c/main.c:214-223,268-270,306-312).  Weights and all
+ * generation state live on the GPU behind `hip` (include/qtts_hip.h); the
+ * CPU-side weight/scratch fields of the reference struct are not present.
+ *
+ *   qwen_tts_load        NULL on failure, message on stderr
+ *   qwen_tts_generate    malloc'd float32 PCM at 24 kHz, caller frees;
+ *                        NULL and *out_samples = 0 on error
+ *   qwen_tts_write_wav   0 / -1
+ *
+ * MI355X additions (not in the reference): qwen_tts_set_device,
+ * qwen_tts_generate_batch, qwen_tts_last_codes.
+ */
+#ifndef QWEN_TTS_H
+#define QWEN_TTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define QWEN_TTS_SAMPLE_RATE      24000
+#define QWEN_TTS_DECODE_UPSAMPLE  1920
+
+/* defaults used when config.json omits a key (c/qwen_tts.h:25-78) */
+#define QWEN_TTS_TALKER_VOCAB        3072
+#define QWEN_TTS_TALKER_HIDDEN       1024
+#define QWEN_TTS_TALKER_INTERMEDIATE 2048
+#define QWEN_TTS_TALKER_LAYERS       20
+#define QWEN_TTS_TALKER_HEADS        16
+#define QWEN_TTS_TALKER_KV_HEADS     2
+#define QWEN_TTS_TALKER_HEAD_DIM     64
+#define QWEN_TTS_TALKER_TEXT_HIDDEN  2048
+#define QWEN_TTS_TALKER_TEXT_VOCAB   151936
+#define QWEN_TTS_NUM_CODE_GROUPS     32
+
+#define QWEN_TTS_SUBTALKER_VOCAB        2048
+#define QWEN_TTS_SUBTALKER_HIDDEN       1024
+#define QWEN_TTS_SUBTALKER_INTERMEDIATE 3072
+#define QWEN_TTS_SUBTALKER_LAYERS       5
+#define QWEN_TTS_SUBTALKER_HEADS        16
+#define QWEN_TTS_SUBTALKER_KV_HEADS     8
+#define QWEN_TTS_SUBTALKER_HEAD_DIM     128
+
+#define QWEN_TTS_CODEC_NUM_QUANTIZERS 16
+#define QWEN_TTS_CODEC_CODEBOOK_SIZE  2048
+#define QWEN_TTS_CODEC_HIDDEN         1024
+#define QWEN_TTS_CODEC_LATENT         1024
+#define QWEN_TTS_CODEC_LAYERS         8
+#define QWEN_TTS_CODEC_HEADS          16
+#define QWEN_TTS_CODEC_KV_HEADS       16
+#define QWEN_TTS_CODEC_INTERMEDIATE   3072
+#define QWEN_TTS_CODEC_SLIDING_WINDOW 72
+#define QWEN_TTS_CODEC_DECODER_DIM    1536
+
+#define QWEN_TTS_MAX_TALKER_LAYERS    32
+#define QWEN_TTS_MAX_SUBTALKER_LAYERS 8
+#define QWEN_TTS_MAX_CODEC_LAYERS     12
+
+#define QWEN_TTS_TOKEN_IM_START  151644
+#define QWEN_TTS_TOKEN_IM_END    151645
+#define QWEN_TTS_TOKEN_ENDOFTEXT 151643
+#define QWEN_TTS_TOKEN_TTS_PAD   151671
+#define QWEN_TTS_TOKEN_TTS_BOS   151672
+#define QWEN_TTS_TOKEN_TTS_EOS   151673
+
+#define QWEN_TTS_CODEC_PAD       2148
+#define QWEN_TTS_CODEC_BOS       2149
+#define QWEN_TTS_CODEC_EOS       2150
+#define QWEN_TTS_CODEC_THINK     2154
+#define QWEN_TTS_CODEC_NOTHINK   2155
+#define QWEN_TTS_CODEC_THINK_BOS 2156
+#define QWEN_TTS_CODEC_THINK_EOS 2157
+
+typedef struct {
+    int talker_vocab_size;
+    int talker_hidden;
+    int talker_intermediate;
+    int talker_layers;
+    int talker_heads;
+    int talker_kv_heads;
+    int talker_head_dim;
+    int talker_text_hidden;
+    int talker_text_vocab;
+    int num_code_groups;
+    float talker_rms_norm_eps;
+    float talker_rope_theta;
+    int mrope_section[3];
+
+    int subtalker_vocab_size;
+    int subtalker_hidden;
+    int subtalker_intermediate;
+    int subtalker_layers;
+    int subtalker_heads;
+    int subtalker_kv_heads;
+    int subtalker_head_dim;
+
+    int codec_num_quantizers;
+    int codec_codebook_size;
+    int codec_codebook_dim;
+    int codec_hidden;
+    int codec_latent;
+    int codec_layers;
+    int codec_heads;
+    int codec_kv_heads;
+    int codec_intermediate;
+    int codec_sliding_window;
+    int codec_decoder_dim;
+    float codec_rms_norm_eps;
+    float codec_layer_scale;
+    int codec_upsample_rates[4];
+    int codec_upsampling_ratios[2];
+
+    int n_speakers;
+    char **speaker_names;
+    int *speaker_ids;
+    int n_languages;
+    char **language_names;
+    int *language_ids;
+
+    int codec_pad_id;
+    int codec_bos_id;
+    int codec_eos_id;
+    int codec_nothink_id;
+    int codec_think_id;
+    int codec_think_bos_id;
+    int codec_think_eos_id;
+} qwen_tts_config_t;
+
+typedef void (*qwen_tts_progress_cb)(int step, int total, void *userdata);
+
+typedef struct {
+    qwen_tts_config_t config;
+    char model_dir[512];
+
+    /* device-resident model + generation state (include/qtts_hip.h) */
+    void *hip;
+    int hip_device;
+
+    int talker_kv_len;          /* positions in the talker KV cache of slot 0 */
+    float *tk_x;                /* host copy of the post-norm last talker hidden (stage API) */
+
+    /* generation parameters (same names and defaults as the reference) */
+    float temperature;
+    float subtalker_temperature;
+    int top_k;
+    int subtalker_top_k;
+    float top_p;
+    float subtalker_top_p;
+    float repetition_penalty;
+    int max_new_tokens;
+    int fixed_codec_tokens;
+    int sample_seed;
+
+    qwen_tts_progress_cb progress_cb;
+    void *progress_cb_userdata;
+
+    /* performance stats */
+    double perf_total_ms;
+    double perf_talker_ms;
+    double perf_codec_ms;
+    int perf_codec_tokens;
+
+    /* MI355X additions */
+    double perf_prefill_ms;
+    double perf_first_frame_ms;  /* generate() entry -> first frame's codes on device */
+    int *last_codes;             /* [last_frames][num_code_groups] of the last call (slot 0) */
+    int last_frames;
+    int last_stop_reason;        /* 1 eos, 2 max_tokens */
+    int last_stop_step;
+} qwen_tts_ctx_t;
+
+qwen_tts_ctx_t *qwen_tts_load(const char *model_dir);
+void qwen_tts_free(qwen_tts_ctx_t *ctx);
+void qwen_tts_set_progress_callback(qwen_tts_ctx_t *ctx, qwen_tts_progress_cb cb, void *userdata);
+float *qwen_tts_generate(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
+                         int *out_samples);
+int qwen_tts_write_wav(const char *path, const float *samples, int n_samples, int sample_rate);
+
+static inline float bf16_to_f32(uint16_t bf16) {
+    uint32_t f32_bits = ((uint32_t)bf16) << 16;
+    float result;
+    __builtin_memcpy(&result, &f32_bits, sizeof(float));
+    return result;
+}
+
+/* stage functions (host pointers; c/qwen_tts.h:483-502) */
+void qwen_tts_talker_prefill(qwen_tts_ctx_t *ctx, const float *input_embeds, int seq_len);
+void qwen_tts_talker_forward(qwen_tts_ctx_t *ctx, const float *input_embed, float *logits);
+void qwen_tts_subtalker_generate(qwen_tts_ctx_t *ctx, const float *talker_hidden, int first_code, int *out_codes);
+float *qwen_tts_codec_decode(qwen_tts_ctx_t *ctx, const int *codes, int time_steps, int *out_samples);
+
+/* post-final-norm hidden of the last talker token (the reference's ctx->tk_x) */
+int qwen_tts_talker_hidden(qwen_tts_ctx_t *ctx, float *out);
+
+/* ---- MI355X additions ---- */
+/* HIP device used by the next qwen_tts_load (default: $QWEN_TTS_HIP_DEVICE or 0) */
+void qwen_tts_set_device(int device);
+/* nb utterances in lock-step frames on this ctx's GPU (weights read once per
+ * frame for all of them).  out_audio[i] malloc'd (caller frees), out_samples[i]
+ * set; returns 0 when every utterance produced audio. */
+int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
+                            const char *const *languages, float **out_audio, int *out_samples);
+/* codes of the last generate() (slot 0): copies up to max_frames rows of
+ * num_code_groups ints, returns the frame count */
+int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
+
+extern int qwen_tts_verbose;
+
+#endif /* QWEN_TTS_H */

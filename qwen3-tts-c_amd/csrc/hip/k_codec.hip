@@ -1,0 +1,686 @@
+// k_codec.hip - 12 Hz codec decoder / vocoder on gfx950 (c/qwen_tts_codec.c).
+//
+// Every dense contraction of the codec -- causal conv1d (K.c:659-871),
+// transposed conv1d (K.c:873-972), the 1x1 RVQ/ConvNeXt projections and the
+// sliding-window transformer's linears (Cd.c:267-522) -- runs through ONE
+// implicit-GEMM kernel on the fp32-input MFMA v_mfma_f32_32x32x2_f32 (exact
+// fp32 products, f32 accumulate; the codec weights are f32 like the
+// reference's).  The operand loaders do the im2col / transposed-conv gather
+// and apply SnakeBeta (K.c:251-311) to the input channels on the fly; the
+// epilogues fuse bias, GELU(tanh), SiLU*up, LayerScale+residual, gamma,
+// transposed stores and the ResUnit residual (Cd.c:549-575).
+//
+// Tile 64x64 per 256-thread workgroup (2x2 waves of 32x32), K step 16 staged
+// through LDS with +1 padding (conflict-free column reads).
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "qtts_codec.h"
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int BM = 64, BN = 64, BK = 16;
+
+__device__ __forceinline__ float snake1(float x, float a, float ib) {
+    const float s = sinf(x * a);
+    return x + ib * s * s;
+}
+
+__device__ __forceinline__ float loadB(const XGemm &g, int k, int n) {
+    if (k >= g.K || n >= g.N) return 0.f;
+    if (g.bmode == XB_WT) return g.B[(size_t)n * g.ldb + k];
+    int ic, t;
+    if (g.bmode == XB_CONV) {
+        ic = k / g.Kw;
+        const int tap = k - ic * g.Kw;
+        t = n + tap * g.dil - g.pad;
+    } else {  // XB_TCONV: k = ic*ntap + j, input position q - j
+        const int ntap = g.Kw / g.stride;
+        ic = k / ntap;
+        t = n - (k - ic * ntap);
+    }
+    if (t < 0 || t >= g.L) return 0.f;
+    const float x = g.B[(size_t)ic * g.ldb + t];
+    return g.sa ? snake1(x, g.sa[ic], g.sb[ic]) : x;
+}
+
+__device__ __forceinline__ float loadA(const XGemm &g, int m, int k) {
+    if (m >= g.M || k >= g.K) return 0.f;
+    if (g.amode == XA_ROWS) return g.A[(size_t)m * g.lda + k];
+    if (g.amode == XA_TRANS) return g.A[(size_t)k * g.lda + m];
+    const int ntap = g.Kw / g.stride;  // tconv weight [ci][co][Kw], k = ic*ntap + j
+    const int ic = k / ntap, j = k - ic * ntap;
+    return g.A[((size_t)ic * g.co + m) * g.Kw + g.phase + j * g.stride];
+}
+
+__device__ __forceinline__ float gelu_tanh(float v) {
+    return 0.5f * v * (1.0f + tanhf(0.7978845608028654f * (v + 0.044715f * v * v * v)));
+}
+
+__global__ __launch_bounds__(256) void k_xgemm(XGemm g) {
+    __shared__ float As[BM][BK + 1];
+    __shared__ float Bs[BN][BK + 1];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const bool a_k_fast = g.amode == XA_ROWS;   // consecutive threads along k
+    const bool b_k_fast = g.bmode == XB_WT;
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+#pragma unroll
+        for (int j = 0; j < (BM * BK) / 256; ++j) {
+            const int e = tid + 256 * j;
+            int mi, ki;
+            if (a_k_fast) { mi = e / BK; ki = e % BK; }
+            else { ki = e / BM; mi = e % BM; }
+            As[mi][ki] = loadA(g, m0 + mi, k0 + ki);
+        }
+#pragma unroll
+        for (int j = 0; j < (BN * BK) / 256; ++j) {
+            const int e = tid + 256 * j;
+            int ni, ki;
+            if (b_k_fast) { ni = e / BK; ki = e % BK; }
+            else { ki = e / BN; ni = e % BN; }
+            Bs[ni][ki] = loadB(g, k0 + ki, n0 + ni);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 2) {
+            const float a = As[wm + (lane & 31)][kk + (lane >> 5)];
+            const float b = Bs[wn + (lane & 31)][kk + (lane >> 5)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + (lane & 31);
+        if (m >= g.M || n >= g.N) continue;
+        const float v = acc[r];
+        switch (g.emode) {
+            case XE_STORE: g.C[(size_t)m * g.ldc + n] = v; break;
+            case XE_BIAS_N: g.C[(size_t)m * g.ldc + n] = v + g.bias[n]; break;
+            case XE_BIAS_N_GELU: g.C[(size_t)m * g.ldc + n] = gelu_tanh(v + g.bias[n]); break;
+            case XE_SILU_MUL: {
+                const float gt = g.aux[(size_t)m * g.ldaux + n];
+                g.C[(size_t)m * g.ldc + n] = (gt / (1.0f + expf(-gt))) * v;
+                break;
+            }
+            case XE_SCALE_RESID_N: g.C[(size_t)m * g.ldc + n] += v * g.vec[n]; break;
+            case XE_BIAS_T: g.C[(size_t)n * g.ldc + m] = v + g.bias[n]; break;
+            case XE_BIAS_GAMMA_RES_T:
+                g.C[(size_t)n * g.ldc + m] = (v + g.bias[n]) * g.vec[n] + g.res[(size_t)n * g.ldres + m];
+                break;
+            case XE_BIAS_M: {
+                float y = v + (g.bias ? g.bias[m] : 0.f);
+                if (g.stride > 1 || g.phase > 0) g.C[(size_t)m * g.ldc + (size_t)n * g.stride + g.phase] = y;
+                else g.C[(size_t)m * g.ldc + n] = y;
+                break;
+            }
+            case XE_BIAS_M_RES:
+                g.C[(size_t)m * g.ldc + n] = v + g.bias[m] + g.res[(size_t)m * g.ldres + n];
+                break;
+            case XE_BIAS_M_SNAKE:
+                g.C[(size_t)m * g.ldc + n] = snake1(v + g.bias[m], g.ea[m], g.eb[m]);
+                break;
+        }
+    }
+}
+
+// RVQ gather-sums (Cd.c:166-227), bit-identical order: sem = 0 + e0[c0];
+// ac = 0 + e1[c1] + ... + e15[c15]; out-of-range codes -> 0
+__global__ void k_rvq_sum(const int *codes, int T, int Q, int CB, int vq, const float *cb, float *ss, float *as) {
+#pragma clang fp contract(off)
+    const int t = blockIdx.x, k = threadIdx.x;
+    if (k >= vq) return;
+    float s = 0.f, a = 0.f;
+    for (int q = 0; q < Q; ++q) {
+        int c = codes[(size_t)t * Q + q];
+        if (c < 0 || c >= CB) c = 0;
+        const float e = cb[((size_t)q * CB + c) * vq + k];
+        if (q == 0) s += e;
+        else a += e;
+    }
+    ss[(size_t)k * T + t] = s;
+    as[(size_t)k * T + t] = a;
+}
+// output projections (1x1, no bias) summed (Cd.c:178-255), sequential sums
+__global__ void k_rvq_proj(const float *ps, const float *pa, const float *ss, const float *as, int vq, int half, int T,
+                           float *out) {
+#pragma clang fp contract(off)
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= half * T) return;
+    const int o = idx / T, t = idx - o * T;
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = 0; k < vq; ++k) s1 += ps[(size_t)o * vq + k] * ss[(size_t)k * T + t];
+    for (int k = 0; k < vq; ++k) s2 += pa[(size_t)o * vq + k] * as[(size_t)k * T + t];
+    out[idx] = s1 + s2;
+}
+// depthwise causal conv k=7 (ConvNeXt dwconv), reference order b + sum_k
+__global__ void k_dwconv(const float *x, const float *w, const float *b, int C, int L, int K, float *y) {
+#pragma clang fp contract(off)
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)C * L) return;
+    const int c = (int)(idx / L), t = (int)(idx - (size_t)c * L);
+    float acc = b ? b[c] : 0.f;
+    for (int k = 0; k < K; ++k) {
+        const int ti = t - (K - 1) + k;
+        if (ti >= 0) acc += w[(size_t)c * K + k] * x[(size_t)c * L + ti];
+    }
+    y[idx] = acc;
+}
+// LayerNorm over channels of a channel-major [C][L] tensor, written time-major [L][C] (Cd.c:480-488)
+__global__ __launch_bounds__(256) void k_ln_t(const float *x, int C, int L, const float *w, const float *b, float eps,
+                                              float *y) {
+    __shared__ float red[8];
+    const int t = blockIdx.x;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) s += x[(size_t)c * L + t];
+    const float mean = block_sum256(s, red) / (float)C;
+    float v = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) { const float d = x[(size_t)c * L + t] - mean; v += d * d; }
+    const float var = block_sum256(v, red + 4) / (float)C;
+    const float inv = div_rn(1.0f, sqrt_rn(var + eps));
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float o = (x[(size_t)c * L + t] - mean) * inv;
+        o *= w[c];
+        y[(size_t)t * C + c] = o + b[c];
+    }
+}
+// RMSNorm rows [T][D] -> out rows (K.c:27-39)
+__global__ __launch_bounds__(256) void k_rms_rows(const float *x, int D, const float *w, float eps, float *y) {
+    __shared__ float red[4];
+    const int t = blockIdx.x;
+    const float *xr = x + (size_t)t * D;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < D; c += 256) s += xr[c] * xr[c];
+    const float inv = rms_inv(block_sum256(s, red), D, eps);
+    for (int c = threadIdx.x; c < D; c += 256) y[(size_t)t * D + c] = xr[c] * inv * w[c];
+}
+// rotate-half RoPE in place on rows [T][nh*hd] (K.c:564-587)
+__global__ void k_rope_rows(float *x, int ld, int nh, int hd, const float *cs, const float *sn) {
+    const int t = blockIdx.x;
+    const int half = hd / 2;
+    for (int i = threadIdx.x; i < nh * half; i += blockDim.x) {
+        const int h = i / half, e = i - h * half;
+        float *q = x + (size_t)t * ld + h * hd;
+        const float a = q[e], bb = q[e + half];
+        q[e] = a * cs[(size_t)t * hd + e] - bb * sn[(size_t)t * hd + e];
+        q[e + half] = bb * cs[(size_t)t * hd + e + half] + a * sn[(size_t)t * hd + e + half];
+    }
+}
+__global__ void k_snake(const float *x, const float *a, const float *ib, int C, int L, float *y) {
+#pragma clang fp contract(off)
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)C * L) return;
+    const int c = (int)(idx / L);
+    const float s = sinf(x[idx] * a[c]);
+    y[idx] = x[idx] + ib[c] * s * s;
+}
+__global__ void k_clamp(float *x, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        float v = x[i];
+        if (v < -1.0f) v = -1.0f;
+        if (v > 1.0f) v = 1.0f;
+        x[i] = v;
+    }
+}
+__global__ void k_expf_glibc(const float *x, float *y, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) y[i] = expf_glibc(x[i]);
+}
+__global__ void k_iota(int *p, int n, int zero) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = zero ? 0 : i;
+}
+
+}  // namespace
+
+int qtts_xgemm(const XGemm &g, hipStream_t st) {
+    if (g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
+    hipLaunchKernelGGL(k_xgemm, grid, dim3(256), 0, st, g);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ===================================================================== model
+static float *cw(CodecModel *m, const std::string &n) {
+    auto it = m->w.find(n);
+    return it == m->w.end() ? nullptr : it->second;
+}
+
+void codec_init(CodecModel *m, const qtts_dims_t *d, hipStream_t st) {
+    m->d = *d;
+    m->st = st;
+}
+
+void codec_free_state(CodecModel *m) {
+    for (void *p : m->scratch) hipFree(p);
+    m->scratch.clear();
+    m->scratch_bytes = 0;
+    m->buf_elems = 0;
+    m->t_cap = 0;
+    m->rope_cap = 0;
+    m->bufA = m->bufB = m->bufC = m->bufD = nullptr;
+}
+
+void codec_destroy(CodecModel *m) {
+    codec_free_state(m);
+    for (auto &kv : m->w) hipFree(kv.second);
+    m->w.clear();
+    if (m->cb) hipFree(m->cb);
+    m->cb = nullptr;
+}
+
+size_t codec_weight_bytes(const CodecModel *m) { return m->wbytes; }
+
+static float f32_of(const void *h, int dtype, size_t i) {
+    if (dtype == 0) return ((const float *)h)[i];
+    uint16_t v = ((const uint16_t *)h)[i];
+    if (dtype == 1) {
+        uint32_t u = (uint32_t)v << 16;
+        float f;
+        memcpy(&f, &u, 4);
+        return f;
+    }
+    _Float16 x;
+    memcpy(&x, &v, 2);
+    return (float)x;
+}
+
+static int build_codebook(CodecModel *m, int q) {
+    const qtts_dims_t &d = m->d;
+    std::string u, e;
+    if (q == 0) {
+        u = "decoder.quantizer.rvq_first.vq.layers.0._codebook.cluster_usage";
+        e = "decoder.quantizer.rvq_first.vq.layers.0._codebook.embedding_sum";
+    } else {
+        u = "decoder.quantizer.rvq_rest.vq.layers." + std::to_string(q - 1) + "._codebook.cluster_usage";
+        e = "decoder.quantizer.rvq_rest.vq.layers." + std::to_string(q - 1) + "._codebook.embedding_sum";
+    }
+    if (!m->host_keep.count(u) || !m->host_keep.count(e)) return 0;  // wait for both
+    const int CB = d.ccb, vq = d.ccbdim / 2;
+    std::vector<float> &us = m->host_keep[u], &es = m->host_keep[e];
+    if ((int)us.size() != CB || (int)es.size() != CB * vq) {
+        fprintf(stderr, "qtts codec: codebook %d has unexpected shape\n", q);
+        return -1;
+    }
+    std::vector<float> cb((size_t)CB * vq);
+    for (int c = 0; c < CB; ++c) {  // Q.c:584-592
+        float usage = us[c];
+        if (usage < 1e-5f) usage = 1e-5f;
+        const float inv = 1.0f / usage;
+        for (int k = 0; k < vq; ++k) cb[(size_t)c * vq + k] = es[(size_t)c * vq + k] * inv;
+    }
+    if (!m->cb) {
+        size_t bytes = (size_t)d.cq * CB * vq * 4;
+        if (hipMalloc(&m->cb, bytes) != hipSuccess) return -1;
+        m->wbytes += bytes;
+    }
+    if (hipMemcpy(m->cb + (size_t)q * CB * vq, cb.data(), cb.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return -1;
+    m->host_keep.erase(u);
+    m->host_keep.erase(e);
+    m->w["__cb" + std::to_string(q)] = nullptr;  // marker
+    return 0;
+}
+
+int codec_put_tensor(CodecModel *m, const std::string &name, const void *host, int dtype, const int64_t *shape,
+                     int ndim, size_t n) {
+    std::vector<float> f(n);
+    for (size_t i = 0; i < n; ++i) f[i] = f32_of(host, dtype, i);
+    const bool is_usage = name.find("._codebook.cluster_usage") != std::string::npos;
+    const bool is_esum = name.find("._codebook.embedding_sum") != std::string::npos;
+    if (is_usage || is_esum) {
+        m->host_keep[name] = std::move(f);
+        const std::string pre1 = "decoder.quantizer.rvq_first.vq.layers.0.";
+        const std::string pre2 = "decoder.quantizer.rvq_rest.vq.layers.";
+        int q = -1;
+        if (name.compare(0, pre1.size(), pre1) == 0) q = 0;
+        else if (name.compare(0, pre2.size(), pre2) == 0) q = 1 + atoi(name.c_str() + pre2.size());
+        if (q < 0 || q >= m->d.cq) return 0;
+        return build_codebook(m, q);
+    }
+    // SnakeBeta parameters pre-exponentiated with libm (Q.c:596-602)
+    const size_t L = name.size();
+    if (L > 6 && (name.compare(L - 6, 6, ".alpha") == 0)) {
+        for (auto &v : f) v = expf(v);
+    } else if (L > 5 && name.compare(L - 5, 5, ".beta") == 0) {
+        for (auto &v : f) v = 1.0f / (expf(v) + 1e-9f);
+    }
+    float *p = nullptr;
+    if (hipMalloc(&p, n * 4) != hipSuccess) return -1;
+    m->wbytes += n * 4;
+    if (hipMemcpy(p, f.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    if (m->w.count(name) && m->w[name]) hipFree(m->w[name]);
+    m->w[name] = p;
+    m->shape[name] = std::vector<int64_t>(shape, shape + ndim);
+    return 0;
+}
+
+int codec_finalize(CodecModel *m) {
+    const qtts_dims_t &d = m->d;
+    std::vector<std::string> need = {"decoder.quantizer.rvq_first.output_proj.weight",
+                                     "decoder.quantizer.rvq_rest.output_proj.weight", "decoder.pre_conv.conv.weight",
+                                     "decoder.pre_transformer.input_proj.weight",
+                                     "decoder.pre_transformer.output_proj.weight", "decoder.decoder.0.conv.weight",
+                                     "decoder.decoder.6.conv.weight"};
+    for (int q = 0; q < d.cq; ++q) need.push_back("__cb" + std::to_string(q));
+    for (int l = 0; l < d.clayers; ++l)
+        for (const char *s : {"input_layernorm.weight", "post_attention_layernorm.weight", "self_attn.q_proj.weight",
+                              "self_attn.k_proj.weight", "self_attn.v_proj.weight", "self_attn.o_proj.weight",
+                              "mlp.gate_proj.weight", "mlp.up_proj.weight", "mlp.down_proj.weight"})
+            need.push_back("decoder.pre_transformer.layers." + std::to_string(l) + "." + s);
+    for (int s = 0; s < 2; ++s)
+        for (const char *t : {"0.conv.weight", "0.conv.bias", "1.dwconv.conv.weight", "1.norm.weight", "1.norm.bias",
+                              "1.pwconv1.weight", "1.pwconv1.bias", "1.pwconv2.weight", "1.pwconv2.bias", "1.gamma"})
+            need.push_back("decoder.upsample." + std::to_string(s) + "." + t);
+    for (int b = 0; b < 4; ++b) {
+        const std::string p = "decoder.decoder." + std::to_string(b + 1) + ".block.";
+        for (const char *t : {"0.alpha", "0.beta", "1.conv.weight", "1.conv.bias"}) need.push_back(p + t);
+        for (int r = 0; r < 3; ++r)
+            for (const char *t : {"act1.alpha", "act1.beta", "conv1.conv.weight", "conv1.conv.bias", "act2.alpha",
+                                  "act2.beta", "conv2.conv.weight", "conv2.conv.bias"})
+                need.push_back(p + std::to_string(r + 2) + "." + t);
+    }
+    for (auto &n : need)
+        if (!m->w.count(n)) {
+            fprintf(stderr, "Error: codec decoder is not fully loaded (missing %s)\n", n.c_str());
+            return -1;
+        }
+    if (d.clat / 2 != d.ccbdim) {
+        fprintf(stderr, "Error: codec requires codebook_dim == latent_dim/2 (got %d, %d)\n", d.ccbdim, d.clat);
+        return -1;
+    }
+    return 0;
+}
+
+static void *scratch_alloc(CodecModel *m, size_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    m->scratch.push_back(p);
+    m->scratch_bytes += bytes;
+    return p;
+}
+
+static int ensure_codec_state(CodecModel *m, int T) {
+    const qtts_dims_t &d = m->d;
+    if (T <= m->t_cap) return 0;
+    codec_free_state(m);
+    const int cap = T < 64 ? 64 : T;
+    // largest channel-major intermediate over the decoder
+    size_t L = (size_t)cap * d.ratios[0] * d.ratios[1];
+    size_t mx = (size_t)d.clat * L * 4;  // ConvNeXt pw1 [L][4C]
+    if ((size_t)d.cdec * L > mx) mx = (size_t)d.cdec * L;
+    int C = d.cdec;
+    for (int b = 0; b < 4; ++b) {
+        L *= d.rates[b];
+        C /= 2;
+        if ((size_t)C * L > mx) mx = (size_t)C * L;
+    }
+    const size_t lat_t = (size_t)d.clat * cap;
+    if (lat_t > mx) mx = lat_t;
+    m->buf_elems = mx;
+    m->bufA = (float *)scratch_alloc(m, mx * 4);
+    m->bufB = (float *)scratch_alloc(m, mx * 4);
+    m->bufC = (float *)scratch_alloc(m, mx * 4);
+    m->bufD = (float *)scratch_alloc(m, mx * 4);
+    const int hid = d.chid, kvd = d.ckv * (d.chid / d.cheads);
+    m->tx = (float *)scratch_alloc(m, (size_t)cap * hid * 4);
+    m->txn = (float *)scratch_alloc(m, (size_t)cap * hid * 4);
+    m->tq = (float *)scratch_alloc(m, (size_t)cap * (hid + 2 * kvd) * 4);
+    m->tatt = (float *)scratch_alloc(m, (size_t)cap * hid * 4);
+    m->tg = (float *)scratch_alloc(m, (size_t)cap * d.cinter * 4);
+    m->tu = (float *)scratch_alloc(m, (size_t)cap * d.cinter * 4);
+    m->codes_tmp = (int *)scratch_alloc(m, (size_t)cap * 2 * 4);  // [0..cap) positions, [cap..2cap) zeros
+    if (!m->bufA || !m->bufB || !m->bufC || !m->bufD || !m->tx || !m->txn || !m->tq || !m->tatt || !m->tg || !m->tu ||
+        !m->codes_tmp)
+        return -1;
+    hipLaunchKernelGGL(k_iota, dim3((cap + 255) / 256), dim3(256), 0, m->st, m->codes_tmp, cap, 0);
+    hipLaunchKernelGGL(k_iota, dim3((cap + 255) / 256), dim3(256), 0, m->st, m->codes_tmp + cap, cap, 1);
+    // RoPE table (theta fixed at 1e4 in the reference, Cd.c:309; head_dim = hidden/heads, Cd.c:275)
+    const int hd = d.chid / d.cheads, half = hd / 2;
+    std::vector<float> c((size_t)cap * hd), s((size_t)cap * hd);
+    for (int p = 0; p < cap; ++p)
+        for (int i = 0; i < half; ++i) {
+            float freq = 1.0f / powf(10000.0f, (float)(2 * i) / (float)hd);
+            float ang = (float)p * freq;
+            c[(size_t)p * hd + i] = c[(size_t)p * hd + i + half] = cosf(ang);
+            s[(size_t)p * hd + i] = s[(size_t)p * hd + i + half] = sinf(ang);
+        }
+    m->rope_cos = (float *)scratch_alloc(m, c.size() * 4);
+    m->rope_sin = (float *)scratch_alloc(m, s.size() * 4);
+    if (!m->rope_cos || !m->rope_sin) return -1;
+    if (hipMemcpy(m->rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    if (hipMemcpy(m->rope_sin, s.data(), s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    m->t_cap = cap;
+    return 0;
+}
+
+#define KCK(x) do { if ((x) != 0) return -1; } while (0)
+
+static XGemm lin(const float *A, int M, int K, const float *W, int N, float *C, int emode) {
+    XGemm g;
+    g.M = M; g.N = N; g.K = K; g.amode = XA_ROWS; g.A = A; g.lda = K; g.bmode = XB_WT; g.B = W; g.ldb = K;
+    g.C = C; g.ldc = N; g.emode = emode;
+    return g;
+}
+
+// causal conv as implicit GEMM: out[co][L] = W[co][ci*K] . im2col(snake?(x))
+static int conv(CodecModel *m, const float *x, int ci, int L, const std::string &wn, const std::string &bn, int co,
+                int K, int dil, float *out, int emode, const float *sa, const float *sb, const float *res,
+                const float *ea = nullptr, const float *eb = nullptr) {
+    XGemm g;
+    g.M = co; g.N = L; g.K = ci * K;
+    g.amode = XA_ROWS; g.A = cw(m, wn); g.lda = ci * K;
+    g.bmode = XB_CONV; g.B = x; g.ldb = L; g.Kw = K; g.dil = dil; g.pad = (K - 1) * dil; g.L = L;
+    g.sa = sa; g.sb = sb;
+    g.C = out; g.ldc = L; g.emode = emode; g.bias = bn.empty() ? nullptr : cw(m, bn); g.res = res; g.ldres = L;
+    g.ea = ea; g.eb = eb;
+    if (!g.A) return -1;
+    return qtts_xgemm(g, m->st);
+}
+
+// transposed conv (stride s, kernel Kw = s * ntap) as s phase GEMMs
+static int tconv(CodecModel *m, const float *x, int ci, int L, const float *w, const float *bias, int co, int Kw,
+                 int s, float *out, const float *sa, const float *sb, hipStream_t st) {
+    for (int ph = 0; ph < s; ++ph) {
+        XGemm g;
+        g.M = co; g.N = L; g.K = ci * (Kw / s);
+        g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s; g.phase = ph;
+        g.bmode = XB_TCONV; g.B = x; g.ldb = L; g.L = L; g.sa = sa; g.sb = sb;
+        g.C = out; g.ldc = L * s; g.emode = XE_BIAS_M; g.bias = bias;
+        KCK(qtts_xgemm(g, st));
+    }
+    return 0;
+}
+
+static int codec_transformer(CodecModel *m, const float *pc /*[lat][T]*/, int T, float *out /*[lat][T]*/) {
+    const qtts_dims_t &d = m->d;
+    const int lat = d.clat, hid = d.chid, nh = d.cheads, nkv = d.ckv, hd = hid / nh, kvd = nkv * hd, I = d.cinter;
+    hipStream_t st = m->st;
+    const std::string P = "decoder.pre_transformer.";
+    XGemm g;
+    g.M = T; g.N = hid; g.K = lat; g.amode = XA_TRANS; g.A = pc; g.lda = T; g.bmode = XB_WT;
+    g.B = cw(m, P + "input_proj.weight"); g.ldb = lat; g.C = m->tx; g.ldc = hid;
+    g.bias = cw(m, P + "input_proj.bias");
+    g.emode = g.bias ? XE_BIAS_N : XE_STORE;
+    KCK(qtts_xgemm(g, st));
+    float *q = m->tq, *k = m->tq + (size_t)T * hid, *v = k + (size_t)T * kvd;
+    for (int l = 0; l < d.clayers; ++l) {
+        const std::string p = P + "layers." + std::to_string(l) + ".";
+        hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, m->tx, hid, cw(m, p + "input_layernorm.weight"),
+                           d.ceps, m->txn);
+        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "self_attn.q_proj.weight"), hid, q, XE_STORE), st));
+        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "self_attn.k_proj.weight"), kvd, k, XE_STORE), st));
+        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "self_attn.v_proj.weight"), kvd, v, XE_STORE), st));
+        hipLaunchKernelGGL(k_rope_rows, dim3(T), dim3(256), 0, st, q, hid, nh, hd, m->rope_cos, m->rope_sin);
+        hipLaunchKernelGGL(k_rope_rows, dim3(T), dim3(256), 0, st, k, kvd, nkv, hd, m->rope_cos, m->rope_sin);
+        AttnArgs a;
+        a.mode = 1; a.qkv = q; a.ld_qkv = hid; a.kc = k; a.vc = v; a.S = T; a.pos = m->codes_tmp;
+        a.row_b = m->codes_tmp + m->t_cap; a.NH = nh; a.KV = nkv; a.HD = hd; a.out = m->tatt; a.ld_out = hid;
+        a.nrows = T; a.win = d.cwin;
+        KCK(qtts_attention(a, st));
+        const float *ls1 = cw(m, p + "self_attn_layer_scale.scale");
+        XGemm o = lin(m->tatt, T, hid, cw(m, p + "self_attn.o_proj.weight"), hid, m->tx, XE_SCALE_RESID_N);
+        o.vec = ls1;
+        if (!ls1) return -1;
+        KCK(qtts_xgemm(o, st));
+        hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, m->tx, hid,
+                           cw(m, p + "post_attention_layernorm.weight"), d.ceps, m->txn);
+        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "mlp.gate_proj.weight"), I, m->tg, XE_STORE), st));
+        XGemm u = lin(m->txn, T, hid, cw(m, p + "mlp.up_proj.weight"), I, m->tu, XE_SILU_MUL);
+        u.aux = m->tg; u.ldaux = I;
+        KCK(qtts_xgemm(u, st));
+        const float *ls2 = cw(m, p + "mlp_layer_scale.scale");
+        XGemm dn = lin(m->tu, T, I, cw(m, p + "mlp.down_proj.weight"), hid, m->tx, XE_SCALE_RESID_N);
+        dn.vec = ls2;
+        if (!ls2) return -1;
+        KCK(qtts_xgemm(dn, st));
+    }
+    const float *fn = cw(m, P + "norm.weight");
+    const float *xin = m->tx;
+    if (fn) {
+        hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, m->tx, hid, fn, d.ceps, m->txn);
+        xin = m->txn;
+    }
+    XGemm og = lin(xin, T, hid, cw(m, P + "output_proj.weight"), lat, out, XE_BIAS_T);
+    og.bias = cw(m, P + "output_proj.bias");
+    og.ldc = T;
+    if (!og.bias) return -1;
+    return qtts_xgemm(og, st);
+}
+
+float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
+    const qtts_dims_t &d = m->d;
+    if (out_samples) *out_samples = 0;
+    if (ensure_codec_state(m, T)) return nullptr;
+    hipStream_t st = m->st;
+    const int lat = d.clat, vq = d.ccbdim / 2, half = lat / 2;
+    float *A = m->bufA, *B = m->bufB, *Cb = m->bufC, *D = m->bufD;
+#define DCK(x) do { if ((x) != 0) { fprintf(stderr, "qtts codec: stage failed at %s:%d\n", __FILE__, __LINE__); return nullptr; } } while (0)
+    // 1. RVQ dequantise -> A [half][T]
+    hipLaunchKernelGGL(k_rvq_sum, dim3(T), dim3(vq < 64 ? 64 : (vq + 63) / 64 * 64), 0, st, codes, T, d.cq, d.ccb, vq,
+                       m->cb, B, Cb);
+    hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 255) / 256), dim3(256), 0, st,
+                       cw(m, "decoder.quantizer.rvq_first.output_proj.weight"),
+                       cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), B, Cb, vq, half, T, A);
+    // 2. pre-conv k=3 -> B [lat][T]
+    DCK(conv(m, A, d.ccbdim, T, "decoder.pre_conv.conv.weight", "decoder.pre_conv.conv.bias", lat, 3, 1, B, XE_BIAS_M,
+             nullptr, nullptr, nullptr));
+    // 3. transformer -> A [lat][T]
+    DCK(codec_transformer(m, B, T, A));
+    // 4. upsample: transposed conv + ConvNeXt, x2
+    int L = T;
+    float *cur = A;
+    for (int s = 0; s < 2; ++s) {
+        const int f = d.ratios[s];
+        const std::string p = "decoder.upsample." + std::to_string(s) + ".";
+        float *up = cur == A ? B : A;
+        DCK(tconv(m, cur, lat, L, cw(m, p + "0.conv.weight"), cw(m, p + "0.conv.bias"), lat, f, f, up, nullptr, nullptr,
+                  st));
+        L *= f;
+        cur = up;
+        // ConvNeXt: dwconv -> LN (time-major) -> pw1+GELU -> pw2*gamma (+res, channel-major)
+        hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)lat * L + 255) / 256)), dim3(256), 0, st, cur,
+                           cw(m, p + "1.dwconv.conv.weight"), cw(m, p + "1.dwconv.conv.bias"), lat, L, 7, Cb);
+        hipLaunchKernelGGL(k_ln_t, dim3(L), dim3(256), 0, st, Cb, lat, L, cw(m, p + "1.norm.weight"),
+                           cw(m, p + "1.norm.bias"), 1e-6f, D);
+        XGemm g1 = lin(D, L, lat, cw(m, p + "1.pwconv1.weight"), 4 * lat, Cb, XE_BIAS_N_GELU);
+        g1.bias = cw(m, p + "1.pwconv1.bias");
+        DCK(qtts_xgemm(g1, st));
+        XGemm g2 = lin(Cb, L, 4 * lat, cw(m, p + "1.pwconv2.weight"), lat, cur, XE_BIAS_GAMMA_RES_T);
+        g2.bias = cw(m, p + "1.pwconv2.bias");
+        g2.vec = cw(m, p + "1.gamma");
+        g2.res = cur; g2.ldres = L; g2.ldc = L;
+        DCK(qtts_xgemm(g2, st));
+    }
+    // 5. vocoder
+    float *voc = cur == A ? B : A;
+    DCK(conv(m, cur, lat, L, "decoder.decoder.0.conv.weight", "decoder.decoder.0.conv.bias", d.cdec, 7, 1, voc,
+             XE_BIAS_M, nullptr, nullptr, nullptr));
+    int C = d.cdec;
+    static const int dil[3] = {1, 3, 9};
+    for (int b = 0; b < 4; ++b) {
+        const int r = d.rates[b], co = C / 2;
+        const std::string p = "decoder.decoder." + std::to_string(b + 1) + ".block.";
+        float *nx = voc == A ? B : A;
+        DCK(tconv(m, voc, C, L, cw(m, p + "1.conv.weight"), cw(m, p + "1.conv.bias"), co, 2 * r, r, nx,
+                  cw(m, p + "0.alpha"), cw(m, p + "0.beta"), st));
+        L *= r;
+        C = co;
+        voc = nx;
+        for (int u = 0; u < 3; ++u) {
+            const std::string q = p + std::to_string(u + 2) + ".";
+            // conv1(snake1(x)) -> snake2 fused in the epilogue -> Cb
+            DCK(conv(m, voc, C, L, q + "conv1.conv.weight", q + "conv1.conv.bias", C, 7, dil[u], Cb, XE_BIAS_M_SNAKE,
+                     cw(m, q + "act1.alpha"), cw(m, q + "act1.beta"), nullptr, cw(m, q + "act2.alpha"),
+                     cw(m, q + "act2.beta")));
+            // conv2 (k=1) + residual, in place on x
+            DCK(conv(m, Cb, C, L, q + "conv2.conv.weight", q + "conv2.conv.bias", C, 1, 1, voc, XE_BIAS_M_RES, nullptr,
+                     nullptr, voc));
+        }
+    }
+    // final SnakeBeta + conv -> 1 channel, clamp
+    float *wav = voc == A ? B : A;
+    DCK(conv(m, voc, C, L, "decoder.decoder.6.conv.weight", "decoder.decoder.6.conv.bias", 1, 7, 1, wav, XE_BIAS_M,
+             cw(m, "decoder.decoder.5.alpha"), cw(m, "decoder.decoder.5.beta"), nullptr));
+    hipLaunchKernelGGL(k_clamp, dim3((L + 255) / 256), dim3(256), 0, st, wav, L);
+    float *host = (float *)malloc((size_t)L * sizeof(float));
+    if (!host) return nullptr;
+    if (hipMemcpyAsync(host, wav, (size_t)L * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        free(host);
+        return nullptr;
+    }
+    if (out_samples) *out_samples = L;
+    return host;
+#undef DCK
+}
+
+// ===================================================================== kernel-level C-ABI
+extern "C" int qtts_hip_causal_conv1d(float *out, const float *in, const float *w, const float *b, int ci, int co,
+                                      int k, int L, int dilation, int groups, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (groups == ci && ci == co) {
+        if (dilation != 1) return -1;
+        hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)co * L + 255) / 256)), dim3(256), 0, st, in, w, b, co, L,
+                           k, out);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    if (groups != 1) return -1;
+    XGemm g;
+    g.M = co; g.N = L; g.K = ci * k;
+    g.amode = XA_ROWS; g.A = w; g.lda = ci * k;
+    g.bmode = XB_CONV; g.B = in; g.ldb = L; g.Kw = k; g.dil = dilation; g.pad = (k - 1) * dilation; g.L = L;
+    g.C = out; g.ldc = L; g.emode = XE_BIAS_M; g.bias = b;
+    return qtts_xgemm(g, st);
+}
+
+extern "C" int qtts_hip_transposed_conv1d(float *out, const float *in, const float *w, const float *b, int ci, int co,
+                                          int k, int stride, int L, void *stream) {
+    if (k % stride) return -1;
+    CodecModel dummy;
+    return tconv(&dummy, in, ci, L, w, b, co, k, stride, out, nullptr, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int qtts_hip_snake_beta(float *out, const float *x, const float *alpha, const float *inv_beta, int channels,
+                                   int length, void *stream) {
+    hipLaunchKernelGGL(k_snake, dim3((unsigned)(((size_t)channels * length + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, alpha, inv_beta, channels, length, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int qtts_hip_expf_glibc(float *out, const float *in, int n, void *stream) {
+    hipLaunchKernelGGL(k_expf_glibc, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, out, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

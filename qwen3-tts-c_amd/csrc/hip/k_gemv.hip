@@ -1,0 +1,230 @@
+// k_gemv.hip - weight-streaming GEMV / skinny GEMM for gfx950.
+//
+// y[b, r] = epilogue( sum_c W[r, c] * xin[b, c] ),  b < nb <= NB (1..16)
+//   W    bf16 row-major [R, C]  (PyTorch Linear.weight), streamed once from HBM
+//   xin  fp32, staged in LDS by the prologue:
+//          - source: fp32 rows x[b*ldx + c], or a bf16 table row gathered by an
+//            id read from device memory (embedding lookup fused in)
+//          - optional RMSNorm (c/qwen_tts_kernels.c:27-39) with the full-row
+//            statistics computed per workgroup
+//          - optional copy-out (raw or normalised) by workgroup 0
+//   epilogue: store / +bias / +bias then SiLU / residual add (x += acc) /
+//             SwiGLU over interleaved gate|up row quads.
+//
+// Replaces kernel_matvec_bf16 (K.c:95-149), kernel_swiglu_matvec_bf16
+// (K.c:213-233), kernel_matmul_bf16 (K.c:185-207, small M) and the
+// rms_norm / add / silu element-wise passes around them (T.c:142-247).
+//
+// Mapping (64-wide waves): 256 threads = 32 slots of 8 lanes.  A slot owns one
+// row; the row's 64-column blocks are dealt round-robin to KSPLIT slots (each
+// lane loads 16 B = 8 bf16 of a block), so one 8-lane slot reads 128 B
+// contiguous per block and the final reduction is 3 xor-shuffles + a KSPLIT
+// combine through LDS.  KSPLIT is chosen on the host so the grid fills the 256
+// CUs.  Weight loads for the first block group are issued before the prologue
+// so HBM latency overlaps the norm.  Accumulation is fp32 (exact bf16->f32).
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+namespace {
+
+constexpr int U = 8;  // blocks per load group (16 B each per lane)
+
+template <int NB, bool NT>
+__global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
+    const int ksn = a.ksplit, RPW = 32 / ksn;
+    const int rloc = slot % RPW, ks = slot / RPW;
+    const int row0 = blockIdx.x * RPW;
+    const int row = row0 + rloc;
+    const int rowc = row < a.R ? row : a.R - 1;
+    const int C = a.C, CCH = a.cch, nb = a.nb;
+    float *xs = smem;                 // [NB][CCH]
+    float *red = xs + NB * CCH;       // [32][NB]
+    float *inv = red + 32 * NB;       // [NB]
+    float *bred = inv + NB;           // [4]
+
+    const v4u *Wr = reinterpret_cast<const v4u *>(a.W + (size_t)rowc * C) + sub;
+    const int nblk = CCH / 64 / ksn;  // blocks per slot per chunk
+    const int ng = (nblk + U - 1) / U;
+
+    float acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = 0.0f;
+
+    v4u wv[U];
+    auto load_group = [&](int c0, int g) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int j = g * U + u;
+            j = j < nblk ? j : nblk - 1;          // clamp: loads stay unconditional
+            const v4u *p = Wr + ((c0 + 64 * (ks + j * ksn)) >> 3);
+            if constexpr (NT) wv[u] = __builtin_nontemporal_load(p);
+            else wv[u] = *p;
+        }
+    };
+
+    // x source row b (fp32 rows or gathered bf16 table row)
+    auto src_row_id = [&](int b) -> int {
+        const int *p = a.ids + (size_t)b * a.ids_bstride + a.ids_off;
+        if (a.row_sel) p += (size_t)a.row_sel[b] * a.ids_rstride;
+        return *p;
+    };
+
+    // ---- prologue: per-row RMS statistics over the full row ----
+    load_group(0, 0);
+    if (a.norm_w) {
+        for (int b = 0; b < NB; ++b) {
+            float ss = 0.0f;
+            if (b < nb) {
+                if (a.table) {
+                    const bf16_t *t = a.table + (size_t)src_row_id(b) * C;
+                    for (int c = tid; c < C; c += 256) { float v = bf2f(t[c]); ss += v * v; }
+                } else {
+                    const float *xr = a.x + (size_t)b * a.ldx;
+                    for (int c = tid; c < C; c += 256) { float v = xr[c]; ss += v * v; }
+                }
+            }
+            ss = block_sum256(ss, bred);
+            if (tid == 0) inv[b] = rms_inv(ss, C, a.eps);
+        }
+    }
+
+    for (int c0 = 0; c0 < C; c0 += CCH) {
+        if (c0 > 0) load_group(c0, 0);
+        __syncthreads();  // inv[] visible, previous chunk consumed
+        // stage the chunk
+        for (int i = tid; i < NB * CCH; i += 256) {
+            const int b = i / CCH, c = i - b * CCH, cg = c0 + c;
+            float v = 0.0f;
+            if (b < nb) {
+                if (a.table) v = bf2f(a.table[(size_t)src_row_id(b) * C + cg]);
+                else v = a.x[(size_t)b * a.ldx + cg];
+                if (a.xcopy && blockIdx.x == 0 && !a.xcopy_normed) a.xcopy[(size_t)b * a.ldxc + cg] = v;
+                if (a.norm_w) v = v * inv[b] * a.norm_w[cg];
+                if (a.xcopy && blockIdx.x == 0 && a.xcopy_normed) a.xcopy[(size_t)b * a.ldxc + cg] = v;
+            }
+            xs[i] = v;
+        }
+        __syncthreads();
+        for (int g = 0; g < ng; ++g) {
+            v4u cur[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = wv[u];
+            if (g + 1 < ng) load_group(c0, g + 1);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = g * U + u;
+                if (j < nblk) {
+                    float f[8];
+                    unpack8(cur[u], f);
+                    const int cl = 64 * (ks + j * ksn) + 8 * sub;
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) {
+                        const float4 x0 = *reinterpret_cast<const float4 *>(xs + b * CCH + cl);
+                        const float4 x1 = *reinterpret_cast<const float4 *>(xs + b * CCH + cl + 4);
+                        float s = acc[b];
+                        s = fmaf(f[0], x0.x, s); s = fmaf(f[1], x0.y, s);
+                        s = fmaf(f[2], x0.z, s); s = fmaf(f[3], x0.w, s);
+                        s = fmaf(f[4], x1.x, s); s = fmaf(f[5], x1.y, s);
+                        s = fmaf(f[6], x1.z, s); s = fmaf(f[7], x1.w, s);
+                        acc[b] = s;
+                    }
+                }
+            }
+        }
+    }
+
+    // ---- reduction: 8 lanes, then KSPLIT slots through LDS ----
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        float v = acc[b];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        acc[b] = v;
+    }
+    __syncthreads();  // xs no longer read; red may alias nothing but be safe
+    if (sub == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) red[(ks * RPW + rloc) * NB + b] = acc[b];
+    }
+    __syncthreads();
+    // final value per (row, b) -> xs scratch [RPW][NB]
+    for (int t = tid; t < RPW * NB; t += 256) {
+        const int rl = t / NB, b = t - rl * NB;
+        float s = red[rl * NB + b];
+        for (int k = 1; k < ksn; ++k) s += red[(k * RPW + rl) * NB + b];
+        xs[t] = s;
+    }
+    __syncthreads();
+    for (int t = tid; t < RPW * NB; t += 256) {
+        const int rl = t / NB, b = t - rl * NB;
+        const int r = row0 + rl;
+        if (r >= a.R || b >= nb) continue;
+        float v = xs[t];
+        switch (a.epi) {
+            case EPI_STORE: a.y[(size_t)b * a.ldy + r] = v; break;
+            case EPI_BIAS: a.y[(size_t)b * a.ldy + r] = v + a.bias[r]; break;
+            case EPI_BIAS_SILU: {
+                float z = v + a.bias[r];
+                a.y[(size_t)b * a.ldy + r] = z / (1.0f + expf(-z));
+                break;
+            }
+            case EPI_RESID: a.y[(size_t)b * a.ldy + r] += v; break;
+            case EPI_SWIGLU: {
+                if ((r & 7) < 4) {  // gate row; its up row is r + 4 in the same workgroup
+                    const float u = xs[(rl + 4) * NB + b];
+                    const int o = (r >> 3) * 4 + (r & 3);
+                    a.y[(size_t)b * a.ldy + o] = (v / (1.0f + expf(-v))) * u;
+                }
+                break;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+static int pick_ksplit(int R, int C, int epi) {
+    int maxk = C / 64;
+    if (maxk > 32) maxk = 32;
+    if (epi == EPI_SWIGLU && maxk > 4) maxk = 4;
+    int ks = 1;
+    while (ks < maxk && (R + (32 / ks) - 1) / (32 / ks) < 256) ks *= 2;
+    while (ks > 1 && (C / 64) % ks) ks /= 2;
+    return ks;
+}
+
+int qtts_gemv(const GemvArgs &in, hipStream_t st) {
+    GemvArgs a = in;
+    if (a.C % 64 || a.nb < 1 || a.nb > 16 || a.R < 1) {
+        fprintf(stderr, "qtts_gemv: unsupported shape R=%d C=%d nb=%d\n", a.R, a.C, a.nb);
+        return -1;
+    }
+    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi);
+    int NB = a.nb <= 1 ? 1 : a.nb <= 2 ? 2 : a.nb <= 4 ? 4 : a.nb <= 8 ? 8 : 16;
+    const int unit = 64 * a.ksplit;
+    int cch = (8192 / NB) / unit * unit;
+    if (cch < unit) cch = unit;
+    if (cch > a.C) cch = a.C;
+    while (a.C % cch) cch -= unit;
+    a.cch = cch;
+    const int rpw = 32 / a.ksplit;
+    const int grid = (a.R + rpw - 1) / rpw;
+    size_t smem = (size_t)(NB * cch + 32 * NB + NB + 4) * sizeof(float);
+#define QTTS_GEMV_CASE(n)                                                                        \
+    case n:                                                                                      \
+        if (a.nt) hipLaunchKernelGGL((k_gemv<n, true>), dim3(grid), dim3(256), smem, st, a);     \
+        else hipLaunchKernelGGL((k_gemv<n, false>), dim3(grid), dim3(256), smem, st, a);         \
+        break;
+    switch (NB) {
+        QTTS_GEMV_CASE(1)
+        QTTS_GEMV_CASE(2)
+        QTTS_GEMV_CASE(4)
+        QTTS_GEMV_CASE(8)
+        QTTS_GEMV_CASE(16)
+    }
+#undef QTTS_GEMV_CASE
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -1,0 +1,71 @@
+// k_misc.hip - small element-wise kernels around the decode loop.
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+namespace {
+
+// next_embed (c/qwen_tts.c:1345-1363), per element in the reference's order:
+//   0 + codec_emb[code0] + st_emb[0][code1] + ... + st_emb[G-2][code G-1]
+//     + (row < n_trailing ? trailing[row] : tts_pad)
+// so the result is bit-identical to the host loop.  Also advances kv_len for
+// the frame's talker token.
+__global__ __launch_bounds__(256) void k_embed_sum(EmbedSumArgs a) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.y;
+    const int d = blockIdx.x * 256 + threadIdx.x;
+    if (a.stopped && a.stopped[b]) return;
+    const int row = a.cur_row[b];
+    const int *cd = a.codes + (size_t)b * a.codes_bstride + (size_t)row * a.G;
+    if (d < a.H) {
+        float s = 0.0f;
+        s += bf2f(a.codec_emb[(size_t)cd[0] * a.H + d]);
+        for (int g = 1; g < a.G; ++g) s += bf2f(a.st_emb[((size_t)(g - 1) * a.Vs + cd[g]) * a.H + d]);
+        const float *tt = row < a.n_trailing[b] ? a.trailing + ((size_t)b * a.tr_cap + row) * a.H : a.pad;
+        s += tt[d];
+        a.out[(size_t)b * a.H + d] = s;
+    }
+    if (a.advance && blockIdx.x == 0 && threadIdx.x == 0) a.kv_len[b] += 1;
+}
+
+// prompt rows (c/qwen_tts.c:1192-1243): dst = proj_row (+ codec_emb[id])
+__global__ __launch_bounds__(256) void k_prompt(PromptArgs a) {
+#pragma clang fp contract(off)
+    const int e = blockIdx.y;
+    const int *pl = a.plan + 5 * e;
+    const int src = pl[0], cid = pl[1], kind = pl[2], b = pl[3], slot = pl[4];
+    float *dst = kind == 0 ? a.prefill + ((size_t)b * a.p_cap + slot) * a.H
+                           : a.trailing + ((size_t)b * a.tr_cap + slot) * a.H;
+    for (int d = blockIdx.x * 256 + threadIdx.x; d < a.H; d += gridDim.x * 256) {
+        float v = a.proj[(size_t)src * a.H + d];
+        if (cid >= 0) v += bf2f(a.codec_emb[(size_t)cid * a.H + d]);
+        dst[d] = v;
+    }
+}
+
+__global__ void k_copy_rows(float *dst, int ldd, const float *src, int lds, const int *rows, int ncols) {
+    const int r = blockIdx.y;
+    const int sr = rows ? rows[r] : r;
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < ncols; c += gridDim.x * 256)
+        dst[(size_t)r * ldd + c] = src[(size_t)sr * lds + c];
+}
+
+}  // namespace
+
+int qtts_embed_sum(const EmbedSumArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_embed_sum, dim3((a.H + 255) / 256, a.nb), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int qtts_prompt_assemble(const PromptArgs &a, hipStream_t st) {
+    if (a.nplan <= 0) return 0;
+    hipLaunchKernelGGL(k_prompt, dim3((a.H + 255) / 256, a.nplan), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int qtts_copy_rows(float *dst, int ldd, const float *src, int lds, const int *rows, int nrows, int ncols,
+                   hipStream_t st) {
+    if (nrows <= 0) return 0;
+    hipLaunchKernelGGL(k_copy_rows, dim3((ncols + 255) / 256, nrows), dim3(256), 0, st, dst, ldd, src, lds, rows,
+                       ncols);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -1,0 +1,71 @@
+// qtts_codec.h - internal interface of the device codec decoder (C++ only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../../include/qtts_hip.h"
+
+struct CodecModel {
+    qtts_dims_t d{};
+    hipStream_t st = nullptr;
+    std::map<std::string, float *> w;                 // f32 device tensors by checkpoint name
+    std::map<std::string, std::vector<int64_t>> shape;
+    std::map<std::string, std::vector<float>> host_keep;  // usage / esum pending codebook build
+    float *cb = nullptr;                              // [Q][CB][vq] codebooks
+    size_t wbytes = 0;
+    // scratch (grown on demand)
+    std::vector<void *> scratch;
+    size_t scratch_bytes = 0;
+    float *bufA = nullptr, *bufB = nullptr, *bufC = nullptr, *bufD = nullptr;
+    size_t buf_elems = 0;
+    float *tq = nullptr, *tx = nullptr, *txn = nullptr, *tatt = nullptr, *tg = nullptr, *tu = nullptr;
+    float *rope_cos = nullptr, *rope_sin = nullptr;
+    int t_cap = 0, rope_cap = 0;
+    int *codes_tmp = nullptr;
+    float *wav = nullptr;
+};
+
+void codec_init(CodecModel *m, const qtts_dims_t *d, hipStream_t st);
+void codec_destroy(CodecModel *m);
+void codec_free_state(CodecModel *m);
+size_t codec_weight_bytes(const CodecModel *m);
+int codec_put_tensor(CodecModel *m, const std::string &name, const void *host, int dtype, const int64_t *shape,
+                     int ndim, size_t n);
+int codec_finalize(CodecModel *m);
+// codes: device int32 [T][cq] (time-major).  Returns malloc'd host audio.
+float *codec_decode(CodecModel *m, const int *codes_dev, int T, int *out_samples);
+
+// ---- generic fp32 implicit GEMM (exported for the kernel-level C-ABI) ----
+// C(m, n) = sum_k A(m, k) * B(k, n), fp32 products on v_mfma_f32_32x32x2_f32.
+enum { XA_ROWS = 0, XA_TRANS = 1, XA_TCONV_W = 2 };
+enum { XB_WT = 0, XB_CONV = 1, XB_TCONV = 2 };
+enum {
+    XE_STORE = 0,        // C[m][n]
+    XE_BIAS_N,           // + bias[n]
+    XE_BIAS_N_GELU,      // gelu_tanh(acc + bias[n])
+    XE_SILU_MUL,         // silu(aux[m][n]) * acc
+    XE_SCALE_RESID_N,    // C[m][n] += acc * vec[n]
+    XE_BIAS_T,           // out[n][m] = acc + bias[n]
+    XE_BIAS_GAMMA_RES_T, // out[n][m] = (acc + bias[n]) * vec[n] + res[n][m]
+    XE_BIAS_M,           // conv: out[m][n] = acc + bias[m]
+    XE_BIAS_M_RES,       // conv: out[m][n] = acc + bias[m] + res[m][n]
+    XE_BIAS_M_SNAKE,     // conv: out[m][n] = snake(acc + bias[m]) with (alpha, inv_beta)[m]
+};
+struct XGemm {
+    int M = 0, N = 0, K = 0;
+    int amode = XA_ROWS, bmode = XB_WT, emode = XE_STORE;
+    const float *A = nullptr;  int lda = 0;   // rows: A[m*lda+k]; trans: A[k*lda+m]; tconv w: [ci][co][Kw]
+    const float *B = nullptr;  int ldb = 0;   // wt: B[n*ldb+k]; conv/tconv: x[ic*ldb + t]
+    // conv geometry (XB_CONV: k = ic*Kw + tap; XB_TCONV: k = ic*2 + j)
+    int Kw = 1, dil = 1, pad = 0, L = 0, stride = 1, phase = 0, co = 0;
+    const float *sa = nullptr, *sb = nullptr;  // optional SnakeBeta on B's input channels
+    float *C = nullptr; int ldc = 0;          // output (XE_*_T: out[n*ldc + m]); tconv: out[m*ldc + n*stride + phase]
+    const float *bias = nullptr, *vec = nullptr, *aux = nullptr, *res = nullptr;
+    int ldaux = 0, ldres = 0;
+    const float *ea = nullptr, *eb = nullptr;  // epilogue snake params (XE_BIAS_M_SNAKE)
+};
+int qtts_xgemm(const XGemm &g, hipStream_t st);

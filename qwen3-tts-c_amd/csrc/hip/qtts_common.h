@@ -1,0 +1,107 @@
+// qtts_common.h - shared device helpers for the gfx950 kernels (HIP C++).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define QTTS_CHECK(x)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "HIP error %s at %s:%d: %s\n", hipGetErrorName(e_), __FILE__, \
+                    __LINE__, #x);                                                       \
+            return -1;                                                                   \
+        }                                                                                \
+    } while (0)
+
+typedef uint16_t bf16_t;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));  // 16 B = 8 packed bf16
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+// 8 packed bf16 (one 16-B load) -> 8 floats
+__device__ __forceinline__ void unpack8(const v4u &w, float (&f)[8]) {
+    f[0] = __uint_as_float(w.x << 16); f[1] = __uint_as_float(w.x & 0xFFFF0000u);
+    f[2] = __uint_as_float(w.y << 16); f[3] = __uint_as_float(w.y & 0xFFFF0000u);
+    f[4] = __uint_as_float(w.z << 16); f[5] = __uint_as_float(w.z & 0xFFFF0000u);
+    f[6] = __uint_as_float(w.w << 16); f[7] = __uint_as_float(w.w & 0xFFFF0000u);
+}
+
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// 256-thread block reduction (4 waves); red must hold >= 4 floats; all threads get the result
+__device__ __forceinline__ float block_sum256(float v, float *red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+__device__ __forceinline__ float block_max256(float v, float *red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// IEEE single-precision helpers (correctly rounded, as the host C does)
+__device__ __forceinline__ float div_rn(float a, float b) { return __fdiv_rn(a, b); }
+__device__ __forceinline__ float sqrt_rn(float a) { return __fsqrt_rn(a); }
+
+// RMSNorm scale exactly as written in the reference (K.c:27-39):
+// inv = 1/sqrtf(ss/dim + eps)
+__device__ __forceinline__ float rms_inv(float ss, int dim, float eps) {
+    return div_rn(1.0f, sqrt_rn(div_rn(ss, (float)dim) + eps));
+}
+
+// expf with glibc 2.35's exact result (sysdeps/ieee754/flt-32/e_expf.c algorithm:
+// 32-entry 2^(i/32) table + cubic in double, FMA ifunc variant).  Verified
+// bit-identical to the host libm expf over every float in [-87, 88]
+// (tests/test_expf.py re-checks it on the box).  Used where the reference's
+// discrete output depends on the exact bits (the sampler's softmax).
+__constant__ uint64_t kExp2fTab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull,
+};
+__device__ __forceinline__ float expf_glibc(float x) {
+#pragma clang fp contract(off)
+    if (x > 0x1.62e42ep6f) return __builtin_inff();
+    if (x < -0x1.9fe368p6f) return 0.0f;
+    const double kInvLn2N = 0x1.71547652b82fep+0 * 32.0;
+    const double kShift = 0x1.8p+52;
+    const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32;
+    const double C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32;
+    const double C2 = 0x1.62e42ff0c52d6p-1 / 32;
+    double xd = (double)x;
+    double z = kInvLn2N * xd;
+    double kd = z + kShift;
+    uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd -= kShift;
+    double r = __fma_rn(kInvLn2N, xd, -kd);
+    uint64_t t = kExp2fTab[ki % 32];
+    t += ki << (52 - 5);
+    double s = __longlong_as_double((long long)t);
+    double zz = __fma_rn(C0, r, C1);
+    double r2 = r * r;
+    double y = __fma_rn(C2, r, 1.0);
+    y = __fma_rn(zz, r2, y);
+    y = y * s;
+    return (float)y;
+}

@@ -1,0 +1,114 @@
+// qtts_kernels.h - internal launch interface of the gfx950 kernels (C++ only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SILU = 2, EPI_RESID = 3, EPI_SWIGLU = 4 };
+
+struct GemvArgs {
+    const bf16_t *W = nullptr;  // [R, C] bf16 row-major
+    int R = 0, C = 0;
+    int ksplit = 0;             // 0 = auto
+    int cch = 0;                // set by launcher
+    int nt = 1;                 // non-temporal weight loads
+    int nb = 1;                 // batch rows
+    // x source: fp32 rows, or bf16 table rows gathered by id
+    const float *x = nullptr;
+    int ldx = 0;
+    const bf16_t *table = nullptr;  // [*, C]
+    const int *ids = nullptr;       // id(b) = ids[b*ids_bstride + row_sel[b]*ids_rstride + ids_off]
+    int ids_bstride = 1, ids_rstride = 0, ids_off = 0;
+    const int *row_sel = nullptr;
+    // prologue
+    const float *norm_w = nullptr;  // RMSNorm weights [C] (nullptr: no norm)
+    float eps = 1e-6f;
+    float *xcopy = nullptr;         // workgroup 0 writes x rows here
+    int ldxc = 0;
+    int xcopy_normed = 0;
+    // epilogue
+    float *y = nullptr;
+    int ldy = 0;
+    const float *bias = nullptr;
+    int epi = EPI_STORE;
+};
+int qtts_gemv(const GemvArgs &a, hipStream_t st);
+
+struct AttnArgs {
+    int mode = 0;                  // 0 decode (fused q/k norm + rope + cache write), 1 cached
+    const float *qkv = nullptr;    // row r: [q NH*HD | k KV*HD | v KV*HD]
+    int ld_qkv = 0;
+    const float *qn_w = nullptr, *kn_w = nullptr;
+    float eps = 1e-6f;
+    const float *rope_cos = nullptr, *rope_sin = nullptr;  // [pos][HD]
+    float *kc = nullptr, *vc = nullptr;                    // layer slice [B][S][KV*HD]
+    int S = 0;
+    const int *pos = nullptr;      // decode: pos[b]; cached: pos[row]
+    int pos_const = 0;             // used when pos == nullptr
+    const int *row_b = nullptr;    // cached: batch index of each row
+    int NH = 0, KV = 0, HD = 0;
+    float *out = nullptr;          // [rows][NH*HD]
+    int ld_out = 0;
+    int nrows = 0;
+    const int *skip = nullptr;     // decode: per-b stop flags (skip the cache write)
+    int win = 0;                   // >0: sliding window (keys t > pos - win), c/qwen_tts_codec.c:363-367
+};
+int qtts_attention(const AttnArgs &a, hipStream_t st);
+// prefill helper: q/k RMSNorm + RoPE in place on qkv rows, k/v -> cache at (row_b, pos)
+int qtts_qk_prep(const AttnArgs &a, hipStream_t st);
+
+struct SampArgs {
+    const float *logits = nullptr;
+    int ld = 0, n = 0, nb = 1;
+    int top_k = 50;
+    float top_p = 1.0f, temp = 0.9f;
+    uint32_t *rng = nullptr;       // [B] float-bit xorshift state
+    int mode = 0;                  // 0 sub-talker, 1 talker
+    // talker mode
+    int suppress_lo = 0, eos = -1;
+    float rep = 1.0f;
+    int *counts = nullptr;         // [B][n] occurrences of each generated id
+    int fixed = 0;
+    int *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr, *stop_step = nullptr;
+    uint32_t *st_rng = nullptr;    // sub-talker state reset per frame
+    uint32_t seed_bits = 0;
+    // outputs: codes[b*codes_bstride + cur_row[b]*G + g]
+    int *codes = nullptr;
+    int codes_bstride = 0, G = 16, g = 0;
+    int *out_tok = nullptr;        // optional plain output [b]
+};
+int qtts_sample(const SampArgs &a, hipStream_t st);
+
+struct EmbedSumArgs {
+    const int *codes = nullptr;
+    int codes_bstride = 0, G = 16;
+    const int *cur_row = nullptr, *stopped = nullptr;
+    const bf16_t *codec_emb = nullptr;   // [V][H]
+    const bf16_t *st_emb = nullptr;      // [G-1][Vs][H]
+    int Vs = 0, H = 0, nb = 1;
+    const float *trailing = nullptr;     // [B][tr_cap][H]
+    int tr_cap = 0;
+    const int *n_trailing = nullptr;
+    const float *pad = nullptr;          // [H]
+    float *out = nullptr;                // [B][H]
+    int *kv_len = nullptr;
+    int advance = 0;
+};
+int qtts_embed_sum(const EmbedSumArgs &a, hipStream_t st);
+
+// prompt assembly: prefill rows [B][p_cap][H] and trailing rows [B][tr_cap][H]
+struct PromptArgs {
+    const float *proj = nullptr;   // projected text rows [nrows][H]
+    const int *plan = nullptr;     // per output row: {proj_row, codec_id(-1 none), dest_kind(0 prefill/1 trailing), b, slot}
+    int nplan = 0, H = 0;
+    const bf16_t *codec_emb = nullptr;
+    float *prefill = nullptr;
+    int p_cap = 0;
+    float *trailing = nullptr;
+    int tr_cap = 0;
+};
+int qtts_prompt_assemble(const PromptArgs &a, hipStream_t st);
+
+int qtts_copy_rows(float *dst, int ldd, const float *src, int lds, const int *src_rows, int nrows, int ncols,
+                   hipStream_t st);

@@ -1,0 +1,935 @@
+// qtts_runtime.hip - device model, weight layout in HBM, generation state,
+// frame HIP graphs and the C-ABI of include/qtts_hip.h.
+//
+// HBM layout (per device, one model, B slots):
+//   talker layer l:  wqkv [(NH+2KV)*HD, H] bf16   fused q|k|v rows
+//                    wo   [H, NH*HD]            bf16
+//                    wgu  [2I, H]               bf16   gate/up interleaved in row quads
+//                                                      (g0..g3 u0..u3 g4..g7 u4..u7 ...)
+//                    wdown[H, I]                bf16
+//                    q/k norm [HD], in/post norm [H] f32
+//   sub-talker: same per layer; codec embeddings [G-1][Vs][H] and lm heads
+//               [G-1][Vs][Hs] contiguous so a pass selects its table by offset
+//   KV caches fp32 (as the reference, T.c:191-196): talker [L][B][S][KV*HD],
+//               sub-talker [Ls][B][G][KVs*HDs]
+//   codec: f32 tensors by name (k_codec.hip)
+//
+// One frame (group-0 sample + 15 sub-talker groups + next embedding) is ONE
+// captured HIP graph; position / row / stop state lives in device memory so
+// the same graph replays every frame with no host round trip.
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+#include "qtts_codec.h"
+#include "../../../include/qtts_hip.h"
+
+#define CK(x)                                                                                              \
+    do {                                                                                                   \
+        hipError_t e_ = (x);                                                                               \
+        if (e_ != hipSuccess) {                                                                            \
+            fprintf(stderr, "HIP error %s at %s:%d: %s\n", hipGetErrorName(e_), __FILE__, __LINE__, #x);   \
+            return -1;                                                                                     \
+        }                                                                                                  \
+    } while (0)
+#define CKI(x)                                                                                             \
+    do {                                                                                                   \
+        if ((x) != 0) return -1;                                                                           \
+    } while (0)
+
+namespace {
+
+struct Layer {
+    bf16_t *wqkv = nullptr, *wo = nullptr, *wgu = nullptr, *wdown = nullptr;
+    float *qn = nullptr, *kn = nullptr, *in = nullptr, *post = nullptr;
+};
+
+float host_bf16(uint16_t v) {
+    uint32_t u = (uint32_t)v << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+uint16_t host_to_bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (uint16_t)((u + (((u >> 16) & 1) + 0x7FFF)) >> 16);
+}
+float host_f16(uint16_t h) {
+    _Float16 x;
+    memcpy(&x, &h, 2);
+    return (float)x;
+}
+
+}  // namespace
+
+struct qtts_dev {
+    qtts_dims_t d{};
+    int device = 0;
+    hipStream_t st = nullptr;
+    size_t wbytes = 0, sbytes = 0;
+    std::vector<void *> wallocs, sallocs;
+    // talker
+    std::vector<Layer> tl, sl;
+    bf16_t *codec_emb = nullptr, *text_emb = nullptr, *fc1w = nullptr, *fc2w = nullptr, *head = nullptr;
+    float *fc1b = nullptr, *fc2b = nullptr, *tk_norm = nullptr;
+    // sub-talker
+    bf16_t *st_emb = nullptr, *lm = nullptr, *st_proj = nullptr;
+    float *st_projb = nullptr, *st_norm = nullptr;
+    // codec
+    CodecModel codec;
+    // rope
+    float *rope_cos = nullptr, *rope_sin = nullptr, *rope_cos_s = nullptr, *rope_sin_s = nullptr;
+    int rope_max = 0;
+    std::set<std::string> got;
+    // state
+    int nb = 0, nrun = 0, max_frames = 0, S = 0, p_cap = 0, tr_cap = 0, rows_cap = 0;  // nb: allocated slots (strides), nrun: rows launched
+    float *x_tk = nullptr, *qkv = nullptr, *att = nullptr, *hbuf = nullptr, *logits = nullptr, *tk_hid = nullptr;
+    float *x_st = nullptr, *qkv_s = nullptr, *att_s = nullptr, *h_s = nullptr, *logits_s = nullptr;
+    float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
+    int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
+    int *stop_step = nullptr, *kv_len = nullptr, *n_trailing = nullptr;
+    uint32_t *rng = nullptr, *st_rng = nullptr;
+    float *trailing = nullptr, *prefill = nullptr, *pad_emb = nullptr;
+    // prefill / prompt scratch
+    float *px = nullptr, *pqkv = nullptr, *patt = nullptr, *ph = nullptr, *pt1 = nullptr, *pproj = nullptr;
+    int *prow_b = nullptr, *ppos = nullptr, *psrc = nullptr, *pids = nullptr, *pplan = nullptr, *plast = nullptr;
+    int ids_cap = 0;
+    std::vector<int> p_len_h, n_tr_h;
+    qtts_gen_params_t par{};
+    bool have_par = false;
+    hipGraphExec_t g0 = nullptr, gN = nullptr;
+    int graph_key = -1;
+
+    int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
+    int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
+};
+
+// ----------------------------------------------------------------- helpers
+static void *dalloc(qtts_dev *dv, size_t n, bool weight) {
+    void *p = nullptr;
+    if (n == 0) n = 16;
+    if (hipMalloc(&p, n) != hipSuccess) {
+        fprintf(stderr, "qtts: hipMalloc(%zu) failed\n", n);
+        return nullptr;
+    }
+    if (weight) { dv->wallocs.push_back(p); dv->wbytes += n; }
+    else { dv->sallocs.push_back(p); dv->sbytes += n; }
+    return p;
+}
+
+static void free_state(qtts_dev *dv) {
+    if (dv->g0) { hipGraphExecDestroy(dv->g0); dv->g0 = nullptr; }
+    if (dv->gN) { hipGraphExecDestroy(dv->gN); dv->gN = nullptr; }
+    for (void *p : dv->sallocs) hipFree(p);
+    dv->sallocs.clear();
+    dv->sbytes = 0;
+    dv->nb = 0;
+    dv->nrun = 0;
+    dv->ids_cap = 0;  // prompt scratch lived in sallocs
+    dv->pids = dv->pplan = nullptr;
+    dv->pt1 = dv->pproj = nullptr;
+    dv->graph_key = -1;
+    codec_free_state(&dv->codec);
+}
+
+static std::vector<float> to_f32(const void *host, int dtype, size_t n) {
+    std::vector<float> o(n);
+    if (dtype == 0) memcpy(o.data(), host, n * 4);
+    else if (dtype == 1) for (size_t i = 0; i < n; ++i) o[i] = host_bf16(((const uint16_t *)host)[i]);
+    else for (size_t i = 0; i < n; ++i) o[i] = host_f16(((const uint16_t *)host)[i]);
+    return o;
+}
+
+static float *upload_f32(qtts_dev *dv, const void *host, int dtype, size_t n) {
+    std::vector<float> f = to_f32(host, dtype, n);
+    float *p = (float *)dalloc(dv, n * 4, true);
+    if (!p || hipMemcpy(p, f.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return p;
+}
+
+static int upload_bf16_at(bf16_t *dst, const void *host, int dtype, size_t n) {
+    if (dtype == 1) return hipMemcpy(dst, host, n * 2, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+    std::vector<uint16_t> t(n);
+    std::vector<float> f = to_f32(host, dtype, n);
+    for (size_t i = 0; i < n; ++i) t[i] = host_to_bf16(f[i]);
+    return hipMemcpy(dst, t.data(), n * 2, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
+static bf16_t *upload_bf16(qtts_dev *dv, const void *host, int dtype, size_t n) {
+    bf16_t *p = (bf16_t *)dalloc(dv, n * 2, true);
+    if (!p || upload_bf16_at(p, host, dtype, n)) return nullptr;
+    return p;
+}
+
+// ----------------------------------------------------------------- weights
+static int put_layer(qtts_dev *dv, Layer &ly, const std::string &suf, const void *host, int dtype, size_t n,
+                     int H, int NH, int KV, int HD, int I) {
+    const size_t qd = (size_t)NH * HD, kd = (size_t)KV * HD;
+    const size_t qkv_rows = qd + 2 * kd;
+    if (suf == "self_attn.q_proj.weight" || suf == "self_attn.k_proj.weight" || suf == "self_attn.v_proj.weight") {
+        if (!ly.wqkv) ly.wqkv = (bf16_t *)dalloc(dv, qkv_rows * H * 2, true);
+        if (!ly.wqkv) return -1;
+        size_t off = suf[10] == 'q' ? 0 : suf[10] == 'k' ? qd : qd + kd;
+        size_t rows = suf[10] == 'q' ? qd : kd;
+        if (n != rows * H) { fprintf(stderr, "qtts: %s has %zu elements, expected %zu\n", suf.c_str(), n, rows * H); return -1; }
+        return upload_bf16_at(ly.wqkv + off * H, host, dtype, n);
+    }
+    if (suf == "self_attn.o_proj.weight") {
+        if (n != (size_t)H * qd) return -1;
+        ly.wo = upload_bf16(dv, host, dtype, n);
+        return ly.wo ? 0 : -1;
+    }
+    if (suf == "mlp.gate_proj.weight" || suf == "mlp.up_proj.weight") {
+        if (n != (size_t)I * H || I % 4) return -1;
+        if (!ly.wgu) ly.wgu = (bf16_t *)dalloc(dv, (size_t)2 * I * H * 2, true);
+        if (!ly.wgu) return -1;
+        const bool up = suf[4] == 'u';
+        std::vector<uint16_t> tmp;
+        const void *src = host;
+        if (dtype != 1) {
+            tmp.resize(n);
+            std::vector<float> f = to_f32(host, dtype, n);
+            for (size_t i = 0; i < n; ++i) tmp[i] = host_to_bf16(f[i]);
+            src = tmp.data();
+        }
+        // quad q of gate -> rows 8q..8q+3, of up -> rows 8q+4..8q+7
+        const size_t quad = (size_t)4 * H * 2;
+        return hipMemcpy2D((char *)ly.wgu + (up ? quad : 0), 2 * quad, src, quad, quad, I / 4,
+                           hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+    }
+    if (suf == "mlp.down_proj.weight") {
+        if (n != (size_t)H * I) return -1;
+        ly.wdown = upload_bf16(dv, host, dtype, n);
+        return ly.wdown ? 0 : -1;
+    }
+    float **f = suf == "self_attn.q_norm.weight" ? &ly.qn : suf == "self_attn.k_norm.weight" ? &ly.kn
+              : suf == "input_layernorm.weight" ? &ly.in : suf == "post_attention_layernorm.weight" ? &ly.post : nullptr;
+    if (f) {
+        *f = upload_f32(dv, host, dtype, n);
+        return *f ? 0 : -1;
+    }
+    return 0;  // unused tensor
+}
+
+static int parse_idx(const std::string &name, const std::string &pre, std::string *rest) {
+    if (name.compare(0, pre.size(), pre) != 0) return -1;
+    size_t p = pre.size(), q = p;
+    while (q < name.size() && isdigit((unsigned char)name[q])) ++q;
+    if (q == p || q >= name.size() || name[q] != '.') return -1;
+    *rest = name.substr(q + 1);
+    return atoi(name.c_str() + p);
+}
+
+extern "C" int qtts_dev_put_tensor(qtts_dev_t *dv, const char *cname, const void *host, int dtype,
+                                   const int64_t *shape, int ndim) {
+    if (!dv || !cname || !host) return -1;
+    hipSetDevice(dv->device);
+    std::string name(cname), rest;
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
+    const qtts_dims_t &d = dv->d;
+    int rc = 0, idx;
+    if (name.compare(0, 8, "decoder.") == 0) {
+        rc = codec_put_tensor(&dv->codec, name, host, dtype, shape, ndim, n);
+    } else if (name == "talker.model.codec_embedding.weight") {
+        dv->codec_emb = upload_bf16(dv, host, dtype, n); rc = dv->codec_emb ? 0 : -1;
+    } else if (name == "talker.model.text_embedding.weight") {
+        dv->text_emb = upload_bf16(dv, host, dtype, n); rc = dv->text_emb ? 0 : -1;
+    } else if (name == "talker.text_projection.linear_fc1.weight") {
+        dv->fc1w = upload_bf16(dv, host, dtype, n); rc = dv->fc1w ? 0 : -1;
+    } else if (name == "talker.text_projection.linear_fc1.bias") {
+        dv->fc1b = upload_f32(dv, host, dtype, n); rc = dv->fc1b ? 0 : -1;
+    } else if (name == "talker.text_projection.linear_fc2.weight") {
+        dv->fc2w = upload_bf16(dv, host, dtype, n); rc = dv->fc2w ? 0 : -1;
+    } else if (name == "talker.text_projection.linear_fc2.bias") {
+        dv->fc2b = upload_f32(dv, host, dtype, n); rc = dv->fc2b ? 0 : -1;
+    } else if (name == "talker.model.norm.weight") {
+        dv->tk_norm = upload_f32(dv, host, dtype, n); rc = dv->tk_norm ? 0 : -1;
+    } else if (name == "talker.codec_head.weight") {
+        dv->head = upload_bf16(dv, host, dtype, n); rc = dv->head ? 0 : -1;
+    } else if (name == "talker.code_predictor.small_to_mtp_projection.weight") {
+        dv->st_proj = upload_bf16(dv, host, dtype, n); rc = dv->st_proj ? 0 : -1;
+    } else if (name == "talker.code_predictor.small_to_mtp_projection.bias") {
+        dv->st_projb = upload_f32(dv, host, dtype, n); rc = dv->st_projb ? 0 : -1;
+    } else if (name == "talker.code_predictor.model.norm.weight") {
+        dv->st_norm = upload_f32(dv, host, dtype, n); rc = dv->st_norm ? 0 : -1;
+    } else if ((idx = parse_idx(name, "talker.code_predictor.model.codec_embedding.", &rest)) >= 0 && rest == "weight") {
+        if (idx >= d.G - 1 || n != (size_t)d.Vs * d.H) { fprintf(stderr, "qtts: bad %s\n", cname); return -1; }
+        if (!dv->st_emb) dv->st_emb = (bf16_t *)dalloc(dv, (size_t)(d.G - 1) * d.Vs * d.H * 2, true);
+        rc = dv->st_emb ? upload_bf16_at(dv->st_emb + (size_t)idx * d.Vs * d.H, host, dtype, n) : -1;
+    } else if ((idx = parse_idx(name, "talker.code_predictor.lm_head.", &rest)) >= 0 && rest == "weight") {
+        if (idx >= d.G - 1 || n != (size_t)d.Vs * d.Hs) { fprintf(stderr, "qtts: bad %s\n", cname); return -1; }
+        if (!dv->lm) dv->lm = (bf16_t *)dalloc(dv, (size_t)(d.G - 1) * d.Vs * d.Hs * 2, true);
+        rc = dv->lm ? upload_bf16_at(dv->lm + (size_t)idx * d.Vs * d.Hs, host, dtype, n) : -1;
+    } else if ((idx = parse_idx(name, "talker.code_predictor.model.layers.", &rest)) >= 0) {
+        if (idx >= d.Ls) return 0;
+        rc = put_layer(dv, dv->sl[idx], rest, host, dtype, n, d.Hs, d.NHs, d.KVs, d.HDs, d.Is);
+    } else if ((idx = parse_idx(name, "talker.model.layers.", &rest)) >= 0) {
+        if (idx >= d.L) return 0;
+        rc = put_layer(dv, dv->tl[idx], rest, host, dtype, n, d.H, d.NH, d.KV, d.HD, d.I);
+    } else {
+        return 0;
+    }
+    if (rc) {
+        fprintf(stderr, "qtts: failed to upload tensor %s\n", cname);
+        return -1;
+    }
+    dv->got.insert(name);
+    return 0;
+}
+
+extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
+    if (hipSetDevice(device) != hipSuccess) {
+        fprintf(stderr, "qtts: cannot select HIP device %d\n", device);
+        return nullptr;
+    }
+    qtts_dev *dv = new qtts_dev();
+    dv->d = *dims;
+    dv->device = device;
+    if (hipStreamCreateWithFlags(&dv->st, hipStreamNonBlocking) != hipSuccess) {
+        delete dv;
+        return nullptr;
+    }
+    dv->tl.resize(dims->L);
+    dv->sl.resize(dims->Ls);
+    codec_init(&dv->codec, dims, dv->st);
+    return dv;
+}
+
+extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
+    if (!dv) return;
+    hipSetDevice(dv->device);
+    hipStreamSynchronize(dv->st);
+    free_state(dv);
+    codec_destroy(&dv->codec);
+    for (void *p : dv->wallocs) hipFree(p);
+    hipStreamDestroy(dv->st);
+    delete dv;
+}
+
+extern "C" size_t qtts_dev_bytes(const qtts_dev_t *dv, int which) {
+    if (!dv) return 0;
+    return which == 0 ? dv->wbytes + codec_weight_bytes(&dv->codec) : dv->sbytes;
+}
+
+// RoPE tables with the reference's exact libm arithmetic (T.c:97-113)
+static int build_rope(qtts_dev *dv, int npos, int hd, float theta, float **cs, float **sn) {
+    std::vector<float> c((size_t)npos * hd), s((size_t)npos * hd);
+    const int half = hd / 2;
+    for (int p = 0; p < npos; ++p)
+        for (int i = 0; i < half; ++i) {
+            float freq = 1.0f / powf(theta, (float)(2 * i) / (float)hd);
+            float ang = (float)p * freq;
+            c[(size_t)p * hd + i] = c[(size_t)p * hd + i + half] = cosf(ang);
+            s[(size_t)p * hd + i] = s[(size_t)p * hd + i + half] = sinf(ang);
+        }
+    *cs = (float *)dalloc(dv, c.size() * 4, true);
+    *sn = (float *)dalloc(dv, s.size() * 4, true);
+    if (!*cs || !*sn) return -1;
+    CK(hipMemcpy(*cs, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(*sn, s.data(), s.size() * 4, hipMemcpyHostToDevice));
+    return 0;
+}
+
+extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
+    const qtts_dims_t &d = dv->d;
+    hipSetDevice(dv->device);
+    auto need = [&](const std::string &n) {
+        if (!dv->got.count(n)) { fprintf(stderr, "Error: missing required tensor: %s\n", n.c_str()); return false; }
+        return true;
+    };
+    bool ok = need("talker.model.codec_embedding.weight") && need("talker.model.text_embedding.weight") &&
+              need("talker.text_projection.linear_fc1.weight") && need("talker.text_projection.linear_fc2.weight") &&
+              need("talker.model.norm.weight") && need("talker.codec_head.weight") &&
+              need("talker.code_predictor.model.norm.weight");
+    static const char *lsuf[] = {"self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight",
+                                 "self_attn.o_proj.weight", "self_attn.q_norm.weight", "self_attn.k_norm.weight",
+                                 "input_layernorm.weight", "post_attention_layernorm.weight", "mlp.gate_proj.weight",
+                                 "mlp.up_proj.weight", "mlp.down_proj.weight"};
+    for (int l = 0; ok && l < d.L; ++l)
+        for (const char *s : lsuf) ok = ok && need("talker.model.layers." + std::to_string(l) + "." + s);
+    for (int l = 0; ok && l < d.Ls; ++l)
+        for (const char *s : lsuf) ok = ok && need("talker.code_predictor.model.layers." + std::to_string(l) + "." + s);
+    for (int g = 0; ok && g < d.G - 1; ++g) {
+        ok = ok && need("talker.code_predictor.model.codec_embedding." + std::to_string(g) + ".weight");
+        ok = ok && need("talker.code_predictor.lm_head." + std::to_string(g) + ".weight");
+    }
+    if (ok && d.H != d.Hs) ok = need("talker.code_predictor.small_to_mtp_projection.weight");
+    if (!ok) return -1;
+    if (d.HD > 128 || d.HDs > 128 || d.G > 32) {
+        fprintf(stderr, "Error: unsupported head_dim (talker=%d subtalker=%d) or code groups %d\n", d.HD, d.HDs, d.G);
+        return -1;
+    }
+    if (d.V > 4096 || d.Vs > 4096) {
+        fprintf(stderr, "Error: vocab > 4096 unsupported by the device sampler\n");
+        return -1;
+    }
+    return codec_finalize(&dv->codec);
+}
+
+// ----------------------------------------------------------------- state
+static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
+    const qtts_dims_t &d = dv->d;
+    free_state(dv);
+    dv->nb = nb;
+    dv->nrun = nb;
+    dv->max_frames = max_frames;
+    dv->p_cap = max_prefill;
+    dv->S = max_prefill + max_frames + 1;
+    dv->tr_cap = 4096;  // trailing rows per slot (text length bound)
+    dv->rows_cap = nb * max_prefill;
+    const size_t B = nb;
+#define A(ptr, type, cnt)                                                 \
+    do {                                                                  \
+        dv->ptr = (type *)dalloc(dv, (size_t)(cnt) * sizeof(type), false); \
+        if (!dv->ptr) return -1;                                          \
+    } while (0)
+    A(x_tk, float, B * d.H);
+    A(qkv, float, B * dv->QKV());
+    A(att, float, B * d.NH * d.HD);
+    A(hbuf, float, B * d.I);
+    A(logits, float, B * d.V);
+    A(tk_hid, float, B * d.H);
+    A(x_st, float, B * d.Hs);
+    A(qkv_s, float, B * dv->QKVs());
+    A(att_s, float, B * d.NHs * d.HDs);
+    A(h_s, float, B * d.Is);
+    A(logits_s, float, B * d.Vs);
+    A(kc, float, (size_t)d.L * B * dv->S * d.KV * d.HD);
+    A(vc, float, (size_t)d.L * B * dv->S * d.KV * d.HD);
+    A(kcs, float, (size_t)d.Ls * B * d.G * d.KVs * d.HDs);
+    A(vcs, float, (size_t)d.Ls * B * d.G * d.KVs * d.HDs);
+    A(codes, int, B * (max_frames + 1) * d.G);
+    A(counts, int, B * d.V);
+    A(n_gen, int, B);
+    A(stopped, int, B);
+    A(cur_row, int, B);
+    A(stop_step, int, B);
+    A(kv_len, int, B);
+    A(n_trailing, int, B);
+    A(rng, uint32_t, B);
+    A(st_rng, uint32_t, B);
+    A(trailing, float, B * 64 * d.H);  // grown on demand in qtts_dev_prompt
+    dv->tr_cap = 64;
+    A(prefill, float, B * max_prefill * d.H);
+    A(pad_emb, float, d.H);
+    const size_t R = dv->rows_cap;
+    A(px, float, R * d.H);
+    A(pqkv, float, R * dv->QKV());
+    A(patt, float, R * d.NH * d.HD);
+    A(ph, float, R * d.I);
+    A(prow_b, int, R);
+    A(ppos, int, R);
+    A(psrc, int, R);
+    A(plast, int, B);
+#undef A
+    dv->p_len_h.assign(nb, 0);
+    dv->n_tr_h.assign(nb, 0);
+    CK(hipMemsetAsync(dv->codes, 0, B * (max_frames + 1) * d.G * sizeof(int), dv->st));
+    CK(hipMemsetAsync(dv->kcs, 0, (size_t)d.Ls * B * d.G * d.KVs * d.HDs * 4, dv->st));
+    CK(hipMemsetAsync(dv->vcs, 0, (size_t)d.Ls * B * d.G * d.KVs * d.HDs * 4, dv->st));
+    // RoPE tables sized to the KV capacity
+    if (dv->rope_max < dv->S) {
+        dv->rope_max = dv->S;
+        CKI(build_rope(dv, dv->S, d.HD, d.theta, &dv->rope_cos, &dv->rope_sin));
+        if (d.HDs != d.HD) CKI(build_rope(dv, d.G + 2, d.HDs, d.theta, &dv->rope_cos_s, &dv->rope_sin_s));
+        else { dv->rope_cos_s = dv->rope_cos; dv->rope_sin_s = dv->rope_sin; }
+    }
+    dv->graph_key = -1;
+    return 0;
+}
+
+static uint32_t seed_bits(int seed) {
+    float f = (float)seed;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+
+static int reset_counters(qtts_dev *dv) {
+    const size_t B = dv->nb;
+    hipStream_t st = dv->st;
+    CK(hipMemsetAsync(dv->counts, 0, B * dv->d.V * sizeof(int), st));
+    CK(hipMemsetAsync(dv->n_gen, 0, B * sizeof(int), st));
+    CK(hipMemsetAsync(dv->stopped, 0, B * sizeof(int), st));
+    CK(hipMemsetAsync(dv->cur_row, 0, B * sizeof(int), st));
+    CK(hipMemsetAsync(dv->stop_step, 0, B * sizeof(int), st));
+    std::vector<uint32_t> r(B, seed_bits(dv->par.seed));
+    CK(hipMemcpyAsync(dv->rng, r.data(), B * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dv->st_rng, r.data(), B * 4, hipMemcpyHostToDevice, st));
+    CK(hipStreamSynchronize(st));
+    return 0;
+}
+
+// ----------------------------------------------------------------- kernels of one frame
+static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float *y, int ldy, int nb, int epi) {
+    GemvArgs a;
+    a.W = W; a.R = R; a.C = C; a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy; a.nb = nb; a.epi = epi;
+    return a;
+}
+
+static int talker_layers(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    const int nb = dv->nrun, NBA = dv->nb, QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
+    hipStream_t st = dv->st;
+    for (int l = 0; l < d.L; ++l) {
+        Layer &ly = dv->tl[l];
+        GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->x_tk, d.H, dv->qkv, QKV, nb, EPI_STORE);
+        a.norm_w = ly.in; a.eps = d.eps;
+        CKI(qtts_gemv(a, st));
+        AttnArgs t;
+        t.mode = 0; t.qkv = dv->qkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
+        t.rope_cos = dv->rope_cos; t.rope_sin = dv->rope_sin;
+        t.kc = dv->kc + (size_t)l * NBA * dv->S * KVD; t.vc = dv->vc + (size_t)l * NBA * dv->S * KVD; t.S = dv->S;
+        t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
+        t.skip = dv->stopped;
+        CKI(qtts_attention(t, st));
+        CKI(qtts_gemv(gv(ly.wo, d.H, AD, dv->att, AD, dv->x_tk, d.H, nb, EPI_RESID), st));
+        a = gv(ly.wgu, 2 * d.I, d.H, dv->x_tk, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
+        a.norm_w = ly.post; a.eps = d.eps;
+        CKI(qtts_gemv(a, st));
+        CKI(qtts_gemv(gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, dv->x_tk, d.H, nb, EPI_RESID), st));
+    }
+    return 0;
+}
+
+// final norm + codec head; normed hidden -> tk_hid (T.c:526-530, Q.c:1295)
+static int talker_tail(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    GemvArgs a = gv(dv->head, d.V, d.H, dv->x_tk, d.H, dv->logits, d.V, dv->nrun, EPI_STORE);
+    a.norm_w = dv->tk_norm; a.eps = d.eps; a.xcopy = dv->tk_hid; a.ldxc = d.H; a.xcopy_normed = 1;
+    return qtts_gemv(a, dv->st);
+}
+
+static int talker_sample(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    SampArgs s;
+    s.logits = dv->logits; s.ld = d.V; s.n = d.V; s.nb = dv->nrun;
+    s.top_k = dv->par.top_k; s.top_p = dv->par.top_p; s.temp = dv->par.temperature;
+    s.rng = dv->rng; s.mode = 1; s.suppress_lo = d.V - 1024; s.eos = d.eos_id;
+    s.rep = dv->par.repetition_penalty; s.counts = dv->counts; s.fixed = dv->par.fixed_codec_tokens;
+    s.n_gen = dv->n_gen; s.stopped = dv->stopped; s.cur_row = dv->cur_row; s.stop_step = dv->stop_step;
+    s.st_rng = dv->st_rng; s.seed_bits = seed_bits(dv->par.seed);
+    s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G;
+    return qtts_sample(s, dv->st);
+}
+
+// 16 sub-talker passes (T.c:539-736)
+static int subtalker(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    const int nb = dv->nrun, NBA = dv->nb, QKV = dv->QKVs(), AD = d.NHs * d.HDs, KVD = d.KVs * d.HDs;
+    const int cstride = (dv->max_frames + 1) * d.G;
+    hipStream_t st = dv->st;
+    const bool proj = dv->st_proj != nullptr;
+    for (int g = 0; g < d.G; ++g) {
+        // input source for this pass
+        GemvArgs src;  // x / table description only
+        src.nb = nb;
+        if (g == 0) { src.x = dv->tk_hid; src.ldx = d.H; }
+        else {
+            src.table = g == 1 ? dv->codec_emb : dv->st_emb + (size_t)(g - 2) * d.Vs * d.H;
+            src.ids = dv->codes; src.ids_bstride = cstride; src.row_sel = dv->cur_row; src.ids_rstride = d.G;
+            src.ids_off = g - 1;
+        }
+        auto set_src = [&](GemvArgs &a) {
+            a.x = src.x; a.ldx = src.ldx; a.table = src.table; a.ids = src.ids; a.ids_bstride = src.ids_bstride;
+            a.row_sel = src.row_sel; a.ids_rstride = src.ids_rstride; a.ids_off = src.ids_off;
+        };
+        if (proj) {  // ST_PROJECT_INPUT (T.c:693-702)
+            GemvArgs a = gv(dv->st_proj, d.Hs, d.H, nullptr, 0, dv->x_st, d.Hs, nb, dv->st_projb ? EPI_BIAS : EPI_STORE);
+            set_src(a);
+            a.bias = dv->st_projb;
+            a.nt = 0;
+            CKI(qtts_gemv(a, st));
+        }
+        for (int l = 0; l < d.Ls; ++l) {
+            Layer &ly = dv->sl[l];
+            GemvArgs a = gv(ly.wqkv, QKV, d.Hs, dv->x_st, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
+            a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
+            if (l == 0 && !proj) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
+            CKI(qtts_gemv(a, st));
+            AttnArgs t;
+            t.mode = 0; t.qkv = dv->qkv_s; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
+            t.rope_cos = dv->rope_cos_s; t.rope_sin = dv->rope_sin_s;
+            t.kc = dv->kcs + (size_t)l * NBA * d.G * KVD; t.vc = dv->vcs + (size_t)l * NBA * d.G * KVD; t.S = d.G;
+            t.pos = nullptr; t.pos_const = g; t.NH = d.NHs; t.KV = d.KVs; t.HD = d.HDs; t.out = dv->att_s;
+            t.ld_out = AD; t.nrows = nb; t.skip = dv->stopped;
+            CKI(qtts_attention(t, st));
+            a = gv(ly.wo, d.Hs, AD, dv->att_s, AD, dv->x_st, d.Hs, nb, EPI_RESID);
+            a.nt = 0;
+            CKI(qtts_gemv(a, st));
+            a = gv(ly.wgu, 2 * d.Is, d.Hs, dv->x_st, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
+            a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
+            CKI(qtts_gemv(a, st));
+            a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, dv->x_st, d.Hs, nb, EPI_RESID);
+            a.nt = 0;
+            CKI(qtts_gemv(a, st));
+        }
+        if (g == 0) continue;  // pass 0 produces no logits
+        GemvArgs a = gv(dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, dv->x_st, d.Hs, dv->logits_s, d.Vs, nb,
+                        EPI_STORE);
+        a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
+        CKI(qtts_gemv(a, st));
+        SampArgs s;
+        s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
+        s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
+        s.mode = 0; s.st_rng = dv->st_rng; s.stopped = dv->stopped; s.cur_row = dv->cur_row;
+        s.codes = dv->codes; s.codes_bstride = cstride; s.G = d.G; s.g = g;
+        CKI(qtts_sample(s, st));
+    }
+    return 0;
+}
+
+static int embed_sum(qtts_dev *dv, int advance) {
+    const qtts_dims_t &d = dv->d;
+    EmbedSumArgs e;
+    e.codes = dv->codes; e.codes_bstride = (dv->max_frames + 1) * d.G; e.G = d.G;
+    e.cur_row = dv->cur_row; e.stopped = dv->stopped; e.codec_emb = dv->codec_emb; e.st_emb = dv->st_emb;
+    e.Vs = d.Vs; e.H = d.H; e.nb = dv->nrun; e.trailing = dv->trailing; e.tr_cap = dv->tr_cap;
+    e.n_trailing = dv->n_trailing; e.pad = dv->pad_emb; e.out = dv->x_tk; e.kv_len = dv->kv_len; e.advance = advance;
+    return qtts_embed_sum(e, dv->st);
+}
+
+static int record_frame(qtts_dev *dv, bool with_talker) {
+    if (with_talker) CKI(talker_layers(dv));
+    CKI(talker_tail(dv));
+    CKI(talker_sample(dv));
+    CKI(subtalker(dv));
+    CKI(embed_sum(dv, with_talker ? 1 : 0));
+    return 0;
+}
+
+static int capture(qtts_dev *dv, bool with_talker, hipGraphExec_t *out) {
+    hipGraph_t g = nullptr;
+    CK(hipStreamBeginCapture(dv->st, hipStreamCaptureModeThreadLocal));
+    int rc = record_frame(dv, with_talker);
+    hipError_t e = hipStreamEndCapture(dv->st, &g);
+    if (rc || e != hipSuccess) {
+        fprintf(stderr, "qtts: frame graph capture failed\n");
+        if (g) hipGraphDestroy(g);
+        return -1;
+    }
+    e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    CK(e);
+    return 0;
+}
+
+static int ensure_graphs(qtts_dev *dv) {
+    if (dv->g0 && dv->gN && dv->graph_key == 1) return 0;
+    if (dv->g0) { hipGraphExecDestroy(dv->g0); dv->g0 = nullptr; }
+    if (dv->gN) { hipGraphExecDestroy(dv->gN); dv->gN = nullptr; }
+    if (getenv("QTTS_HIP_NO_GRAPH")) { dv->graph_key = 0; return 0; }
+    CKI(capture(dv, false, &dv->g0));
+    CKI(capture(dv, true, &dv->gN));
+    dv->graph_key = 1;
+    return 0;
+}
+
+static bool same_params(const qtts_gen_params_t &a, const qtts_gen_params_t &b) {
+    return memcmp(&a, &b, sizeof a) == 0;
+}
+
+extern "C" int qtts_dev_begin(qtts_dev_t *dv, int nb, int max_frames, int max_prefill, const qtts_gen_params_t *p) {
+    if (!dv || nb < 1 || max_frames < 1) return -1;
+    hipSetDevice(dv->device);
+    if (max_prefill < 16) max_prefill = 16;
+    const bool realloc_ = nb != dv->nb || max_frames > dv->max_frames || max_prefill > dv->p_cap;
+    if (realloc_) CKI(alloc_state(dv, nb, max_frames, max_prefill));
+    if (!dv->have_par || !same_params(dv->par, *p)) {
+        dv->par = *p;
+        dv->have_par = true;
+        dv->graph_key = -1;
+    }
+    CKI(reset_counters(dv));
+    return 0;
+}
+
+// ----------------------------------------------------------------- prompt + prefill
+static int ensure_trailing(qtts_dev *dv, int n_tr) {
+    if (n_tr <= dv->tr_cap) return 0;
+    const qtts_dims_t &d = dv->d;
+    int cap = dv->tr_cap;
+    while (cap < n_tr) cap *= 2;
+    float *nt = (float *)dalloc(dv, (size_t)dv->nb * cap * d.H * 4, false);
+    if (!nt) return -1;
+    CK(hipStreamSynchronize(dv->st));
+    for (int b = 0; b < dv->nb; ++b)
+        CK(hipMemcpy(nt + (size_t)b * cap * d.H, dv->trailing + (size_t)b * dv->tr_cap * d.H,
+                     (size_t)dv->tr_cap * d.H * 4, hipMemcpyDeviceToDevice));
+    dv->trailing = nt;  // old block stays in sallocs until free_state
+    dv->tr_cap = cap;
+    dv->graph_key = -1;
+    return 0;
+}
+
+extern "C" int qtts_dev_prompt(qtts_dev_t *dv, int b, const int *text_ids, int n_text, const int *plan, int nplan,
+                               int p_len, int n_trailing, int pad_row) {
+    if (!dv || b < 0 || b >= dv->nb || p_len > dv->p_cap || n_text < 1) return -1;
+    hipSetDevice(dv->device);
+    const qtts_dims_t &d = dv->d;
+    CKI(ensure_trailing(dv, n_trailing));
+    CK(hipStreamSynchronize(dv->st));
+    if (n_text > dv->ids_cap) {
+        int cap = n_text < 256 ? 256 : n_text;
+        dv->pids = (int *)dalloc(dv, (size_t)cap * 4, false);
+        dv->pplan = (int *)dalloc(dv, (size_t)cap * 4 * 5 + 64, false);
+        dv->pt1 = (float *)dalloc(dv, (size_t)cap * d.TH * 4, false);
+        dv->pproj = (float *)dalloc(dv, (size_t)cap * d.H * 4, false);
+        if (!dv->pids || !dv->pplan || !dv->pt1 || !dv->pproj) return -1;
+        dv->ids_cap = cap;
+    }
+    if (nplan > 4 * dv->ids_cap) return -1;
+    CK(hipMemcpy(dv->pids, text_ids, (size_t)n_text * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dv->pplan, plan, (size_t)nplan * 5 * 4, hipMemcpyHostToDevice));
+    // text_embedding -> fc1 (+b, SiLU) -> fc2 (+b), 16 rows per launch (Q.c:823-847)
+    for (int r0 = 0; r0 < n_text; r0 += 16) {
+        const int nr = n_text - r0 < 16 ? n_text - r0 : 16;
+        GemvArgs a = gv(dv->fc1w, d.TH, d.TH, nullptr, 0, dv->pt1 + (size_t)r0 * d.TH, d.TH, nr,
+                        dv->fc1b ? EPI_BIAS_SILU : EPI_STORE);
+        a.table = dv->text_emb; a.ids = dv->pids + r0; a.ids_bstride = 1; a.bias = dv->fc1b;
+        if (!dv->fc1b) { fprintf(stderr, "qtts: text projection without fc1 bias unsupported\n"); return -1; }
+        CKI(qtts_gemv(a, dv->st));
+        a = gv(dv->fc2w, d.H, d.TH, dv->pt1 + (size_t)r0 * d.TH, d.TH, dv->pproj + (size_t)r0 * d.H, d.H, nr,
+               dv->fc2b ? EPI_BIAS : EPI_STORE);
+        a.bias = dv->fc2b;
+        CKI(qtts_gemv(a, dv->st));
+    }
+    PromptArgs pa;
+    pa.proj = dv->pproj; pa.plan = dv->pplan; pa.nplan = nplan; pa.H = d.H; pa.codec_emb = dv->codec_emb;
+    pa.prefill = dv->prefill; pa.p_cap = dv->p_cap; pa.trailing = dv->trailing; pa.tr_cap = dv->tr_cap;
+    CKI(qtts_prompt_assemble(pa, dv->st));
+    if (pad_row >= 0) CK(hipMemcpyAsync(dv->pad_emb, dv->pproj + (size_t)pad_row * d.H, (size_t)d.H * 4,
+                                        hipMemcpyDeviceToDevice, dv->st));
+    CK(hipMemcpyAsync(dv->n_trailing + b, &n_trailing, 4, hipMemcpyHostToDevice, dv->st));
+    CK(hipStreamSynchronize(dv->st));
+    dv->p_len_h[b] = p_len;
+    dv->n_tr_h[b] = n_trailing;
+    return 0;
+}
+
+// talker prefill over all slots' prompt rows (T.c:254-472)
+extern "C" int qtts_dev_prefill(qtts_dev_t *dv) {
+    if (!dv || dv->nb < 1) return -1;
+    hipSetDevice(dv->device);
+    const qtts_dims_t &d = dv->d;
+    hipStream_t st = dv->st;
+    std::vector<int> rb, pp, src, last(dv->nb);
+    for (int b = 0; b < dv->nb; ++b) {
+        for (int t = 0; t < dv->p_len_h[b]; ++t) {
+            rb.push_back(b);
+            pp.push_back(t);
+            src.push_back(b * dv->p_cap + t);
+        }
+        last[b] = (int)rb.size() - 1;
+    }
+    const int R = (int)rb.size();
+    if (R < 1 || R > dv->rows_cap) return -1;
+    CK(hipMemcpyAsync(dv->prow_b, rb.data(), R * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dv->ppos, pp.data(), R * 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dv->psrc, src.data(), R * 4, hipMemcpyHostToDevice, st));
+    CKI(qtts_copy_rows(dv->px, d.H, dv->prefill, d.H, dv->psrc, R, d.H, st));
+    const int QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
+    for (int l = 0; l < d.L; ++l) {
+        Layer &ly = dv->tl[l];
+        for (int r0 = 0; r0 < R; r0 += 16) {
+            const int nr = R - r0 < 16 ? R - r0 : 16;
+            GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->px + (size_t)r0 * d.H, d.H, dv->pqkv + (size_t)r0 * QKV, QKV, nr,
+                            EPI_STORE);
+            a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
+            CKI(qtts_gemv(a, st));
+        }
+        AttnArgs t;
+        t.mode = 1; t.qkv = dv->pqkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
+        t.rope_cos = dv->rope_cos; t.rope_sin = dv->rope_sin;
+        t.kc = dv->kc + (size_t)l * dv->nb * dv->S * KVD; t.vc = dv->vc + (size_t)l * dv->nb * dv->S * KVD;
+        t.S = dv->S; t.pos = dv->ppos; t.row_b = dv->prow_b; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD;
+        t.out = dv->patt; t.ld_out = AD; t.nrows = R;
+        CKI(qtts_qk_prep(t, st));
+        CKI(qtts_attention(t, st));
+        for (int r0 = 0; r0 < R; r0 += 16) {
+            const int nr = R - r0 < 16 ? R - r0 : 16;
+            GemvArgs a = gv(ly.wo, d.H, AD, dv->patt + (size_t)r0 * AD, AD, dv->px + (size_t)r0 * d.H, d.H, nr,
+                            EPI_RESID);
+            a.nt = 0;
+            CKI(qtts_gemv(a, st));
+            a = gv(ly.wgu, 2 * d.I, d.H, dv->px + (size_t)r0 * d.H, d.H, dv->ph + (size_t)r0 * d.I, d.I, nr,
+                   EPI_SWIGLU);
+            a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
+            CKI(qtts_gemv(a, st));
+            a = gv(ly.wdown, d.H, d.I, dv->ph + (size_t)r0 * d.I, d.I, dv->px + (size_t)r0 * d.H, d.H, nr, EPI_RESID);
+            a.nt = 0;
+            CKI(qtts_gemv(a, st));
+        }
+    }
+    // last raw hidden of each slot -> x_tk; kv_len = prefill length
+    CK(hipMemcpyAsync(dv->plast, last.data(), dv->nb * 4, hipMemcpyHostToDevice, st));
+    CKI(qtts_copy_rows(dv->x_tk, d.H, dv->px, d.H, dv->plast, dv->nb, d.H, st));
+    CK(hipMemcpyAsync(dv->kv_len, dv->p_len_h.data(), dv->nb * 4, hipMemcpyHostToDevice, st));
+    CK(hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int qtts_dev_frame(qtts_dev_t *dv, int step) {
+    if (!dv) return -1;
+    hipSetDevice(dv->device);
+    CKI(ensure_graphs(dv));
+    if (dv->graph_key == 0) return record_frame(dv, step > 0);
+    CK(hipGraphLaunch(step == 0 ? dv->g0 : dv->gN, dv->st));
+    return 0;
+}
+
+extern "C" int qtts_dev_poll(qtts_dev_t *dv, int *stopped, int *n_gen, int *stop_step) {
+    if (!dv) return -1;
+    hipSetDevice(dv->device);
+    const size_t B = dv->nb;
+    if (stopped) CK(hipMemcpyAsync(stopped, dv->stopped, B * 4, hipMemcpyDeviceToHost, dv->st));
+    if (n_gen) CK(hipMemcpyAsync(n_gen, dv->n_gen, B * 4, hipMemcpyDeviceToHost, dv->st));
+    if (stop_step) CK(hipMemcpyAsync(stop_step, dv->stop_step, B * 4, hipMemcpyDeviceToHost, dv->st));
+    CK(hipStreamSynchronize(dv->st));
+    return 0;
+}
+
+extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int max_frames) {
+    if (!dv || b < 0 || b >= dv->nb) return -1;
+    hipSetDevice(dv->device);
+    int n = 0;
+    CK(hipMemcpyAsync(&n, dv->n_gen + b, 4, hipMemcpyDeviceToHost, dv->st));
+    CK(hipStreamSynchronize(dv->st));
+    if (n > max_frames) n = max_frames;
+    CK(hipMemcpyAsync(host_codes, dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G, (size_t)n * dv->d.G * 4,
+                      hipMemcpyDeviceToHost, dv->st));
+    CK(hipStreamSynchronize(dv->st));
+    return n;
+}
+
+extern "C" float *qtts_dev_codec_slot(qtts_dev_t *dv, int b, int T, int *out_samples) {
+    if (out_samples) *out_samples = 0;
+    if (!dv || b < 0 || b >= dv->nb || T < 1) return nullptr;
+    hipSetDevice(dv->device);
+    return codec_decode(&dv->codec, dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G, T, out_samples);
+}
+
+// ----------------------------------------------------------------- host-pointer stage wrappers
+static int ensure_slot0(qtts_dev *dv) {
+    if (dv->nb >= 1) return 0;
+    qtts_gen_params_t p{0.9f, 1.0f, 1.05f, 50, 0.9f, 1.0f, 50, 0, 42};
+    return qtts_dev_begin(dv, 1, 4096, 256, &p);
+}
+
+extern "C" int qtts_dev_talker_prefill_host(qtts_dev_t *dv, const float *embeds, int n, float *hidden_out) {
+    if (!dv) return -1;
+    hipSetDevice(dv->device);
+    CKI(ensure_slot0(dv));
+    if (n > dv->p_cap) {
+        qtts_gen_params_t p = dv->par;
+        CKI(qtts_dev_begin(dv, dv->nb, dv->max_frames > 4096 ? dv->max_frames : 4096, n, &p));
+    }
+    const qtts_dims_t &d = dv->d;
+    for (int b = 0; b < dv->nb; ++b) dv->p_len_h[b] = b == 0 ? n : 0;
+    CK(hipMemcpy(dv->prefill, embeds, (size_t)n * d.H * 4, hipMemcpyHostToDevice));
+    CKI(qtts_dev_prefill(dv));
+    if (hidden_out) {
+        GemvArgs a = gv(dv->head, d.V, d.H, dv->x_tk, d.H, dv->logits, d.V, 1, EPI_STORE);
+        a.norm_w = dv->tk_norm; a.eps = d.eps; a.xcopy = dv->tk_hid; a.ldxc = d.H; a.xcopy_normed = 1;
+        CKI(qtts_gemv(a, dv->st));
+        CK(hipMemcpyAsync(hidden_out, dv->tk_hid, (size_t)d.H * 4, hipMemcpyDeviceToHost, dv->st));
+        CK(hipStreamSynchronize(dv->st));
+    }
+    return 0;
+}
+
+extern "C" int qtts_dev_talker_forward_host(qtts_dev_t *dv, const float *embed, float *logits, float *hidden_out) {
+    if (!dv) return -1;
+    hipSetDevice(dv->device);
+    CKI(ensure_slot0(dv));
+    const qtts_dims_t &d = dv->d;
+    dv->nrun = 1;  // slot 0 only
+    int rc = 0;
+    if (hipMemcpy(dv->x_tk, embed, (size_t)d.H * 4, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+    if (!rc) rc = talker_layers(dv);
+    if (!rc) rc = talker_tail(dv);
+    dv->nrun = dv->nb;
+    CKI(rc);
+    int kl = 0;
+    CK(hipMemcpyAsync(&kl, dv->kv_len, 4, hipMemcpyDeviceToHost, dv->st));
+    CK(hipStreamSynchronize(dv->st));
+    kl += 1;
+    CK(hipMemcpy(dv->kv_len, &kl, 4, hipMemcpyHostToDevice));
+    if (logits) CK(hipMemcpy(logits, dv->logits, (size_t)d.V * 4, hipMemcpyDeviceToHost));
+    if (hidden_out) CK(hipMemcpy(hidden_out, dv->tk_hid, (size_t)d.H * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int qtts_dev_subtalker_host(qtts_dev_t *dv, const float *hidden, int first_code, int *out_codes) {
+    if (!dv) return -1;
+    hipSetDevice(dv->device);
+    CKI(ensure_slot0(dv));
+    const qtts_dims_t &d = dv->d;
+    CK(hipStreamSynchronize(dv->st));
+    CK(hipMemcpy(dv->tk_hid, hidden, (size_t)d.H * 4, hipMemcpyHostToDevice));
+    int zero = 0;
+    uint32_t sb = seed_bits(dv->par.seed);
+    CK(hipMemcpy(dv->cur_row, &zero, 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dv->stopped, &zero, 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dv->st_rng, &sb, 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dv->codes, &first_code, 4, hipMemcpyHostToDevice));
+    dv->nrun = 1;
+    int rc = subtalker(dv);
+    dv->nrun = dv->nb;
+    CKI(rc);
+    CK(hipMemcpyAsync(out_codes, dv->codes, (size_t)d.G * 4, hipMemcpyDeviceToHost, dv->st));
+    CK(hipStreamSynchronize(dv->st));
+    return 0;
+}
+
+extern "C" float *qtts_dev_codec_decode_host(qtts_dev_t *dv, const int *codes, int T, int *out_samples) {
+    if (out_samples) *out_samples = 0;
+    if (!dv || T < 1) return nullptr;
+    hipSetDevice(dv->device);
+    int *dc = nullptr;
+    if (hipMalloc(&dc, (size_t)T * dv->d.cq * 4) != hipSuccess) return nullptr;
+    float *r = nullptr;
+    if (hipMemcpy(dc, codes, (size_t)T * dv->d.cq * 4, hipMemcpyHostToDevice) == hipSuccess)
+        r = codec_decode(&dv->codec, dc, T, out_samples);
+    hipFree(dc);
+    return r;
+}
+
+// ----------------------------------------------------------------- kernel-level C-ABI
+extern "C" int qtts_hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int qtts_hip_sync(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }
+
+extern "C" int qtts_hip_matvec_bf16(float *out, const uint16_t *A, const float *x, int rows, int cols, int batch,
+                                    void *stream) {
+    GemvArgs a = gv(A, rows, cols, x, cols, out, rows, batch, EPI_STORE);
+    return qtts_gemv(a, (hipStream_t)stream);
+}
+
+extern "C" int qtts_hip_rmsnorm_matvec_bf16(float *out, const uint16_t *A, const float *x, const float *w, float eps,
+                                            int rows, int cols, int batch, void *stream) {
+    GemvArgs a = gv(A, rows, cols, x, cols, out, rows, batch, EPI_STORE);
+    a.norm_w = w; a.eps = eps;
+    return qtts_gemv(a, (hipStream_t)stream);
+}
+
+extern "C" int qtts_hip_sample_top_k(int *out, const float *logits, int vocab, int top_k, float top_p, float temp,
+                                     uint32_t *rng_bits, int batch, void *stream) {
+    SampArgs s;
+    s.logits = logits; s.ld = vocab; s.n = vocab; s.nb = batch; s.top_k = top_k; s.top_p = top_p; s.temp = temp;
+    s.mode = 0; s.st_rng = rng_bits; s.out_tok = out;
+    return qtts_sample(s, (hipStream_t)stream);
+}

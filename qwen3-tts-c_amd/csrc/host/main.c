@@ -1,0 +1,220 @@
+/*
+ * main.c - `qwen-tts` CLI on the MI355X hot path.
+ *
+ * Flags, defaults and the stderr lines the reference harness parses are the
+ * reference CLI's (c/main.c:25-69,126-173,266-271; regexes in
+ * scripts/benchmark_py_vs_c.py:104-138, test/test_eos_regression.py:20-28):
+ *   -d DIR -t IDS | -f FILE  -s SPK -l LANG -o OUT -v [-v]
+ *   --temperature --top-k --top-p --repetition-penalty --max-tokens
+ *   --fixed-codec-tokens --seed --subtalker-temperature --subtalker-top-k
+ *   --subtalker-top-p --benchmark-runs --benchmark-warmup
+ * Additions: --device N (HIP device), --batch N (N copies of the prompt in
+ * one lock-step batch; the first one's audio is written).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "../../../include/qwen_tts.h"
+
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1000.0 + (double)ts.tv_nsec / 1e6;
+}
+
+static void usage(const char *prog) {
+    fprintf(stderr,
+            "qwen-tts (MI355X / gfx950) - Qwen3-TTS talker + sub-talker decode and codec vocoder on the GPU\n\n"
+            "usage: %s -d <model_dir> (-t <ids> | -f <file>) [options]\n\n"
+            "  -d <dir>    model directory (config.json, *.safetensors, speech_tokenizer/)\n"
+            "  -t <ids>    comma-separated token ids in the chat template\n"
+            "  -f <file>   token ids from a file (comma- or newline-separated)\n"
+            "  -s <name>   speaker (config.json spk_id)      -l <lang>  language or auto\n"
+            "  -o <path>   output wav (default output.wav)   -v         verbose (repeatable)\n"
+            "  --temperature F (0.9)   --top-k N (50)   --top-p F (1.0)   --repetition-penalty F (1.05)\n"
+            "  --max-tokens N (4096)   --fixed-codec-tokens N   --seed N (42)\n"
+            "  --subtalker-temperature F (0.9)   --subtalker-top-k N (50)   --subtalker-top-p F (1.0)\n"
+            "  --benchmark-runs N (1)  --benchmark-warmup N (0)\n"
+            "  --device N (HIP device, default 0)   --batch N (lock-step batch of N copies, default 1)\n",
+            prog);
+}
+
+static char *read_ids_file(const char *path) {
+    FILE *f = fopen(path, "r");
+    if (!f) {
+        fprintf(stderr, "Error: cannot open token file: %s\n", path);
+        return NULL;
+    }
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    char *buf = (char *)malloc((size_t)n + 1);
+    if (!buf || fread(buf, 1, (size_t)n, f) != (size_t)n) {
+        free(buf);
+        fclose(f);
+        return NULL;
+    }
+    fclose(f);
+    buf[n] = 0;
+    for (long i = 0; i < n; i++)
+        if (buf[i] == '\n' || buf[i] == '\r') buf[i] = ',';
+    return buf;
+}
+
+static void progress(int step, int total, void *u) {
+    (void)total;
+    (void)u;
+    if (step % 50 == 0 || step < 5) {
+        fprintf(stderr, "\rGenerating... step %d", step);
+        fflush(stderr);
+    }
+}
+
+int main(int argc, char **argv) {
+    const char *dir = NULL, *ids = NULL, *ids_file = NULL, *spk = NULL, *lang = NULL, *out = "output.wav";
+    int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1;
+    float temp = -1, st_temp = -1, top_p = -1, st_top_p = -1, rep = -1;
+    int top_k = -1, st_top_k = -1, max_tokens = -1, fixed = -1, seed = -1;
+    for (int i = 1; i < argc; i++) {
+        const char *a = argv[i];
+        const int more = i + 1 < argc;
+#define ARG(flag) (!strcmp(a, flag) && more)
+        if (ARG("-d")) dir = argv[++i];
+        else if (ARG("-t")) ids = argv[++i];
+        else if (ARG("-f")) ids_file = argv[++i];
+        else if (ARG("-s")) spk = argv[++i];
+        else if (ARG("-l")) lang = argv[++i];
+        else if (ARG("-o")) out = argv[++i];
+        else if (!strcmp(a, "-v")) verbose++;
+        else if (ARG("--temperature")) temp = strtof(argv[++i], NULL);
+        else if (ARG("--top-k")) top_k = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--top-p")) top_p = strtof(argv[++i], NULL);
+        else if (ARG("--repetition-penalty")) rep = strtof(argv[++i], NULL);
+        else if (ARG("--max-tokens")) max_tokens = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--fixed-codec-tokens")) fixed = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--seed")) seed = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--subtalker-temperature")) st_temp = strtof(argv[++i], NULL);
+        else if (ARG("--subtalker-top-k")) st_top_k = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--subtalker-top-p")) st_top_p = strtof(argv[++i], NULL);
+        else if (ARG("--benchmark-runs")) runs = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--benchmark-warmup")) warmup = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--device")) device = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--batch")) batch = (int)strtol(argv[++i], NULL, 10);
+        else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); return 0; }
+        else {
+            fprintf(stderr, "Unknown option: %s\n", a);
+            usage(argv[0]);
+            return 1;
+        }
+#undef ARG
+    }
+    if (!dir) { fprintf(stderr, "Error: model directory required (-d)\n\n"); usage(argv[0]); return 1; }
+    if (!ids && !ids_file) { fprintf(stderr, "Error: token IDs required (-t or -f)\n\n"); usage(argv[0]); return 1; }
+    if (runs < 1 || warmup < 0 || batch < 1) {
+        fprintf(stderr, "Error: invalid benchmark settings (--benchmark-runs >= 1, --benchmark-warmup >= 0)\n");
+        return 1;
+    }
+    char *file_ids = NULL;
+    if (ids_file) {
+        if (!(file_ids = read_ids_file(ids_file))) return 1;
+        ids = file_ids;
+    }
+    qwen_tts_verbose = verbose;
+    if (device >= 0) qwen_tts_set_device(device);
+    if (verbose >= 1) fprintf(stderr, "Loading model from %s...\n", dir);
+    qwen_tts_ctx_t *ctx = qwen_tts_load(dir);
+    if (!ctx) {
+        fprintf(stderr, "Error: failed to load model\n");
+        free(file_ids);
+        return 1;
+    }
+    if (temp >= 0) ctx->temperature = temp;
+    if (st_temp >= 0) ctx->subtalker_temperature = st_temp;
+    if (top_k >= 0) ctx->top_k = top_k;
+    if (st_top_k >= 0) ctx->subtalker_top_k = st_top_k;
+    if (top_p >= 0) ctx->top_p = top_p;
+    if (st_top_p >= 0) ctx->subtalker_top_p = st_top_p;
+    if (rep >= 0) ctx->repetition_penalty = rep;
+    if (max_tokens >= 0) ctx->max_new_tokens = max_tokens;
+    if (fixed >= 0) ctx->fixed_codec_tokens = fixed;
+    if (seed >= 0) ctx->sample_seed = seed;
+    if (verbose == 0) qwen_tts_set_progress_callback(ctx, progress, NULL);
+    if (verbose >= 1) {
+        fprintf(stderr, "Generation params: temp=%.2f top_k=%d top_p=%.2f rep_penalty=%.2f max_tokens=%d\n",
+                ctx->temperature, ctx->top_k, ctx->top_p, ctx->repetition_penalty, ctx->max_new_tokens);
+        if (ctx->fixed_codec_tokens > 0) fprintf(stderr, "Fixed codec tokens: %d\n", ctx->fixed_codec_tokens);
+        fprintf(stderr, "Seed: %d\n", ctx->sample_seed);
+        if (spk) fprintf(stderr, "Speaker: %s\n", spk);
+        if (lang) fprintf(stderr, "Language: %s\n", lang);
+    }
+    float *audio = NULL;
+    int n_samples = 0, rc = 0;
+    for (int run = 0; run < warmup + runs; run++) {
+        const double t0 = now_ms();
+        float *ra = NULL;
+        int rn = 0;
+        long total_samples = 0;
+        if (batch == 1) {
+            ra = qwen_tts_generate(ctx, ids, spk, lang, &rn);
+            total_samples = rn;
+        } else {
+            const char **tx = (const char **)malloc(batch * sizeof(char *));
+            const char **sp = (const char **)malloc(batch * sizeof(char *));
+            const char **lg = (const char **)malloc(batch * sizeof(char *));
+            float **au = (float **)calloc(batch, sizeof(float *));
+            int *ns = (int *)calloc(batch, sizeof(int));
+            for (int b = 0; b < batch; b++) { tx[b] = ids; sp[b] = spk; lg[b] = lang; }
+            if (qwen_tts_generate_batch(ctx, batch, tx, sp, lg, au, ns) == 0) {
+                ra = au[0];
+                rn = ns[0];
+                for (int b = 0; b < batch; b++) total_samples += ns[b];
+            }
+            for (int b = 1; b < batch; b++) free(au[b]);
+            free(tx); free(sp); free(lg); free(au); free(ns);
+        }
+        const double el = now_ms() - t0;
+        if (verbose == 0) fprintf(stderr, "\n");
+        if (!ra || rn == 0) {
+            fprintf(stderr, "Error: generation produced no audio\n");
+            free(ra);
+            rc = 1;
+            break;
+        }
+        const int mi = run - warmup;
+        if (mi >= 0 && runs > 1)
+            fprintf(stderr,
+                    "[persistent] run %d/%d: elapsed=%.1f ms, audio=%.2fs, talker=%.1f ms, codec=%.1f ms, "
+                    "total=%.1f ms, tokens=%d\n",
+                    mi + 1, runs, el, (float)total_samples / QWEN_TTS_SAMPLE_RATE, ctx->perf_talker_ms,
+                    ctx->perf_codec_ms, ctx->perf_total_ms, ctx->perf_codec_tokens);
+        free(audio);
+        audio = ra;
+        n_samples = rn;
+    }
+    if (rc == 0) {
+        if (qwen_tts_write_wav(out, audio, n_samples, QWEN_TTS_SAMPLE_RATE) != 0) {
+            fprintf(stderr, "Error: failed to write %s\n", out);
+            rc = 1;
+        } else {
+            const float dur = (float)n_samples / QWEN_TTS_SAMPLE_RATE;
+            fprintf(stderr, "Wrote %s: %.2f seconds (%d samples at %d Hz)\n", out, dur, n_samples,
+                    QWEN_TTS_SAMPLE_RATE);
+            if (verbose >= 1) {
+                fprintf(stderr, "\nPerformance:\n");
+                fprintf(stderr, "  Talker:  %.1f ms (%d tokens, %.1f ms/token)\n", ctx->perf_talker_ms,
+                        ctx->perf_codec_tokens,
+                        ctx->perf_codec_tokens > 0 ? ctx->perf_talker_ms / ctx->perf_codec_tokens : 0);
+                fprintf(stderr, "  Codec:   %.1f ms\n", ctx->perf_codec_ms);
+                fprintf(stderr, "  Total:   %.1f ms\n", ctx->perf_total_ms);
+                fprintf(stderr, "  RTF:     %.2fx realtime\n", dur > 0 ? dur / (ctx->perf_total_ms / 1000.0) : 0);
+                fprintf(stderr, "  First frame: %.1f ms\n", ctx->perf_first_frame_ms);
+            }
+        }
+    }
+    free(audio);
+    qwen_tts_free(ctx);
+    free(file_ids);
+    return rc;
+}

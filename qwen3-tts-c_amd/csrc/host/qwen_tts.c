@@ -1,0 +1,621 @@
+/*
+ * qwen_tts.c - C host for the MI355X hot path: config + checkpoint loading,
+ * prompt layout, the per-frame decode loop and the public qwen_tts.h API.
+ *
+ * The arithmetic runs on the GPU through include/qtts_hip.h; this file owns
+ * what the reference's c/qwen_tts.c owns on the host side:
+ *   - config keys and defaults          (c/qwen_tts.c:235-355)
+ *   - speaker / language lookup         (c/qwen_tts.c:1120-1145)
+ *   - prompt layout (streaming layout)  (c/qwen_tts.c:1147-1243)
+ *   - the generation loop, stop rules, progress callback, stderr lines and
+ *     perf counters                     (c/qwen_tts.c:1258-1443)
+ */
+#define _GNU_SOURCE
+#include "../../../include/qwen_tts.h"
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../../../include/qtts_hip.h"
+#include "qjson.h"
+
+int qwen_tts_verbose = 0;
+static int g_device = -1;
+
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1000.0 + (double)ts.tv_nsec / 1e6;
+}
+
+void qwen_tts_set_device(int device) { g_device = device; }
+
+/* ------------------------------------------------------------------ config */
+static void read_map(const qj_t *root, const char *path, int *n, char ***names, int **ids) {
+    const qj_t *m = qj_path(root, path);
+    *n = 0;
+    *names = NULL;
+    *ids = NULL;
+    if (!m || m->type != QJ_OBJ || m->n == 0) return;
+    *names = (char **)calloc(m->n, sizeof(char *));
+    *ids = (int *)calloc(m->n, sizeof(int));
+    for (int i = 0; i < m->n; i++) {
+        const qj_t *v = m->items[i];
+        int id = -1;
+        if (v->type == QJ_NUM) id = (int)v->num;
+        else if (v->type == QJ_ARR && v->n > 0 && v->items[0]->type == QJ_NUM) id = (int)v->items[0]->num;
+        (*names)[*n] = strdup(m->keys[i]);
+        (*ids)[*n] = id;
+        (*n)++;
+    }
+}
+
+static int load_config(qwen_tts_ctx_t *ctx) {
+    qwen_tts_config_t *c = &ctx->config;
+    char path[1100];
+    size_t len = 0;
+    snprintf(path, sizeof path, "%s/config.json", ctx->model_dir);
+    char *txt = qj_read_file(path, &len);
+    if (!txt) { fprintf(stderr, "Error: cannot read %s\n", path); return -1; }
+    qj_t *js = qj_parse(txt, len);
+    free(txt);
+    if (!js) { fprintf(stderr, "Error: cannot parse %s\n", path); return -1; }
+#define TI(f, k, d) c->f = qj_int(js, "talker_config." k, d)
+    TI(talker_vocab_size, "vocab_size", QWEN_TTS_TALKER_VOCAB);
+    TI(talker_hidden, "hidden_size", QWEN_TTS_TALKER_HIDDEN);
+    TI(talker_intermediate, "intermediate_size", QWEN_TTS_TALKER_INTERMEDIATE);
+    TI(talker_layers, "num_hidden_layers", QWEN_TTS_TALKER_LAYERS);
+    TI(talker_heads, "num_attention_heads", QWEN_TTS_TALKER_HEADS);
+    TI(talker_kv_heads, "num_key_value_heads", QWEN_TTS_TALKER_KV_HEADS);
+    TI(talker_head_dim, "head_dim", 0);
+    if (c->talker_head_dim <= 0 && c->talker_heads > 0) c->talker_head_dim = c->talker_hidden / c->talker_heads;
+    TI(talker_text_hidden, "text_hidden_size", QWEN_TTS_TALKER_TEXT_HIDDEN);
+    TI(talker_text_vocab, "text_vocab_size", QWEN_TTS_TALKER_TEXT_VOCAB);
+    TI(num_code_groups, "num_code_groups", QWEN_TTS_NUM_CODE_GROUPS);
+    c->talker_rms_norm_eps = qj_float(js, "talker_config.rms_norm_eps", 1e-6f);
+    c->talker_rope_theta = qj_float(js, "talker_config.rope_theta", 10000.0f);
+    c->mrope_section[0] = 16; c->mrope_section[1] = 16; c->mrope_section[2] = 0;
+    qj_ints(js, "talker_config.rope_scaling.mrope_section", c->mrope_section, 3);
+    TI(subtalker_vocab_size, "code_predictor_config.vocab_size", QWEN_TTS_SUBTALKER_VOCAB);
+    TI(subtalker_hidden, "code_predictor_config.hidden_size", QWEN_TTS_SUBTALKER_HIDDEN);
+    TI(subtalker_intermediate, "code_predictor_config.intermediate_size", QWEN_TTS_SUBTALKER_INTERMEDIATE);
+    TI(subtalker_layers, "code_predictor_config.num_hidden_layers", QWEN_TTS_SUBTALKER_LAYERS);
+    TI(subtalker_heads, "code_predictor_config.num_attention_heads", QWEN_TTS_SUBTALKER_HEADS);
+    TI(subtalker_kv_heads, "code_predictor_config.num_key_value_heads", QWEN_TTS_SUBTALKER_KV_HEADS);
+    TI(subtalker_head_dim, "code_predictor_config.head_dim", QWEN_TTS_SUBTALKER_HEAD_DIM);
+    TI(codec_pad_id, "codec_pad_id", QWEN_TTS_CODEC_PAD);
+    TI(codec_bos_id, "codec_bos_id", QWEN_TTS_CODEC_BOS);
+    TI(codec_eos_id, "codec_eos_token_id", QWEN_TTS_CODEC_EOS);
+    TI(codec_nothink_id, "codec_nothink_id", QWEN_TTS_CODEC_NOTHINK);
+    TI(codec_think_id, "codec_think_id", QWEN_TTS_CODEC_THINK);
+    TI(codec_think_bos_id, "codec_think_bos_id", QWEN_TTS_CODEC_THINK_BOS);
+    TI(codec_think_eos_id, "codec_think_eos_id", QWEN_TTS_CODEC_THINK_EOS);
+#undef TI
+    read_map(js, "talker_config.spk_id", &c->n_speakers, &c->speaker_names, &c->speaker_ids);
+    read_map(js, "talker_config.codec_language_id", &c->n_languages, &c->language_names, &c->language_ids);
+    qj_free(js);
+    if (c->talker_heads <= 0 || c->talker_kv_heads <= 0 || c->talker_head_dim <= 0) {
+        fprintf(stderr, "Error: invalid talker attention config (heads=%d kv_heads=%d head_dim=%d)\n",
+                c->talker_heads, c->talker_kv_heads, c->talker_head_dim);
+        return -1;
+    }
+    if (c->talker_heads % c->talker_kv_heads != 0) {
+        fprintf(stderr, "Error: talker heads (%d) must be divisible by kv heads (%d)\n", c->talker_heads,
+                c->talker_kv_heads);
+        return -1;
+    }
+    if (c->talker_head_dim > 512 || c->subtalker_head_dim > 512) {
+        fprintf(stderr, "Error: unsupported head_dim (talker=%d subtalker=%d, max=512)\n", c->talker_head_dim,
+                c->subtalker_head_dim);
+        return -1;
+    }
+    if (c->num_code_groups > QWEN_TTS_NUM_CODE_GROUPS) {
+        fprintf(stderr, "Error: num_code_groups %d > %d\n", c->num_code_groups, QWEN_TTS_NUM_CODE_GROUPS);
+        return -1;
+    }
+
+    snprintf(path, sizeof path, "%s/speech_tokenizer/config.json", ctx->model_dir);
+    txt = qj_read_file(path, &len);
+    if (!txt) { fprintf(stderr, "Error: cannot read %s\n", path); return -1; }
+    js = qj_parse(txt, len);
+    free(txt);
+    if (!js) { fprintf(stderr, "Error: cannot parse %s\n", path); return -1; }
+#define DI(f, k, d) c->f = qj_int(js, "decoder_config." k, d)
+    DI(codec_num_quantizers, "num_quantizers", QWEN_TTS_CODEC_NUM_QUANTIZERS);
+    DI(codec_codebook_size, "codebook_size", QWEN_TTS_CODEC_CODEBOOK_SIZE);
+    DI(codec_codebook_dim, "codebook_dim", 128);
+    DI(codec_hidden, "hidden_size", QWEN_TTS_CODEC_HIDDEN);
+    DI(codec_latent, "latent_dim", QWEN_TTS_CODEC_LATENT);
+    DI(codec_layers, "num_hidden_layers", QWEN_TTS_CODEC_LAYERS);
+    DI(codec_heads, "num_attention_heads", QWEN_TTS_CODEC_HEADS);
+    DI(codec_kv_heads, "num_key_value_heads", QWEN_TTS_CODEC_KV_HEADS);
+    DI(codec_intermediate, "intermediate_size", QWEN_TTS_CODEC_INTERMEDIATE);
+    DI(codec_sliding_window, "sliding_window", QWEN_TTS_CODEC_SLIDING_WINDOW);
+    DI(codec_decoder_dim, "decoder_dim", QWEN_TTS_CODEC_DECODER_DIM);
+#undef DI
+    c->codec_rms_norm_eps = qj_float(js, "decoder_config.rms_norm_eps", 1e-5f);
+    c->codec_layer_scale = qj_float(js, "decoder_config.layer_scale_initial_scale", 0.01f);
+    int rates[4] = {8, 5, 4, 3}, ratios[2] = {2, 2};
+    qj_ints(js, "decoder_config.upsample_rates", rates, 4);
+    qj_ints(js, "decoder_config.upsampling_ratios", ratios, 2);
+    memcpy(c->codec_upsample_rates, rates, sizeof rates);
+    memcpy(c->codec_upsampling_ratios, ratios, sizeof ratios);
+    qj_free(js);
+    if (qwen_tts_verbose >= 1) {
+        fprintf(stderr, "Config loaded:\n");
+        fprintf(stderr, "  Talker: %d layers, hidden=%d, heads=%d/%d, head_dim=%d\n", c->talker_layers,
+                c->talker_hidden, c->talker_heads, c->talker_kv_heads, c->talker_head_dim);
+        fprintf(stderr, "  Sub-talker: %d layers, hidden=%d, heads=%d/%d, head_dim=%d\n", c->subtalker_layers,
+                c->subtalker_hidden, c->subtalker_heads, c->subtalker_kv_heads, c->subtalker_head_dim);
+        fprintf(stderr, "  Codec: %d layers, hidden=%d, codebook_dim=%d, decoder_dim=%d\n", c->codec_layers,
+                c->codec_hidden, c->codec_codebook_dim, c->codec_decoder_dim);
+        fprintf(stderr, "  Speakers: %d, Languages: %d\n", c->n_speakers, c->n_languages);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------- checkpoint */
+static int cmp_name(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
+
+static int is_talker_attn_proj(const char *n) {
+    if (strncmp(n, "talker.model.layers.", 20) != 0) return 0;
+    const char *s = strstr(n, ".self_attn.");
+    return s && s[11] && strchr("qkvo", s[11]) && !strcmp(s + 12, "_proj.weight");
+}
+
+/* mmap one .safetensors file and hand every tensor to the device */
+static int upload_file(qtts_dev_t *dev, const char *path) {
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) { fprintf(stderr, "Error: cannot open %s\n", path); return -1; }
+    struct stat st;
+    if (fstat(fd, &st) < 0 || st.st_size < 8) { close(fd); return -1; }
+    size_t size = (size_t)st.st_size;
+    uint8_t *base = (uint8_t *)mmap(NULL, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (base == MAP_FAILED) { fprintf(stderr, "Error: mmap failed for %s\n", path); return -1; }
+    uint64_t hlen;
+    memcpy(&hlen, base, 8);
+    int rc = -1;
+    qj_t *hdr = NULL;
+    if (hlen + 8 > size || !(hdr = qj_parse((const char *)base + 8, (size_t)hlen)) || hdr->type != QJ_OBJ) {
+        fprintf(stderr, "Error: bad safetensors header in %s\n", path);
+        goto done;
+    }
+    const uint8_t *data = base + 8 + hlen;
+    for (int i = 0; i < hdr->n; i++) {
+        const char *name = hdr->keys[i];
+        const qj_t *e = hdr->items[i];
+        if (!strcmp(name, "__metadata__")) continue;
+        const qj_t *dt = qj_get(e, "dtype"), *sh = qj_get(e, "shape"), *off = qj_get(e, "data_offsets");
+        if (!dt || dt->type != QJ_STR || !sh || sh->type != QJ_ARR || !off || off->type != QJ_ARR || off->n != 2) {
+            fprintf(stderr, "Error: malformed entry %s in %s\n", name, path);
+            goto done;
+        }
+        int dtype = !strcmp(dt->str, "F32") ? 0 : !strcmp(dt->str, "BF16") ? 1 : !strcmp(dt->str, "F16") ? 2 : -1;
+        if (is_talker_attn_proj(name) && dtype != 1) {  /* c/qwen_tts.c:389-393 */
+            fprintf(stderr, "Error: tensor %s dtype mismatch: expected BF16, got %s\n", name, dt->str);
+            goto done;
+        }
+        if (dtype < 0) continue;
+        int64_t shape[8];
+        int nd = sh->n < 8 ? sh->n : 8;
+        size_t n = 1;
+        for (int k = 0; k < nd; k++) { shape[k] = (int64_t)sh->items[k]->num; n *= (size_t)shape[k]; }
+        size_t a = (size_t)off->items[0]->num, b = (size_t)off->items[1]->num;
+        size_t esz = dtype == 0 ? 4 : 2;
+        if (b < a || b - a != n * esz || 8 + hlen + b > size) {
+            fprintf(stderr, "Error: tensor %s has inconsistent size in %s\n", name, path);
+            goto done;
+        }
+        if (qtts_dev_put_tensor(dev, name, data + a, dtype, shape, nd) != 0) goto done;
+    }
+    rc = 0;
+done:
+    qj_free(hdr);
+    munmap(base, size);
+    return rc;
+}
+
+static int upload_dir(qtts_dev_t *dev, const char *dir) {
+    DIR *d = opendir(dir);
+    if (!d) { fprintf(stderr, "Error: cannot open directory %s\n", dir); return -1; }
+    char **names = NULL;
+    int n = 0, cap = 0;
+    struct dirent *ent;
+    while ((ent = readdir(d))) {
+        const char *dot = strrchr(ent->d_name, '.');
+        if (!dot || strcmp(dot, ".safetensors")) continue;
+        if (n == cap) { cap = cap ? cap * 2 : 8; names = (char **)realloc(names, cap * sizeof(char *)); }
+        names[n++] = strdup(ent->d_name);
+    }
+    closedir(d);
+    if (n == 0) { fprintf(stderr, "Error: no .safetensors files in %s\n", dir); free(names); return -1; }
+    qsort(names, n, sizeof(char *), cmp_name);
+    int rc = 0;
+    for (int i = 0; i < n; i++) {
+        char p[1400];
+        snprintf(p, sizeof p, "%s/%s", dir, names[i]);
+        if (!rc && upload_file(dev, p)) rc = -1;
+        free(names[i]);
+    }
+    free(names);
+    return rc;
+}
+
+static void dims_of(const qwen_tts_config_t *c, qtts_dims_t *d) {
+    memset(d, 0, sizeof *d);
+    d->H = c->talker_hidden; d->I = c->talker_intermediate; d->L = c->talker_layers; d->NH = c->talker_heads;
+    d->KV = c->talker_kv_heads; d->HD = c->talker_head_dim; d->TH = c->talker_text_hidden;
+    d->TV = c->talker_text_vocab; d->V = c->talker_vocab_size; d->G = c->num_code_groups;
+    d->Hs = c->subtalker_hidden; d->Is = c->subtalker_intermediate; d->Ls = c->subtalker_layers;
+    d->NHs = c->subtalker_heads; d->KVs = c->subtalker_kv_heads; d->HDs = c->subtalker_head_dim;
+    d->Vs = c->subtalker_vocab_size;
+    d->eps = c->talker_rms_norm_eps; d->theta = c->talker_rope_theta;
+    d->cq = c->codec_num_quantizers; d->ccb = c->codec_codebook_size; d->ccbdim = c->codec_codebook_dim;
+    d->chid = c->codec_hidden; d->clat = c->codec_latent; d->clayers = c->codec_layers; d->cheads = c->codec_heads;
+    d->ckv = c->codec_kv_heads; d->cinter = c->codec_intermediate; d->cwin = c->codec_sliding_window;
+    d->cdec = c->codec_decoder_dim;
+    memcpy(d->rates, c->codec_upsample_rates, sizeof d->rates);
+    memcpy(d->ratios, c->codec_upsampling_ratios, sizeof d->ratios);
+    d->ceps = c->codec_rms_norm_eps;
+    d->pad_id = c->codec_pad_id; d->bos_id = c->codec_bos_id; d->eos_id = c->codec_eos_id;
+}
+
+qwen_tts_ctx_t *qwen_tts_load(const char *model_dir) {
+    double t0 = now_ms();
+    qwen_tts_ctx_t *ctx = (qwen_tts_ctx_t *)calloc(1, sizeof(qwen_tts_ctx_t));
+    if (!ctx) return NULL;
+    snprintf(ctx->model_dir, sizeof ctx->model_dir, "%s", model_dir);
+    ctx->temperature = 0.9f;      /* c/qwen_tts.c:871-880 */
+    ctx->subtalker_temperature = 0.9f;
+    ctx->top_k = 50;
+    ctx->subtalker_top_k = 50;
+    ctx->top_p = 1.0f;
+    ctx->subtalker_top_p = 1.0f;
+    ctx->repetition_penalty = 1.05f;
+    ctx->max_new_tokens = 4096;
+    ctx->fixed_codec_tokens = 0;
+    ctx->sample_seed = 42;
+    if (load_config(ctx) != 0) { qwen_tts_free(ctx); return NULL; }
+    int dev_id = g_device;
+    if (dev_id < 0) {
+        const char *e = getenv("QWEN_TTS_HIP_DEVICE");
+        dev_id = e ? atoi(e) : 0;
+    }
+    if (qtts_hip_device_count() <= dev_id) {
+        fprintf(stderr, "Error: no HIP device %d available (MI355X / gfx950 required)\n", dev_id);
+        qwen_tts_free(ctx);
+        return NULL;
+    }
+    ctx->hip_device = dev_id;
+    qtts_dims_t dims;
+    dims_of(&ctx->config, &dims);
+    qtts_dev_t *dev = qtts_dev_create(&dims, dev_id);
+    if (!dev) { qwen_tts_free(ctx); return NULL; }
+    ctx->hip = dev;
+    char cdir[1100];
+    snprintf(cdir, sizeof cdir, "%s/speech_tokenizer", model_dir);
+    if (upload_dir(dev, model_dir) != 0 || upload_dir(dev, cdir) != 0 || qtts_dev_finalize(dev) != 0) {
+        qwen_tts_free(ctx);
+        return NULL;
+    }
+    ctx->tk_x = (float *)calloc(ctx->config.talker_hidden, sizeof(float));
+    if (qwen_tts_verbose >= 1)
+        fprintf(stderr, "Model loaded in %.1f ms (%.2f GB weights on HIP device %d)\n", now_ms() - t0,
+                (double)qtts_dev_bytes(dev, 0) / 1e9, dev_id);
+    return ctx;
+}
+
+void qwen_tts_free(qwen_tts_ctx_t *ctx) {
+    if (!ctx) return;
+    if (ctx->hip) qtts_dev_destroy((qtts_dev_t *)ctx->hip);
+    for (int i = 0; i < ctx->config.n_speakers; i++) free(ctx->config.speaker_names[i]);
+    free(ctx->config.speaker_names);
+    free(ctx->config.speaker_ids);
+    for (int i = 0; i < ctx->config.n_languages; i++) free(ctx->config.language_names[i]);
+    free(ctx->config.language_names);
+    free(ctx->config.language_ids);
+    free(ctx->last_codes);
+    free(ctx->tk_x);
+    free(ctx);
+}
+
+void qwen_tts_set_progress_callback(qwen_tts_ctx_t *ctx, qwen_tts_progress_cb cb, void *userdata) {
+    ctx->progress_cb = cb;
+    ctx->progress_cb_userdata = userdata;
+}
+
+/* ------------------------------------------------------------------ prompt */
+static int parse_ids(const char *text, int **out) {
+    *out = NULL;
+    if (!text) return 0;
+    int cap = 1;
+    for (const char *p = text; *p; p++) cap += *p == ',';
+    int *ids = (int *)malloc(cap * sizeof(int)), n = 0;
+    const char *p = text;
+    while (*p && n < cap) {
+        while (*p == ' ' || *p == ',') p++;
+        if (!*p) break;
+        char *end = NULL;
+        long v = strtol(p, &end, 10);
+        if (end == p) {
+            fprintf(stderr, "Error: invalid token ID near '%s'\n", p);
+            free(ids);
+            return -1;
+        }
+        ids[n++] = (int)v;
+        p = end;
+    }
+    *out = ids;
+    return n;
+}
+
+typedef struct {
+    int *text;  /* text ids to project */
+    int n_text;
+    int *plan;  /* 5 ints per row */
+    int nplan;
+    int p_len, n_trailing, pad_row;
+} prompt_t;
+
+/* Streaming prompt layout of c/qwen_tts.c:1147-1243:
+ *   prefill = proj(ids[0:3]),
+ *             (tts_pad x (np-2), tts_bos) + codec_emb(prefix[0:np-1]),
+ *             proj(ids[3]) + codec_emb(bos)
+ *   trailing = proj(ids[4:-5]) ++ tts_eos; tts_pad once exhausted */
+static int build_prompt(const qwen_tts_ctx_t *ctx, const int *ids, int n, int spk, int lang, int b, prompt_t *pr) {
+    const qwen_tts_config_t *c = &ctx->config;
+    int prefix[8], np = 0;
+    if (lang < 0) {
+        prefix[np++] = c->codec_nothink_id; prefix[np++] = c->codec_think_bos_id; prefix[np++] = c->codec_think_eos_id;
+    } else {
+        prefix[np++] = c->codec_think_id; prefix[np++] = c->codec_think_bos_id; prefix[np++] = lang;
+        prefix[np++] = c->codec_think_eos_id;
+    }
+    if (spk >= 0) prefix[np++] = spk;
+    prefix[np++] = c->codec_pad_id;
+    prefix[np++] = c->codec_bos_id;
+    int nt = (n - 4 - 5) + 1;
+    if (nt < 1) nt = 1;
+    pr->n_text = 7 + (nt - 1);
+    pr->text = (int *)malloc(pr->n_text * sizeof(int));
+    pr->plan = (int *)malloc((size_t)(3 + np + nt) * 5 * sizeof(int));
+    int *t = pr->text;
+    t[0] = ids[0]; t[1] = ids[1]; t[2] = ids[2];
+    t[3] = QWEN_TTS_TOKEN_TTS_PAD; t[4] = QWEN_TTS_TOKEN_TTS_BOS; t[5] = QWEN_TTS_TOKEN_TTS_EOS; t[6] = ids[3];
+    for (int i = 0; i < nt - 1; i++) t[7 + i] = ids[4 + i];
+    int k = 0;
+#define ROW(src, cid, kind, slot) do { int *r_ = pr->plan + 5 * k++; r_[0] = src; r_[1] = cid; r_[2] = kind; r_[3] = b; r_[4] = slot; } while (0)
+    for (int i = 0; i < 3; i++) ROW(i, -1, 0, i);
+    for (int i = 0; i < np - 1; i++) ROW(i < np - 2 ? 3 : 4, prefix[i], 0, 3 + i);
+    ROW(6, c->codec_bos_id, 0, 3 + np - 1);
+    for (int i = 0; i < nt - 1; i++) ROW(7 + i, -1, 1, i);
+    ROW(5, -1, 1, nt - 1);
+#undef ROW
+    pr->nplan = k;
+    pr->p_len = 3 + np;
+    pr->n_trailing = nt;
+    pr->pad_row = 3;
+    return 0;
+}
+
+static void lookup(const qwen_tts_ctx_t *ctx, const char *speaker, const char *language, int *spk, int *lang) {
+    const qwen_tts_config_t *c = &ctx->config;
+    *spk = -1;
+    *lang = -1;
+    if (speaker && strlen(speaker) > 0) {
+        for (int i = 0; i < c->n_speakers; i++)
+            if (strcasecmp(c->speaker_names[i], speaker) == 0) { *spk = c->speaker_ids[i]; break; }
+        if (*spk < 0) fprintf(stderr, "Warning: speaker '%s' not found, using no speaker embedding\n", speaker);
+    }
+    if (language && strlen(language) > 0 && strcasecmp(language, "auto") != 0) {
+        for (int i = 0; i < c->n_languages; i++)
+            if (strcasecmp(c->language_names[i], language) == 0) { *lang = c->language_ids[i]; break; }
+        if (*lang < 0) fprintf(stderr, "Warning: language '%s' not found\n", language);
+    }
+}
+
+static void params_of(const qwen_tts_ctx_t *ctx, qtts_gen_params_t *p) {
+    p->temperature = ctx->temperature; p->top_p = ctx->top_p; p->repetition_penalty = ctx->repetition_penalty;
+    p->top_k = ctx->top_k; p->st_temperature = ctx->subtalker_temperature; p->st_top_p = ctx->subtalker_top_p;
+    p->st_top_k = ctx->subtalker_top_k; p->fixed_codec_tokens = ctx->fixed_codec_tokens; p->seed = ctx->sample_seed;
+}
+
+/* ------------------------------------------------------------- generation */
+/* Runs nb utterances in lock-step frames.  Fills per-slot frame counts and
+ * stop info; audio[i] decoded per slot.  Returns 0 on success. */
+static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
+                     const char *const *languages, float **audio, int *samples, double t_start) {
+    qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
+    const qwen_tts_config_t *c = &ctx->config;
+    const int G = c->num_code_groups;
+    int rc = -1;
+    prompt_t *pr = (prompt_t *)calloc(nb, sizeof(prompt_t));
+    int max_p = 0;
+    for (int b = 0; b < nb; b++) {
+        int *ids = NULL;
+        int n = parse_ids(texts[b], &ids);
+        if (n < 8) {
+            if (n >= 0) fprintf(stderr, "Error: need at least 8 text tokens (chat template format)\n");
+            free(ids);
+            goto out;
+        }
+        for (int i = 0; i < n; i++)
+            if (ids[i] < 0 || ids[i] >= c->talker_text_vocab) {
+                fprintf(stderr, "Error: text token id %d out of range\n", ids[i]);
+                free(ids);
+                goto out;
+            }
+        int spk, lang;
+        lookup(ctx, speakers ? speakers[b] : NULL, languages ? languages[b] : NULL, &spk, &lang);
+        build_prompt(ctx, ids, n, spk, lang, b, &pr[b]);
+        free(ids);
+        if (pr[b].p_len > max_p) max_p = pr[b].p_len;
+    }
+    const int fixed = ctx->fixed_codec_tokens > 0 ? ctx->fixed_codec_tokens : 0;
+    const int max_tokens = fixed > 0 ? fixed : ctx->max_new_tokens;
+    if (max_tokens < 1) goto out;
+    qtts_gen_params_t gp;
+    params_of(ctx, &gp);
+    if (qtts_dev_begin(dev, nb, max_tokens, max_p, &gp) != 0) goto out;
+    for (int b = 0; b < nb; b++)
+        if (qtts_dev_prompt(dev, b, pr[b].text, pr[b].n_text, pr[b].plan, pr[b].nplan, pr[b].p_len,
+                            pr[b].n_trailing, pr[b].pad_row) != 0)
+            goto out;
+    double t_prefill = now_ms();
+    if (qtts_dev_prefill(dev) != 0) goto out;
+    double t_prefill_done = now_ms();
+    ctx->perf_prefill_ms = t_prefill_done - t_prefill;
+    if (qwen_tts_verbose >= 1) {
+        fprintf(stderr, "Talker prefill complete: %d tokens\n", pr[0].p_len);
+        fprintf(stderr, "Prefill: %d tokens in %.1f ms\n", pr[0].p_len, t_prefill_done - t_prefill);
+    }
+    int *stopped = (int *)calloc(nb, sizeof(int)), *ngen = (int *)calloc(nb, sizeof(int));
+    int *sstep = (int *)calloc(nb, sizeof(int));
+    double t_gen = now_ms();
+    const int poll_every = fixed > 0 ? 0 : 8;
+    int step = 0;
+    for (; step < max_tokens; step++) {
+        if (qtts_dev_frame(dev, step) != 0) { free(stopped); free(ngen); free(sstep); goto out; }
+        if (step == 0) {
+            qtts_dev_poll(dev, NULL, NULL, NULL);
+            ctx->perf_first_frame_ms = now_ms() - t_start;
+        }
+        if (ctx->progress_cb) ctx->progress_cb(step + 1, max_tokens, ctx->progress_cb_userdata);
+        if (poll_every && ((step + 1) % poll_every == 0 || step + 1 == max_tokens)) {
+            qtts_dev_poll(dev, stopped, ngen, sstep);
+            int all = 1;
+            for (int b = 0; b < nb; b++) all &= stopped[b];
+            if (qwen_tts_verbose >= 1 && ngen[0] > 0 && ngen[0] % 10 < poll_every)
+                fprintf(stderr, "\r  Token %d (%.1f ms/token)...", ngen[0], (now_ms() - t_gen) / ngen[0]);
+            if (all) break;
+        }
+    }
+    qtts_dev_poll(dev, stopped, ngen, sstep);
+    double t_gen_done = now_ms();
+    ctx->perf_talker_ms = t_gen_done - t_gen;
+    ctx->perf_codec_tokens = ngen[0];
+    ctx->last_stop_reason = stopped[0] ? 1 : 2;
+    ctx->last_stop_step = stopped[0] ? sstep[0] : max_tokens;
+    free(ctx->last_codes);
+    ctx->last_codes = (int *)malloc((size_t)(ngen[0] > 0 ? ngen[0] : 1) * G * sizeof(int));
+    ctx->last_frames = ngen[0] > 0 ? qtts_dev_get_codes(dev, 0, ctx->last_codes, ngen[0]) : 0;
+    if (qwen_tts_verbose >= 1) {
+        if (stopped[0]) fprintf(stderr, "EOS at step %d\n", sstep[0]);
+        fprintf(stderr, "\r                                        \r");
+        fprintf(stderr, "Generated %d codec tokens in %.1f ms (%.1f ms/token)\n", ngen[0], ctx->perf_talker_ms,
+                ngen[0] > 0 ? ctx->perf_talker_ms / ngen[0] : 0);
+        fprintf(stderr, "Stop: %s at step %d\n", stopped[0] ? "eos" : "max_tokens", ctx->last_stop_step);
+        if (qwen_tts_verbose >= 2) {
+            fprintf(stderr, "Token trace:");
+            for (int i = 0; i < ctx->last_frames; i++)
+                fprintf(stderr, "%s%d", i == 0 ? " " : ",", ctx->last_codes[(size_t)i * G]);
+            fprintf(stderr, "\n");
+        }
+    }
+    double t_codec = now_ms();
+    rc = 0;
+    for (int b = 0; b < nb; b++) {
+        audio[b] = NULL;
+        samples[b] = 0;
+        if (ngen[b] <= 0) { rc = -1; continue; }
+        audio[b] = qtts_dev_codec_slot(dev, b, ngen[b], &samples[b]);
+        if (!audio[b] || samples[b] <= 0) rc = -1;
+    }
+    ctx->perf_codec_ms = now_ms() - t_codec;
+    ctx->perf_total_ms = now_ms() - t_start;
+    free(stopped); free(ngen); free(sstep);
+out:
+    for (int b = 0; b < nb; b++) { free(pr[b].text); free(pr[b].plan); }
+    free(pr);
+    return rc;
+}
+
+float *qwen_tts_generate(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
+                         int *out_samples) {
+    if (!ctx || !out_samples) return NULL;
+    *out_samples = 0;
+    double t_start = now_ms();
+    float *audio = NULL;
+    int n = 0;
+    const char *texts[1] = {text}, *spk[1] = {speaker}, *lang[1] = {language};
+    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start);
+    if (rc != 0 || !audio || n <= 0) {
+        free(audio);
+        *out_samples = 0;
+        return NULL;
+    }
+    if (qwen_tts_verbose >= 1) {
+        fprintf(stderr, "Codec decode: %d samples in %.1f ms\n", n, ctx->perf_codec_ms);
+        fprintf(stderr, "Total: %.1f ms (%.2f s audio, %.2fx realtime)\n", ctx->perf_total_ms,
+                (float)n / QWEN_TTS_SAMPLE_RATE, ((float)n / QWEN_TTS_SAMPLE_RATE) / (ctx->perf_total_ms / 1000.0));
+    }
+    *out_samples = n;
+    return audio;
+}
+
+int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
+                            const char *const *languages, float **out_audio, int *out_samples) {
+    if (!ctx || nb < 1 || !texts || !out_audio || !out_samples) return -1;
+    return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms());
+}
+
+int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames) {
+    if (!ctx || !ctx->last_codes) return 0;
+    int n = ctx->last_frames < max_frames ? ctx->last_frames : max_frames;
+    memcpy(codes, ctx->last_codes, (size_t)n * ctx->config.num_code_groups * sizeof(int));
+    return n;
+}
+
+/* -------------------------------------------------- stage functions (host) */
+void qwen_tts_talker_prefill(qwen_tts_ctx_t *ctx, const float *input_embeds, int seq_len) {
+    if (qtts_dev_talker_prefill_host((qtts_dev_t *)ctx->hip, input_embeds, seq_len, ctx->tk_x) != 0) {
+        fprintf(stderr, "Error: talker prefill failed\n");
+        return;
+    }
+    ctx->talker_kv_len = seq_len;
+    if (qwen_tts_verbose >= 1) fprintf(stderr, "Talker prefill complete: %d tokens\n", seq_len);
+}
+
+void qwen_tts_talker_forward(qwen_tts_ctx_t *ctx, const float *input_embed, float *logits) {
+    if (qtts_dev_talker_forward_host((qtts_dev_t *)ctx->hip, input_embed, logits, ctx->tk_x) != 0) {
+        fprintf(stderr, "Error: talker forward failed\n");
+        return;
+    }
+    ctx->talker_kv_len++;
+}
+
+void qwen_tts_subtalker_generate(qwen_tts_ctx_t *ctx, const float *talker_hidden, int first_code, int *out_codes) {
+    qtts_gen_params_t gp;
+    params_of(ctx, &gp);
+    qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
+    /* keep the device's sampling parameters in sync with the ctx fields */
+    if (qtts_dev_begin(dev, 1, ctx->max_new_tokens > 0 ? ctx->max_new_tokens : 1, 16, &gp) != 0 ||
+        qtts_dev_subtalker_host(dev, talker_hidden, first_code, out_codes) != 0)
+        fprintf(stderr, "Error: sub-talker failed\n");
+}
+
+float *qwen_tts_codec_decode(qwen_tts_ctx_t *ctx, const int *codes, int time_steps, int *out_samples) {
+    if (!ctx || !codes || !out_samples || time_steps <= 0) {
+        if (out_samples) *out_samples = 0;
+        return NULL;
+    }
+    return qtts_dev_codec_decode_host((qtts_dev_t *)ctx->hip, codes, time_steps, out_samples);
+}
+
+int qwen_tts_talker_hidden(qwen_tts_ctx_t *ctx, float *out) {
+    if (!ctx || !ctx->tk_x) return -1;
+    memcpy(out, ctx->tk_x, ctx->config.talker_hidden * sizeof(float));
+    return 0;
+}
+
+/* ABI self-check for FFI bindings (tests/test_host.py compares this with the
+ * ctypes mirror of qwen_tts_ctx_t) */
+size_t qwen_tts_abi_sizeof_ctx(void) { return sizeof(qwen_tts_ctx_t); }

@@ -1,0 +1,266 @@
+"""Python (ctypes) binding of the MI355X drop-in library lib/libqwen_tts_amd.so.
+
+This is the binding a maintainer of the reference would add next to its CLI
+(see INTEGRATION.md): it mirrors `qwen_tts.h` (ctx struct + functions) and
+`qtts_hip.h` (kernel-level entry points on device buffers).  Tests and
+bench.py use it; device buffers for the kernel-level calls are torch tensors
+(PyTorch is plumbing only: allocation, streams, torch.distributed).
+
+The library is required: importing works without a GPU (symbols resolve),
+but every compute call needs the HIP device and fails loudly without it.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libqwen_tts_amd.so")
+CLI_PATH = os.path.join(HERE, "bin", "qwen-tts")
+
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int)
+
+PROGRESS_CB = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p)
+
+
+class Config(C.Structure):  # qwen_tts_config_t (include/qwen_tts.h)
+    _fields_ = [(n, C.c_int) for n in (
+        "talker_vocab_size", "talker_hidden", "talker_intermediate", "talker_layers", "talker_heads",
+        "talker_kv_heads", "talker_head_dim", "talker_text_hidden", "talker_text_vocab", "num_code_groups")] + [
+        ("talker_rms_norm_eps", C.c_float), ("talker_rope_theta", C.c_float), ("mrope_section", C.c_int * 3)] + [
+        (n, C.c_int) for n in (
+            "subtalker_vocab_size", "subtalker_hidden", "subtalker_intermediate", "subtalker_layers",
+            "subtalker_heads", "subtalker_kv_heads", "subtalker_head_dim",
+            "codec_num_quantizers", "codec_codebook_size", "codec_codebook_dim", "codec_hidden", "codec_latent",
+            "codec_layers", "codec_heads", "codec_kv_heads", "codec_intermediate", "codec_sliding_window",
+            "codec_decoder_dim")] + [
+        ("codec_rms_norm_eps", C.c_float), ("codec_layer_scale", C.c_float),
+        ("codec_upsample_rates", C.c_int * 4), ("codec_upsampling_ratios", C.c_int * 2),
+        ("n_speakers", C.c_int), ("speaker_names", C.POINTER(C.c_char_p)), ("speaker_ids", _ip),
+        ("n_languages", C.c_int), ("language_names", C.POINTER(C.c_char_p)), ("language_ids", _ip)] + [
+        (n, C.c_int) for n in ("codec_pad_id", "codec_bos_id", "codec_eos_id", "codec_nothink_id", "codec_think_id",
+                               "codec_think_bos_id", "codec_think_eos_id")]
+
+
+class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
+    _fields_ = [
+        ("config", Config), ("model_dir", C.c_char * 512), ("hip", C.c_void_p), ("hip_device", C.c_int),
+        ("talker_kv_len", C.c_int), ("tk_x", _fp),
+        ("temperature", C.c_float), ("subtalker_temperature", C.c_float), ("top_k", C.c_int),
+        ("subtalker_top_k", C.c_int), ("top_p", C.c_float), ("subtalker_top_p", C.c_float),
+        ("repetition_penalty", C.c_float), ("max_new_tokens", C.c_int), ("fixed_codec_tokens", C.c_int),
+        ("sample_seed", C.c_int), ("progress_cb", C.c_void_p), ("progress_cb_userdata", C.c_void_p),
+        ("perf_total_ms", C.c_double), ("perf_talker_ms", C.c_double), ("perf_codec_ms", C.c_double),
+        ("perf_codec_tokens", C.c_int), ("perf_prefill_ms", C.c_double), ("perf_first_frame_ms", C.c_double),
+        ("last_codes", _ip), ("last_frames", C.c_int), ("last_stop_reason", C.c_int), ("last_stop_step", C.c_int),
+    ]
+
+
+# Every symbol include/qwen_tts.h and include/qtts_hip.h declare (checked by tests/test_host.py)
+EXPORTS = [
+    "qwen_tts_load", "qwen_tts_free", "qwen_tts_set_progress_callback", "qwen_tts_generate", "qwen_tts_write_wav",
+    "qwen_tts_talker_prefill", "qwen_tts_talker_forward", "qwen_tts_subtalker_generate", "qwen_tts_codec_decode",
+    "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
+    "qwen_tts_verbose",
+    "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
+    "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
+    "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
+    "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
+    "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
+    "qtts_hip_transposed_conv1d", "qtts_hip_snake_beta", "qtts_hip_expf_glibc", "qtts_hip_sync",
+]
+
+_LIB = None
+
+
+def lib():
+    """Load the in-tree library (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C qwen3-tts-c_amd` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    L.qwen_tts_load.restype = C.POINTER(Ctx)
+    L.qwen_tts_load.argtypes = [C.c_char_p]
+    L.qwen_tts_free.argtypes = [C.POINTER(Ctx)]
+    L.qwen_tts_generate.restype = C.c_void_p
+    L.qwen_tts_generate.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, C.c_char_p, _ip]
+    L.qwen_tts_generate_batch.restype = C.c_int
+    L.qwen_tts_generate_batch.argtypes = [C.POINTER(Ctx), C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                          C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), _ip]
+    L.qwen_tts_last_codes.restype = C.c_int
+    L.qwen_tts_last_codes.argtypes = [C.POINTER(Ctx), _ip, C.c_int]
+    L.qwen_tts_talker_prefill.argtypes = [C.POINTER(Ctx), _fp, C.c_int]
+    L.qwen_tts_talker_forward.argtypes = [C.POINTER(Ctx), _fp, _fp]
+    L.qwen_tts_subtalker_generate.argtypes = [C.POINTER(Ctx), _fp, C.c_int, _ip]
+    L.qwen_tts_codec_decode.restype = C.c_void_p
+    L.qwen_tts_codec_decode.argtypes = [C.POINTER(Ctx), _ip, C.c_int, _ip]
+    L.qwen_tts_talker_hidden.argtypes = [C.POINTER(Ctx), _fp]
+    L.qwen_tts_set_device.argtypes = [C.c_int]
+    L.qwen_tts_set_progress_callback.argtypes = [C.POINTER(Ctx), PROGRESS_CB, C.c_void_p]
+    L.qwen_tts_write_wav.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
+    L.qwen_tts_abi_sizeof_ctx.restype = C.c_size_t
+    L.qtts_hip_device_count.restype = C.c_int
+    vp = C.c_void_p
+    L.qtts_hip_matvec_bf16.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
+    L.qtts_hip_rmsnorm_matvec_bf16.argtypes = [vp, vp, vp, vp, C.c_float, C.c_int, C.c_int, C.c_int, vp]
+    L.qtts_hip_sample_top_k.argtypes = [vp, vp, C.c_int, C.c_int, C.c_float, C.c_float, vp, C.c_int, vp]
+    L.qtts_hip_causal_conv1d.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+    L.qtts_hip_transposed_conv1d.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+    L.qtts_hip_snake_beta.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp]
+    L.qtts_hip_expf_glibc.argtypes = [vp, vp, C.c_int, vp]
+    _LIB = L
+    return L
+
+
+_libc = C.CDLL("libc.so.6")
+_libc.free.argtypes = [C.c_void_p]
+
+
+def _take_audio(ptr, n):
+    if not ptr or n <= 0:
+        return None
+    a = np.ctypeslib.as_array(C.cast(ptr, _fp), shape=(n,)).copy()
+    _libc.free(ptr)
+    return a
+
+
+def set_verbose(v):
+    C.c_int.in_dll(lib(), "qwen_tts_verbose").value = int(v)
+
+
+class QwenTTS:
+    """One model on one HIP device (the reference's qwen_tts_ctx_t)."""
+
+    def __init__(self, model_dir, device=0):
+        L = lib()
+        L.qwen_tts_set_device(int(device))
+        self.ctx = L.qwen_tts_load(model_dir.encode())
+        if not self.ctx:
+            raise RuntimeError(f"qwen_tts_load({model_dir}) failed")
+        self.c = self.ctx.contents
+        self.cfg = self.c.config
+
+    def close(self):
+        if self.ctx:
+            lib().qwen_tts_free(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, max_tokens=4096, fixed=0, seed=42, temperature=0.9, top_k=50, top_p=1.0, rep=1.05,
+                   st_temperature=0.9, st_top_k=50, st_top_p=1.0):
+        c = self.c
+        c.temperature, c.top_k, c.top_p, c.repetition_penalty = temperature, top_k, top_p, rep
+        c.subtalker_temperature, c.subtalker_top_k, c.subtalker_top_p = st_temperature, st_top_k, st_top_p
+        c.max_new_tokens, c.fixed_codec_tokens, c.sample_seed = max_tokens, fixed, seed
+
+    def generate(self, ids, speaker=None, language=None):
+        csv = ",".join(str(int(i)) for i in ids).encode()
+        n = C.c_int(0)
+        p = lib().qwen_tts_generate(self.ctx, csv, speaker.encode() if speaker else None,
+                                    language.encode() if language else None, C.byref(n))
+        return _take_audio(p, n.value)
+
+    def generate_batch(self, id_lists, speakers=None, languages=None):
+        nb = len(id_lists)
+        tx = (C.c_char_p * nb)(*[",".join(str(int(i)) for i in ids).encode() for ids in id_lists])
+        sp = (C.c_char_p * nb)(*[(s.encode() if s else None) for s in (speakers or [None] * nb)])
+        lg = (C.c_char_p * nb)(*[(s.encode() if s else None) for s in (languages or [None] * nb)])
+        out = (C.c_void_p * nb)()
+        ns = (C.c_int * nb)()
+        rc = lib().qwen_tts_generate_batch(self.ctx, nb, tx, sp, lg, out, ns)
+        audio = [_take_audio(out[i], ns[i]) for i in range(nb)]
+        return rc, audio
+
+    def last_codes(self):
+        G = self.cfg.num_code_groups
+        n = self.c.last_frames
+        buf = np.zeros((max(n, 1), G), np.int32)
+        k = lib().qwen_tts_last_codes(self.ctx, buf.ctypes.data_as(_ip), n)
+        return buf[:k].copy()
+
+    # stage functions (host pointers)
+    def prefill(self, embeds):
+        e = np.ascontiguousarray(embeds, np.float32)
+        lib().qwen_tts_talker_prefill(self.ctx, e.ctypes.data_as(_fp), e.shape[0])
+        return self.hidden()
+
+    def hidden(self):
+        h = np.zeros(self.cfg.talker_hidden, np.float32)
+        lib().qwen_tts_talker_hidden(self.ctx, h.ctypes.data_as(_fp))
+        return h
+
+    def step(self, embed):
+        e = np.ascontiguousarray(embed, np.float32)
+        lg = np.zeros(self.cfg.talker_vocab_size, np.float32)
+        lib().qwen_tts_talker_forward(self.ctx, e.ctypes.data_as(_fp), lg.ctypes.data_as(_fp))
+        return lg, self.hidden()
+
+    def subtalker(self, hidden, code0):
+        out = np.zeros(self.cfg.num_code_groups, np.int32)
+        h = np.ascontiguousarray(hidden, np.float32)
+        lib().qwen_tts_subtalker_generate(self.ctx, h.ctypes.data_as(_fp), int(code0), out.ctypes.data_as(_ip))
+        return out
+
+    def codec_decode(self, codes):
+        c = np.ascontiguousarray(codes, np.int32)
+        n = C.c_int(0)
+        p = lib().qwen_tts_codec_decode(self.ctx, c.ctypes.data_as(_ip), c.shape[0], C.byref(n))
+        return _take_audio(p, n.value)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+class Kernels:
+    """Kernel-level entry points of qtts_hip.h on torch device tensors."""
+
+    @staticmethod
+    def matvec_bf16(out, A_u16, x, rows, cols, batch=1):
+        _ok(lib().qtts_hip_matvec_bf16(_ptr(out), _ptr(A_u16), _ptr(x), rows, cols, batch, _stream()), "matvec")
+
+    @staticmethod
+    def rmsnorm_matvec_bf16(out, A_u16, x, w, eps, rows, cols, batch=1):
+        _ok(lib().qtts_hip_rmsnorm_matvec_bf16(_ptr(out), _ptr(A_u16), _ptr(x), _ptr(w), eps, rows, cols, batch,
+                                               _stream()), "rmsnorm_matvec")
+
+    @staticmethod
+    def sample_top_k(out_i32, logits, vocab, top_k, top_p, temperature, rng_u32, batch=1):
+        _ok(lib().qtts_hip_sample_top_k(_ptr(out_i32), _ptr(logits), vocab, top_k, top_p, temperature,
+                                        _ptr(rng_u32), batch, _stream()), "sample")
+
+    @staticmethod
+    def causal_conv1d(out, x, w, b, ci, co, k, L, dil=1, groups=1):
+        _ok(lib().qtts_hip_causal_conv1d(_ptr(out), _ptr(x), _ptr(w), _ptr(b), ci, co, k, L, dil, groups,
+                                         _stream()), "conv1d")
+
+    @staticmethod
+    def transposed_conv1d(out, x, w, b, ci, co, k, stride, L):
+        _ok(lib().qtts_hip_transposed_conv1d(_ptr(out), _ptr(x), _ptr(w), _ptr(b), ci, co, k, stride, L,
+                                             _stream()), "tconv1d")
+
+    @staticmethod
+    def snake_beta(out, x, alpha, inv_beta, C_, L):
+        _ok(lib().qtts_hip_snake_beta(_ptr(out), _ptr(x), _ptr(alpha), _ptr(inv_beta), C_, L, _stream()), "snake")
+
+    @staticmethod
+    def expf_glibc(out, x, n):
+        _ok(lib().qtts_hip_expf_glibc(_ptr(out), _ptr(x), n, _stream()), "expf")
