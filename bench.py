@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py - Qwen3-TTS hot path on MI355X: audio-seconds per wall-second.
+
+Workload (BASELINE.json metric "audio-sec/wall-sec (RTF^-1) + first-packet ms,
+Qwen3-TTS-1.7B @ 1 & 8 GPU"): the 1.7B-shaped synthetic model
+(tools/synth_model.py, random init -- no checkpoint offline), the P128 prompt
+(SURVEY.md 8d), fixed 128 codec frames per utterance (10.24 s of audio),
+default sampling (T 0.9 / top-k 50 / rep 1.05, seed 42), batch 1 per GPU.
+
+One STEP = one full qwen_tts_generate() call through the drop-in C API:
+prompt embedding + talker prefill + 128 frames of talker/sub-talker decode
+with on-device sampling + codec decode, audio copied back to host memory.
+
+N GPUs (torchrun, one process per GPU): every rank runs its own utterances
+(data parallel, no collective in the data path); barrier + synchronize around
+the timed region, time = max over ranks, value = total audio seconds / time.
+
+Also reported:
+  first_packet_ms  generate() entry -> first 1920 samples available: prefill +
+                   frame 0 + codec decode of that frame (the codec is causal,
+                   so the first frame decodes on its own; measured after the
+                   timed region)
+  roofline         dominant kernel (weight-streaming GEMV), measured live with
+                   HIP events on the context stream over one eager frame
+  cpu_baseline     the reference c/ build (oracle/_ref/qwen-tts, scalar+OpenMP)
+                   on a bounded sample of the same workload, rank 0, N=1 only
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "qwen3-tts-c_amd"), os.path.join(ROOT, "tools"), os.path.join(ROOT, "tests")]
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def reduce_max(ws, v):
+    if ws == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(ws, v):
+    if ws == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def ensure_model_shared(md, preset, ws, local):
+    """local rank 0 of the node writes the model; the others wait."""
+    from synth_model import ensure_model
+    if local == 0:
+        t = time.time()
+        ensure_model(md, preset, seed=0)
+        log(f"[bench] model {preset} ready in {time.time() - t:.1f}s at {md}")
+    barrier(ws)
+
+
+def profile_roofline(m, lib):
+    """One eager frame with HIP events around every kernel (qtts_dev_profile_frame)."""
+    import ctypes as C
+    n_max = 4096
+    kind = (C.c_int * n_max)()
+    byt = (C.c_double * n_max)()
+    ms = (C.c_float * n_max)()
+    lib.qtts_dev_profile_frame.restype = C.c_int
+    lib.qtts_dev_profile_frame.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    n = lib.qtts_dev_profile_frame(m.c.hip, 1, n_max, kind, byt, ms)
+    if n <= 0:
+        return None
+    k = np.array(kind[:n])
+    b = np.array(byt[:n])
+    t = np.array(ms[:n], dtype=np.float64)
+    names = {0: "gemv_talker", 1: "gemv_subtalker", 2: "attention", 3: "sampler", 4: "embed_sum"}
+    share = {names[i]: float(t[k == i].sum()) for i in names}
+    frame_ms = float(t.sum())
+    # dominant kernel: the GEMV class with the largest share of the frame
+    dom = 0 if share["gemv_talker"] >= share["gemv_subtalker"] else 1
+    sel = k == dom
+    avg_bytes = float(b[sel].mean())
+    avg_ms = float(t[sel].mean())
+    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
+    # the largest single launch (talker gate|up GEMV) as a bandwidth probe
+    imax = int(np.argmax(np.where(k == 0, b, -1)))
+    big = {"bytes": float(b[imax]), "ms": float(t[imax]), "GBs": float(b[imax] / (t[imax] * 1e-3) / 1e9)}
+    return dict(kernel=("k_gemv<1,true> (talker weight stream)" if dom == 0
+                        else "k_gemv<1,false> (sub-talker weight stream)"),
+                launches_per_frame=int(sel.sum()), avg_bytes=avg_bytes, avg_ms=avg_ms, achieved_GBs=achieved,
+                frame_kernel_ms=frame_ms, share_ms=share, n_kernels=n, biggest_launch=big,
+                gemv_bytes_per_frame=float(b[(k == 0) | (k == 1)].sum()),
+                gemv_ms_per_frame=float(t[(k == 0) | (k == 1)].sum()))
+
+
+def cpu_baseline(md, frames, ids, threads):
+    exe = os.path.join(ROOT, "oracle", "_ref", "qwen-tts")
+    if not os.path.exists(exe):
+        return None
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    cmd = [exe, "-d", md, "-t", ",".join(map(str, ids)), "-s", "aiden", "-l", "english", "-o", "/tmp/qtts_cpu.wav",
+           "--fixed-codec-tokens", str(frames), "-v"]
+    t = time.time()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    wall = time.time() - t
+    m = re.search(r"Total: ([0-9.]+) ms \(([0-9.]+) s audio", r.stderr)
+    g = re.search(r"Generated (\d+) codec tokens in ([0-9.]+) ms \(([0-9.]+) ms/token\)", r.stderr)
+    if r.returncode != 0 or not m:
+        log("[bench] cpu baseline failed:", r.stderr[-400:])
+        return None
+    total_s = float(m.group(1)) / 1e3
+    audio_s = float(m.group(2))
+    return dict(value=audio_s / total_s, unit="audio-s/s", cores=threads, kind="reference",
+                sample=(f"reference c/ (oracle/_ref/qwen-tts, scalar GEMV + OpenMP {threads} threads, no BLAS in image) "
+                        f"on the same 1.7B synthetic model, same prompt, {frames} frames ({audio_s:.2f} s audio): "
+                        f"generate {total_s:.1f} s (talker {float(g.group(3)) if g else -1:.0f} ms/frame), "
+                        f"process wall incl. load {wall:.1f} s"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--preset", default="1.7b")
+    ap.add_argument("--frames", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU per step (lock-step batch)")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--model-dir", default=None)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_setup()
+    import torch
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import qtts
+    from synth_model import prompt_ids
+
+    md = args.model_dir or f"/tmp/qtts_bench_{args.preset}"
+    ensure_model_shared(md, args.preset, ws, local)
+    t = time.time()
+    m = qtts.QwenTTS(md, device=local)
+    log(f"[bench] rank {rank}: model loaded on HIP device {local} in {time.time() - t:.1f}s")
+    m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
+    prompts = [prompt_ids("p128", seed=1234 + rank * args.batch + i) for i in range(args.batch)]
+
+    def one_step():
+        if args.batch == 1:
+            a = m.generate(prompts[0], "aiden", "english")
+            if a is None:
+                raise RuntimeError("generation produced no audio")
+            return len(a)
+        rc, aud = m.generate_batch(prompts, ["aiden"] * args.batch, ["english"] * args.batch)
+        if rc != 0:
+            raise RuntimeError("batch generation failed")
+        return sum(len(a) for a in aud)
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    samples = 0
+    for _ in range(args.steps):
+        samples += one_step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    el = time.perf_counter() - t0
+    el_max = reduce_max(ws, el)
+    audio_total = reduce_sum(ws, samples / 24000.0)
+    value = audio_total / el_max
+    ms_per_step = el_max / args.steps * 1e3
+
+    # ---- first packet: prefill + frame 0 + codec decode of frame 0 ----
+    fp = None
+    if args.batch == 1:
+        m.generate(prompts[0], "aiden", "english")
+        first_frame_ms = m.c.perf_first_frame_ms
+        codes = m.last_codes()
+        t1 = time.perf_counter()
+        a1 = m.codec_decode(codes[:1])
+        codec1_ms = (time.perf_counter() - t1) * 1e3
+        fp = dict(first_packet_ms=first_frame_ms + codec1_ms, first_frame_ms=first_frame_ms,
+                  first_codec_ms=codec1_ms, first_packet_samples=int(len(a1)),
+                  prefill_ms=m.c.perf_prefill_ms, talker_ms=m.c.perf_talker_ms, codec_ms=m.c.perf_codec_ms)
+
+    roof = None if args.no_profile else profile_roofline(m, qtts.lib())
+    m.close()
+
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(md, args.cpu_frames, prompts[0], args.cpu_threads)
+
+    if rank == 0:
+        out = {
+            "metric": "audio-sec/wall-sec (RTF^-1) + first-packet ms, Qwen3-TTS-1.7B @ 1 & 8 GPU",
+            "value": round(value, 3),
+            "unit": "audio-s/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32 activations x bf16 weights (fp32 accumulate)",
+            "data": "synthetic (seeded random-init weights of the 1.7B architecture, tools/synth_model.py)",
+            "config": {"workload": f"Qwen3-TTS-{args.preset} synthetic, P128 prompt, fixed {args.frames} frames "
+                                   f"({args.frames * 0.08:.2f} s audio), default sampling, batch {args.batch} per GPU",
+                       "global_batch": args.batch * ws, "frames": args.frames,
+                       "parallelism": f"dp{ws} (independent replicas, no collective in the data path)"},
+        }
+        if fp:
+            out["first_packet_ms"] = round(fp["first_packet_ms"], 2)
+            out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in fp.items()}
+        if roof:
+            out["roofline"] = {"bound": "hbm", "achieved": round(roof["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(roof["achieved_GBs"] / HBM_PEAK_GBS, 4),
+                               "traffic": None, "kernel": roof["kernel"],
+                               "avg_launch_us": round(roof["avg_ms"] * 1e3, 2),
+                               "avg_launch_bytes": int(roof["avg_bytes"]),
+                               "launches_per_frame": roof["launches_per_frame"]}
+            out["frame_profile"] = {"kernel_ms_per_frame": round(roof["frame_kernel_ms"], 3),
+                                    "share_ms": {k: round(v, 3) for k, v in roof["share_ms"].items()},
+                                    "gemv_GBs_all": round(roof["gemv_bytes_per_frame"] /
+                                                          (roof["gemv_ms_per_frame"] * 1e-3) / 1e9, 1),
+                                    "biggest_gemv": {k: round(v, 4) for k, v in roof["biggest_launch"].items()},
+                                    "n_kernels": roof["n_kernels"]}
+        out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -133,6 +133,14 @@ int qtts_hip_snake_beta(float *out_dev, const float *x_dev, const float *alpha_d
 int qtts_hip_expf_glibc(float *out_dev, const float *in_dev, int n, void *stream);
 int qtts_hip_sync(void);
 
+/* Diagnostics: run ONE frame eagerly on the current generation state with an
+ * event pair around every kernel launch on the context stream.  kind[i]:
+ * 0 talker GEMV, 1 sub-talker GEMV, 2 attention, 3 sampler, 4 embed-sum;
+ * bytes[i]: algorithmic bytes of GEMV launches; ms[i]: measured duration.
+ * Returns the number of kernels (<0 on error).  Advances the state by one
+ * frame, so call it after a generation, not in the middle of one. */
+int qtts_dev_profile_frame(qtts_dev_t *dev, int step, int max, int *kind, double *bytes, float *ms);
+
 #ifdef __cplusplus
 }
 #endif

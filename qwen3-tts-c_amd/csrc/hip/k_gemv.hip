@@ -184,14 +184,159 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Batch-1 decode path.  Same slot mapping; the prologue loads x once as float4
+// (XV per thread), reduces the RMS statistic with one barrier, writes the
+// normalised row to LDS (second barrier); weights for the first U blocks are
+// already in flight.  One barrier in the epilogue: each output thread sums
+// the KSPLIT partials it needs (for SwiGLU also its up row's) straight from
+// LDS.
+template <int U1, int XV, bool NT>
+__global__ __launch_bounds__(256) void k_gemv1(GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
+    const int ksn = a.ksplit, RPW = 32 / ksn;
+    const int rloc = slot % RPW, ks = slot / RPW;
+    const int row0 = blockIdx.x * RPW, row = row0 + rloc;
+    const int rowc = row < a.R ? row : a.R - 1;
+    const int C = a.C;
+    float *xs = smem;          // [C]
+    float *red = xs + C;       // [32]
+    float *bred = red + 32;    // [4]
+    const v4u *Wr = reinterpret_cast<const v4u *>(a.W + (size_t)rowc * C) + sub;
+    const int nblk = C / 64 / ksn;
+    const int ng = (nblk + U1 - 1) / U1;
+    v4u wv[U1];
+    auto load_group = [&](int g) {
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+            int j = g * U1 + u;
+            j = j < nblk ? j : nblk - 1;
+            const v4u *p = Wr + ((64 * (ks + j * ksn)) >> 3);
+            if constexpr (NT) wv[u] = __builtin_nontemporal_load(p);
+            else wv[u] = *p;
+        }
+    };
+    load_group(0);
+
+    // ---- prologue: x (fp32 row or gathered bf16 row) -> optional RMSNorm -> LDS
+    const bf16_t *trow = nullptr;
+    if (a.table) {
+        const int *p = a.ids + a.ids_off;
+        if (a.row_sel) p += (size_t)a.row_sel[0] * a.ids_rstride;
+        trow = a.table + (size_t)(*p) * C;
+    }
+    float4 xv[XV], wn[XV];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int c = 4 * tid + 1024 * i;
+        const int cc = c < C ? c : C - 4;
+        float4 v;
+        if (trow) {
+            const uint2 t = *reinterpret_cast<const uint2 *>(trow + cc);
+            v = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
+                            __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
+        } else {
+            v = *reinterpret_cast<const float4 *>(a.x + cc);
+        }
+        if (c >= C) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        xv[i] = v;
+        if (a.norm_w) {
+            wn[i] = *reinterpret_cast<const float4 *>(a.norm_w + cc);
+            ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+    }
+    float inv = 1.f;
+    if (a.norm_w) {
+        ss = wave_sum(ss);
+        if ((tid & 63) == 0) bred[tid >> 6] = ss;
+        __syncthreads();
+        inv = rms_inv(bred[0] + bred[1] + bred[2] + bred[3], C, a.eps);
+    }
+    const bool cp = a.xcopy && blockIdx.x == 0;
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int c = 4 * tid + 1024 * i;
+        if (c < C) {
+            float4 v = xv[i];
+            if (cp && !a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + c) = v;
+            if (a.norm_w) {
+                v.x = v.x * inv * wn[i].x; v.y = v.y * inv * wn[i].y;
+                v.z = v.z * inv * wn[i].z; v.w = v.w * inv * wn[i].w;
+            }
+            if (cp && a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + c) = v;
+            *reinterpret_cast<float4 *>(xs + c) = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- stream the weights ----
+    float acc = 0.f;
+    for (int g = 0; g < ng; ++g) {
+        v4u cur[U1];
+#pragma unroll
+        for (int u = 0; u < U1; ++u) cur[u] = wv[u];
+        if (g + 1 < ng) load_group(g + 1);
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+            const int j = g * U1 + u;
+            if (j < nblk) {
+                float f[8];
+                unpack8(cur[u], f);
+                const int cl = 64 * (ks + j * ksn) + 8 * sub;
+                const float4 x0 = *reinterpret_cast<const float4 *>(xs + cl);
+                const float4 x1 = *reinterpret_cast<const float4 *>(xs + cl + 4);
+                acc = fmaf(f[0], x0.x, acc); acc = fmaf(f[1], x0.y, acc);
+                acc = fmaf(f[2], x0.z, acc); acc = fmaf(f[3], x0.w, acc);
+                acc = fmaf(f[4], x1.x, acc); acc = fmaf(f[5], x1.y, acc);
+                acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
+            }
+        }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (sub == 0) red[ks * RPW + rloc] = acc;
+    __syncthreads();
+    if (tid < RPW) {
+        const int r = row0 + tid;
+        if (r < a.R) {
+            float v = red[tid];
+            for (int k = 1; k < ksn; ++k) v += red[k * RPW + tid];
+            switch (a.epi) {
+                case EPI_STORE: a.y[r] = v; break;
+                case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
+                case EPI_BIAS_SILU: {
+                    const float z = v + a.bias[r];
+                    a.y[r] = z / (1.0f + expf(-z));
+                    break;
+                }
+                case EPI_RESID: a.y[r] += v; break;
+                case EPI_SWIGLU:
+                    if ((r & 7) < 4) {
+                        float u = red[tid + 4];
+                        for (int k = 1; k < ksn; ++k) u += red[k * RPW + tid + 4];
+                        a.y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * u;
+                    }
+                    break;
+            }
+        }
+    }
+}
+
 }  // namespace
 
-static int pick_ksplit(int R, int C, int epi) {
+// KSPLIT: grow until the grid has >= `target` workgroups (>= 2 per CU for
+// the latency hiding of a weight stream; fewer, larger blocks leave CUs idle
+// in the tail), bounded by the row length and by SwiGLU's 8-row quads.
+static int pick_ksplit(int R, int C, int epi, int target) {
     int maxk = C / 64;
     if (maxk > 32) maxk = 32;
     if (epi == EPI_SWIGLU && maxk > 4) maxk = 4;
     int ks = 1;
-    while (ks < maxk && (R + (32 / ks) - 1) / (32 / ks) < 256) ks *= 2;
+    while (ks < maxk && (R + (32 / ks) - 1) / (32 / ks) < target) ks *= 2;
     while (ks > 1 && (C / 64) % ks) ks /= 2;
     return ks;
 }
@@ -202,7 +347,27 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         fprintf(stderr, "qtts_gemv: unsupported shape R=%d C=%d nb=%d\n", a.R, a.C, a.nb);
         return -1;
     }
-    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi);
+    if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
+        if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
+        const int rpw = 32 / a.ksplit;
+        const int grid = (a.R + rpw - 1) / rpw;
+        const int nblk = a.C / 64 / a.ksplit;
+        const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
+        const size_t smem = (size_t)(a.C + 40) * sizeof(float);
+#define QTTS_G1(U, X)                                                                                 \
+        if (a.nt) hipLaunchKernelGGL((k_gemv1<U, X, true>), dim3(grid), dim3(256), smem, st, a);      \
+        else hipLaunchKernelGGL((k_gemv1<U, X, false>), dim3(grid), dim3(256), smem, st, a);
+        if (nblk >= 8) {
+            switch (xv) { case 1: QTTS_G1(8, 1) break; case 2: QTTS_G1(8, 2) break;
+                          case 4: QTTS_G1(8, 4) break; default: QTTS_G1(8, 8) break; }
+        } else {
+            switch (xv) { case 1: QTTS_G1(4, 1) break; case 2: QTTS_G1(4, 2) break;
+                          case 4: QTTS_G1(4, 4) break; default: QTTS_G1(4, 8) break; }
+        }
+#undef QTTS_G1
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 256);
     int NB = a.nb <= 1 ? 1 : a.nb <= 2 ? 2 : a.nb <= 4 ? 4 : a.nb <= 8 ? 8 : 16;
     const int unit = 64 * a.ksplit;
     int cch = (8192 / NB) / unit * unit;

@@ -32,6 +32,10 @@ struct GemvArgs {
     int ldy = 0;
     const float *bias = nullptr;
     int epi = EPI_STORE;
+    // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
+    bool ldx_ok1() const {
+        return table ? (C % 4 == 0) : (((uintptr_t)x & 15) == 0 && (!norm_w || ((uintptr_t)norm_w & 15) == 0));
+    }
 };
 int qtts_gemv(const GemvArgs &a, hipStream_t st);
 

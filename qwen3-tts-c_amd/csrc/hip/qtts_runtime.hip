@@ -107,6 +107,10 @@ struct qtts_dev {
     bool have_par = false;
     hipGraphExec_t g0 = nullptr, gN = nullptr;
     int graph_key = -1;
+    // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
+    struct Prof { int kind; double bytes; hipEvent_t a, b; };
+    std::vector<Prof> prof;
+    bool profiling = false;
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
     int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
@@ -470,6 +474,30 @@ static int reset_counters(qtts_dev *dv) {
 }
 
 // ----------------------------------------------------------------- kernels of one frame
+enum { PK_GEMV_TALKER = 0, PK_GEMV_SUB = 1, PK_ATTN = 2, PK_SAMPLE = 3, PK_EMBED = 4 };
+struct ProfScope {  // brackets one launch with events when profiling is on
+    qtts_dev *dv;
+    size_t idx;
+    ProfScope(qtts_dev *d, int kind, double bytes) : dv(d), idx((size_t)-1) {
+        if (!dv->profiling) return;
+        qtts_dev::Prof p{kind, bytes, nullptr, nullptr};
+        hipEventCreate(&p.a);
+        hipEventCreate(&p.b);
+        hipEventRecord(p.a, dv->st);
+        dv->prof.push_back(p);
+        idx = dv->prof.size() - 1;
+    }
+    ~ProfScope() {
+        if (idx != (size_t)-1) hipEventRecord(dv->prof[idx].b, dv->st);
+    }
+};
+static double gemv_bytes(const GemvArgs &a) {
+    return (double)a.R * a.C * 2 + (double)a.nb * a.C * 4 + (double)a.nb * a.R * 4 + (a.norm_w ? a.C * 4.0 : 0.0);
+}
+static int pgemv(qtts_dev *dv, const GemvArgs &a, int kind) {
+    ProfScope ps(dv, kind, gemv_bytes(a));
+    return qtts_gemv(a, dv->st);
+}
 static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float *y, int ldy, int nb, int epi) {
     GemvArgs a;
     a.W = W; a.R = R; a.C = C; a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy; a.nb = nb; a.epi = epi;
@@ -484,19 +512,19 @@ static int talker_layers(qtts_dev *dv) {
         Layer &ly = dv->tl[l];
         GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->x_tk, d.H, dv->qkv, QKV, nb, EPI_STORE);
         a.norm_w = ly.in; a.eps = d.eps;
-        CKI(qtts_gemv(a, st));
+        CKI(pgemv(dv, a, PK_GEMV_TALKER));
         AttnArgs t;
         t.mode = 0; t.qkv = dv->qkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
         t.rope_cos = dv->rope_cos; t.rope_sin = dv->rope_sin;
         t.kc = dv->kc + (size_t)l * NBA * dv->S * KVD; t.vc = dv->vc + (size_t)l * NBA * dv->S * KVD; t.S = dv->S;
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
-        CKI(qtts_attention(t, st));
-        CKI(qtts_gemv(gv(ly.wo, d.H, AD, dv->att, AD, dv->x_tk, d.H, nb, EPI_RESID), st));
+        { ProfScope ps(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
+        CKI(pgemv(dv, gv(ly.wo, d.H, AD, dv->att, AD, dv->x_tk, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, dv->x_tk, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
-        CKI(qtts_gemv(a, st));
-        CKI(qtts_gemv(gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, dv->x_tk, d.H, nb, EPI_RESID), st));
+        CKI(pgemv(dv, a, PK_GEMV_TALKER));
+        CKI(pgemv(dv, gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, dv->x_tk, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
     }
     return 0;
 }
@@ -506,7 +534,7 @@ static int talker_tail(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     GemvArgs a = gv(dv->head, d.V, d.H, dv->x_tk, d.H, dv->logits, d.V, dv->nrun, EPI_STORE);
     a.norm_w = dv->tk_norm; a.eps = d.eps; a.xcopy = dv->tk_hid; a.ldxc = d.H; a.xcopy_normed = 1;
-    return qtts_gemv(a, dv->st);
+    return pgemv(dv, a, PK_GEMV_TALKER);
 }
 
 static int talker_sample(qtts_dev *dv) {
@@ -519,6 +547,7 @@ static int talker_sample(qtts_dev *dv) {
     s.n_gen = dv->n_gen; s.stopped = dv->stopped; s.cur_row = dv->cur_row; s.stop_step = dv->stop_step;
     s.st_rng = dv->st_rng; s.seed_bits = seed_bits(dv->par.seed);
     s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G;
+    ProfScope ps(dv, PK_SAMPLE, 0);
     return qtts_sample(s, dv->st);
 }
 
@@ -548,42 +577,42 @@ static int subtalker(qtts_dev *dv) {
             set_src(a);
             a.bias = dv->st_projb;
             a.nt = 0;
-            CKI(qtts_gemv(a, st));
+            CKI(pgemv(dv, a, PK_GEMV_SUB));
         }
         for (int l = 0; l < d.Ls; ++l) {
             Layer &ly = dv->sl[l];
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, dv->x_st, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             if (l == 0 && !proj) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
-            CKI(qtts_gemv(a, st));
+            CKI(pgemv(dv, a, PK_GEMV_SUB));
             AttnArgs t;
             t.mode = 0; t.qkv = dv->qkv_s; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
             t.rope_cos = dv->rope_cos_s; t.rope_sin = dv->rope_sin_s;
             t.kc = dv->kcs + (size_t)l * NBA * d.G * KVD; t.vc = dv->vcs + (size_t)l * NBA * d.G * KVD; t.S = d.G;
             t.pos = nullptr; t.pos_const = g; t.NH = d.NHs; t.KV = d.KVs; t.HD = d.HDs; t.out = dv->att_s;
             t.ld_out = AD; t.nrows = nb; t.skip = dv->stopped;
-            CKI(qtts_attention(t, st));
+            { ProfScope ps(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
             a = gv(ly.wo, d.Hs, AD, dv->att_s, AD, dv->x_st, d.Hs, nb, EPI_RESID);
             a.nt = 0;
-            CKI(qtts_gemv(a, st));
+            CKI(pgemv(dv, a, PK_GEMV_SUB));
             a = gv(ly.wgu, 2 * d.Is, d.Hs, dv->x_st, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
-            CKI(qtts_gemv(a, st));
+            CKI(pgemv(dv, a, PK_GEMV_SUB));
             a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, dv->x_st, d.Hs, nb, EPI_RESID);
             a.nt = 0;
-            CKI(qtts_gemv(a, st));
+            CKI(pgemv(dv, a, PK_GEMV_SUB));
         }
         if (g == 0) continue;  // pass 0 produces no logits
         GemvArgs a = gv(dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, dv->x_st, d.Hs, dv->logits_s, d.Vs, nb,
                         EPI_STORE);
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
-        CKI(qtts_gemv(a, st));
+        CKI(pgemv(dv, a, PK_GEMV_SUB));
         SampArgs s;
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
         s.mode = 0; s.st_rng = dv->st_rng; s.stopped = dv->stopped; s.cur_row = dv->cur_row;
         s.codes = dv->codes; s.codes_bstride = cstride; s.G = d.G; s.g = g;
-        CKI(qtts_sample(s, st));
+        { ProfScope ps(dv, PK_SAMPLE, 0); CKI(qtts_sample(s, st)); }
     }
     return 0;
 }
@@ -595,6 +624,7 @@ static int embed_sum(qtts_dev *dv, int advance) {
     e.cur_row = dv->cur_row; e.stopped = dv->stopped; e.codec_emb = dv->codec_emb; e.st_emb = dv->st_emb;
     e.Vs = d.Vs; e.H = d.H; e.nb = dv->nrun; e.trailing = dv->trailing; e.tr_cap = dv->tr_cap;
     e.n_trailing = dv->n_trailing; e.pad = dv->pad_emb; e.out = dv->x_tk; e.kv_len = dv->kv_len; e.advance = advance;
+    ProfScope ps(dv, PK_EMBED, 0);
     return qtts_embed_sum(e, dv->st);
 }
 
@@ -932,4 +962,28 @@ extern "C" int qtts_hip_sample_top_k(int *out, const float *logits, int vocab, i
     s.logits = logits; s.ld = vocab; s.n = vocab; s.nb = batch; s.top_k = top_k; s.top_p = top_p; s.temp = temp;
     s.mode = 0; s.st_rng = rng_bits; s.out_tok = out;
     return qtts_sample(s, (hipStream_t)stream);
+}
+
+// One frame run eagerly with an event pair around every kernel launch on the
+// context stream; returns the number of kernels, fills kind/bytes/ms.
+extern "C" int qtts_dev_profile_frame(qtts_dev_t *dv, int step, int max, int *kind, double *bytes, float *ms) {
+    if (!dv || dv->nb < 1) return -1;
+    hipSetDevice(dv->device);
+    CK(hipStreamSynchronize(dv->st));
+    dv->prof.clear();
+    dv->profiling = true;
+    int rc = record_frame(dv, step > 0);
+    dv->profiling = false;
+    CK(hipStreamSynchronize(dv->st));
+    int n = 0;
+    for (auto &p : dv->prof) {
+        float t = 0.f;
+        hipEventElapsedTime(&t, p.a, p.b);
+        if (n < max) { kind[n] = p.kind; bytes[n] = p.bytes; ms[n] = t; }
+        ++n;
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    dv->prof.clear();
+    return rc ? -1 : n;
 }
