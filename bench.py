@@ -58,24 +58,31 @@ def barrier(ws):
         dist.barrier()
 
 
-def reduce_max(ws, v):
+def _reduce(ws, v, op):
     if ws == 1:
         return v
     import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"   # RCCL on the box, gloo in CPU tests
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def reduce_max(ws, v):
+    import torch.distributed as dist
+    return _reduce(ws, v, dist.ReduceOp.MAX)
 
 
 def reduce_sum(ws, v):
-    if ws == 1:
-        return v
-    import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(ws, v, dist.ReduceOp.SUM)
+
+
+def rank_prompt_seeds(rank, batch):
+    """Utterances of rank r: prompt seeds 1234 + r*batch + i (SURVEY.md 8e:
+    independent utterances, static partition, no exchange step)."""
+    return [1234 + rank * batch + i for i in range(batch)]
 
 
 def ensure_model_shared(md, preset, ws, local):
@@ -177,7 +184,7 @@ def main():
     m = qtts.QwenTTS(md, device=local)
     log(f"[bench] rank {rank}: model loaded on HIP device {local} in {time.time() - t:.1f}s")
     m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
-    prompts = [prompt_ids("p128", seed=1234 + rank * args.batch + i) for i in range(args.batch)]
+    prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
 
     def one_step():
         if args.batch == 1:

@@ -210,6 +210,8 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
+/* sizeof(qwen_tts_ctx_t) as compiled into the library (FFI layout check) */
+size_t qwen_tts_abi_sizeof_ctx(void);
 
 extern int qwen_tts_verbose;
 

@@ -62,13 +62,14 @@ EXPORTS = [
     "qwen_tts_load", "qwen_tts_free", "qwen_tts_set_progress_callback", "qwen_tts_generate", "qwen_tts_write_wav",
     "qwen_tts_talker_prefill", "qwen_tts_talker_forward", "qwen_tts_subtalker_generate", "qwen_tts_codec_decode",
     "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
-    "qwen_tts_verbose",
+    "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
     "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
     "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
     "qtts_hip_transposed_conv1d", "qtts_hip_snake_beta", "qtts_hip_expf_glibc", "qtts_hip_sync",
+    "qtts_dev_profile_frame",
 ]
 
 _LIB = None

@@ -1,0 +1,178 @@
+"""HIP kernels through the kernel-level C-ABI (include/qtts_hip.h) against
+the reference's golden I/O and the CPU oracle.
+
+Bars: integer outputs (sampled ids, RNG state) bit-exact; fp32 GEMV within
+|err| <= 2e-6 * sum|a_i x_i| + 1e-6 (accumulation order differs: 8-lane
+partials + KSPLIT slots vs the reference's sequential loop); codec convs on
+the fp32 MFMA path within 2e-5 abs + 1e-4 rel.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle_py import fptr
+from qtts_io import f32_to_bf16
+
+import qtts
+
+pytestmark = pytest.mark.gpu
+K = golden("kernels.npz")
+
+
+def T(a, dev, dtype=None):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.view(dtype)
+    return t.to(dev)
+
+
+def bf16_f64(A):
+    return (A.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+def gemv_bound(A, x):
+    return 2e-6 * (np.abs(bf16_f64(A)) @ np.abs(x.astype(np.float64).T)).T + 1e-6
+
+
+def run_matvec(dev, A, x, B):
+    import torch
+    R, Cc = A.shape
+    out = torch.zeros(B * R, device=dev)
+    qtts.Kernels.matvec_bf16(out, T(A, dev, torch.int16), T(x, dev), R, Cc, B)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().reshape(B, R)
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_matvec_golden(gpu, i):
+    A, x, y = K[f"matvec{i}_A"], K[f"matvec{i}_x"], K[f"matvec{i}_y"]
+    got = run_matvec(gpu, A, x[None], 1)[0]
+    assert np.all(np.abs(got - y) <= gemv_bound(A, x[None])[0])
+
+
+# decode shapes of the 1.7B talker / sub-talker + ragged ones
+SHAPES = [(4096, 2048, 1), (2048, 2048, 1), (12288, 2048, 1), (2048, 6144, 1), (3072, 2048, 1), (4096, 1024, 1),
+          (1024, 2048, 1), (6144, 1024, 1), (1024, 3072, 1), (2048, 1024, 1), (100, 64, 1), (37, 8192, 1),
+          (2048, 2048, 2), (4096, 1024, 4), (1000, 192, 3), (3072, 2048, 8), (257, 1024, 16)]
+
+
+@pytest.mark.parametrize("R,Cc,B", SHAPES)
+def test_matvec_shapes(gpu, R, Cc, B):
+    rng = np.random.default_rng(R * 7 + Cc + B)
+    A = f32_to_bf16((rng.standard_normal((R, Cc)) / np.sqrt(Cc)).astype(np.float32))
+    x = rng.standard_normal((B, Cc)).astype(np.float32)
+    got = run_matvec(gpu, A, x, B)
+    ref = x.astype(np.float64) @ bf16_f64(A).T
+    assert np.all(np.abs(got - ref) <= gemv_bound(A, x)), np.abs(got - ref).max()
+
+
+@pytest.mark.parametrize("R,Cc,B", [(4096, 2048, 1), (2048, 1024, 1), (512, 128, 1), (1024, 2048, 4)])
+def test_rmsnorm_matvec(gpu, R, Cc, B):
+    import torch
+    rng = np.random.default_rng(5 + B)
+    A = f32_to_bf16((rng.standard_normal((R, Cc)) / np.sqrt(Cc)).astype(np.float32))
+    x = (rng.standard_normal((B, Cc)) * 3).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(Cc)).astype(np.float32)
+    out = torch.zeros(B * R, device=gpu)
+    qtts.Kernels.rmsnorm_matvec_bf16(out, T(A, gpu, torch.int16), T(x, gpu), T(w, gpu), 1e-6, R, Cc, B)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(B, R)
+    xn = x / np.sqrt((x.astype(np.float64) ** 2).mean(1, keepdims=True) + 1e-6) * w
+    ref = xn @ bf16_f64(A).T
+    assert np.all(np.abs(got - ref) <= gemv_bound(A, xn) + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
+
+
+def sample_gpu(dev, lg, V, k, tp, temp, rng_bits):
+    import torch
+    B = lg.shape[0]
+    out = torch.zeros(B, dtype=torch.int32, device=dev)
+    rs = T(np.asarray(rng_bits, np.uint32).view(np.int32), dev)
+    qtts.Kernels.sample_top_k(out, T(lg, dev), V, k, tp, temp, rs, B)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), rs.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("V", [2048, 3072])
+def test_sampler_golden_bit_exact(gpu, V):
+    lg, meta, fm, rs = K[f"samp{V}_logits"], K[f"samp{V}_meta"], K[f"samp{V}_fmeta"], K[f"samp{V}_rng"]
+    for i in range(len(lg)):
+        r, st = sample_gpu(gpu, lg[i:i + 1], V, int(meta[i, 0]), float(fm[i, 0]), float(fm[i, 1]), [rs[i, 0]])
+        assert r[0] == meta[i, 1], (i, r[0], meta[i])
+        assert st[0] == rs[i, 1], i
+
+
+def test_sampler_random_vs_oracle(gpu, oracle):
+    """Many draws, ties, -inf, top_p cut, k=0/1/large, batched rows with their
+    own RNG states: ids and RNG state bit-exact."""
+    rng = np.random.default_rng(123)
+    for it in range(40):
+        V = [2048, 3072, 1500, 64][it % 4]
+        B = [1, 3, 8][it % 3]
+        lg = (rng.standard_normal((B, V)) * rng.uniform(0.3, 8)).astype(np.float32)
+        if it % 3 == 0:
+            lg[:, rng.integers(0, V, 30)] = lg.max()
+        if it % 5 == 1:
+            lg[:, rng.integers(0, V, V // 3)] = -1e9
+        k = int([1, 50, 0, 7, 300, 2048][it % 6])
+        tp = float([1.0, 0.9, 0.5, 0.99][it % 4])
+        temp = float(rng.uniform(0.4, 1.6))
+        st0 = (rng.integers(1, 10**6, B)).astype(np.float32)
+        r, st = sample_gpu(gpu, lg, V, k, tp, temp, st0.view(np.uint32))
+        for b in range(B):
+            s = np.array([st0[b]], np.float32)
+            e = oracle.lib.orc_sample(fptr(lg[b].copy()), V, k, tp, temp, fptr(s))
+            assert r[b] == e, (it, b, r[b], e)
+            assert st[b] == s.view(np.uint32)[0], (it, b)
+
+
+@pytest.mark.parametrize("i", range(5))
+def test_causal_conv1d_golden(gpu, i):
+    import torch
+    ci, co, k, L, d, g = (int(v) for v in K[f"conv{i}_cfg"])
+    out = torch.zeros(co * L, device=gpu)
+    qtts.Kernels.causal_conv1d(out, T(K[f"conv{i}_x"], gpu), T(K[f"conv{i}_w"], gpu), T(K[f"conv{i}_b"], gpu),
+                               ci, co, k, L, d, g)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy().reshape(co, L), K[f"conv{i}_y"], atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("i", range(5))
+def test_transposed_conv1d_golden(gpu, i):
+    import torch
+    ci, co, k, s, L = (int(v) for v in K[f"tconv{i}_cfg"])
+    out = torch.zeros(co * L * s, device=gpu)
+    qtts.Kernels.transposed_conv1d(out, T(K[f"tconv{i}_x"], gpu), T(K[f"tconv{i}_w"], gpu),
+                                   T(K[f"tconv{i}_b"], gpu), ci, co, k, s, L)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy().reshape(co, L * s), K[f"tconv{i}_y"], atol=2e-5, rtol=1e-4)
+
+
+def test_snake_golden(gpu):
+    import torch
+    x = K["snake_x"]
+    out = torch.zeros(x.size, device=gpu)
+    qtts.Kernels.snake_beta(out, T(x, gpu), T(K["snake_a"], gpu), T(K["snake_ib"], gpu), x.shape[0], x.shape[1])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy().reshape(x.shape), K["snake_y"], atol=2e-6, rtol=2e-6)
+
+
+def test_expf_glibc_matches_libm(gpu):
+    """The sampler's expf replica is bit-identical to glibc expf (the
+    reference's softmax/top-p arithmetic, K.c:371-378, 480-520)."""
+    import torch
+    libm = C.CDLL("libm.so.6")
+    libm.expf.restype = C.c_float
+    libm.expf.argtypes = [C.c_float]
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.uniform(-104, 89, 150000), rng.uniform(-1, 1, 30000), np.linspace(-87.4, 88.7, 20000),
+                        [0.0, -0.0, 88.72283, -103.97, 1e-30, -1e-30]]).astype(np.float32)
+    out = torch.zeros(len(x), device=gpu)
+    qtts.Kernels.expf_glibc(out, T(x, gpu), len(x))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ref = np.array([libm.expf(float(v)) for v in x], np.float32)
+    bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))[0]
+    assert len(bad) == 0, (len(bad), x[bad[:5]], got[bad[:5]], ref[bad[:5]])

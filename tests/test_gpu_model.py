@@ -1,0 +1,191 @@
+"""The HIP hot path (talker + sub-talker decode, on-device sampling, codec)
+through the drop-in C-ABI (include/qwen_tts.h) against the reference's golden
+outputs (tests/golden/, produced by the reference c/ build) and the oracle.
+
+Bars (BASELINE.json north_star): codebook ids bit-exact; waveform MSE < 1e-4
+(asserted, plus a tighter max-abs regression bar of 1e-4 since the fp32 path
+differs from the reference only in summation order).  Hidden states / logits:
+allclose(atol=1e-4, rtol=1e-4).
+"""
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import golden, manifest, model_dir
+from oracle_py import GREEDY, DEFAULT, Oracle
+from qtts_io import lookup_ids
+from synth_model import prompt_ids
+from test_oracle_golden import RUNS
+
+import qtts
+
+pytestmark = pytest.mark.gpu
+S = golden("stages_tiny.npz")
+E = golden("e2e_tiny.npz")
+
+
+def audio_close(a, ref):
+    assert a is not None and a.shape == ref.shape, (None if a is None else a.shape, ref.shape)
+    mse = float(np.mean((a.astype(np.float64) - ref) ** 2)) if len(ref) else 0.0
+    assert mse < 1e-4, mse
+    if len(ref):
+        assert np.abs(a - ref).max() < 1e-4, np.abs(a - ref).max()
+
+
+def test_stage_prefill_and_step(tts_tiny):
+    h = tts_tiny.prefill(S["prefill_embeds"])
+    np.testing.assert_allclose(h, S["prefill_hidden"], atol=1e-4, rtol=1e-4)
+    lg, hid = tts_tiny.step(S["step_embed"])
+    np.testing.assert_allclose(lg, S["step_logits"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(hid, S["step_hidden"], atol=1e-4, rtol=1e-4)
+
+
+def test_stage_subtalker(tts_tiny):
+    m = tts_tiny
+    m.set_params(**{"st_top_k": 1, "st_temperature": 1.0, "st_top_p": 1.0})
+    np.testing.assert_array_equal(m.subtalker(S["step_hidden"], 5), S["st_greedy_codes"])
+    m.set_params(seed=42, st_top_k=50, st_temperature=0.9, st_top_p=1.0)
+    np.testing.assert_array_equal(m.subtalker(S["step_hidden"], 5), S["st_sampled_codes"])
+
+
+def test_stage_codec(tts_tiny):
+    a = tts_tiny.codec_decode(S["codec_codes"])
+    audio_close(a, S["codec_audio"])
+
+
+def test_codec_edge_lengths(tts_tiny, oracle):
+    """T = 1 (first packet), T crossing the 72-frame attention window, and
+    codes out of range (zero contribution, Cd.c:150-160)."""
+    rng = np.random.default_rng(3)
+    for T in (1, 2, 73, 150):
+        codes = rng.integers(0, 2048, size=(T, 16)).astype(np.int32)
+        codes[0, 3] = -1
+        codes[-1, 5] = 4096
+        audio_close(tts_tiny.codec_decode(codes), oracle.codec_decode(codes))
+
+
+def _gen(m, name):
+    fx, pp, fixed, mx, seed = RUNS[name]
+    m.set_params(max_tokens=mx, fixed=fixed, seed=seed, **pp)
+    return m.generate(prompt_ids("short"), "aiden", "english")
+
+
+@pytest.mark.parametrize("name", sorted(RUNS))
+def test_e2e_codes_bit_exact_and_audio(name, request):
+    fx = RUNS[name][0]
+    m = qtts.QwenTTS(request.getfixturevalue(fx))
+    try:
+        a = _gen(m, name)
+        codes = m.last_codes()
+        np.testing.assert_array_equal(codes, E[f"{name}_codes"])
+        audio_close(a, E[f"{name}_audio"])
+        assert m.c.perf_codec_tokens == manifest()["stop_tokens"][name]
+        # determinism: a second run on the same ctx gives the same codes
+        _gen(m, name)
+        np.testing.assert_array_equal(m.last_codes(), codes)
+    finally:
+        m.close()
+
+
+def test_eos_stop_reported_like_reference(tts_tiny):
+    m = qtts.QwenTTS(model_dir("tiny", eos_gain=manifest()["eos_gain"]))
+    try:
+        _gen(m, "eosg")
+        want = int(re.search(r"step (\d+)", manifest()["cli_eos"]["stop_line"]).group(1))
+        assert m.c.last_stop_reason == 1 and m.c.last_stop_step == want
+        _gen(m, "eos")  # max_tokens stop on this model? (it may stop on EOS first)
+    finally:
+        m.close()
+
+
+def test_batch_slots_match_single_runs(tiny_dir, oracle):
+    """Lock-step batch (B GEMV columns, one weight read per frame): every
+    slot's audio equals the oracle's for its own prompt / speaker."""
+    m = qtts.QwenTTS(tiny_dir)
+    try:
+        prompts = [prompt_ids("short"), prompt_ids("p128", 1240), prompt_ids("p128", 1241)]
+        spk = ["aiden", "vivian", "serena"]
+        lang = ["english", "japanese", "chinese"]
+        for pp, fixed, mx in ((GREEDY, 12, 4096), (DEFAULT, 12, 4096)):
+            m.set_params(max_tokens=mx, fixed=fixed, seed=42, **pp)
+            rc, audio = m.generate_batch(prompts, spk, lang)
+            assert rc == 0
+            for b in range(3):
+                s, l = lookup_ids(oracle.cfg, spk[b], lang[b])
+                codes, _ = oracle.generate_codes(prompts[b], s, l, max_tokens=mx, fixed=fixed, seed=42, **pp)
+                audio_close(audio[b], oracle.codec_decode(codes))
+    finally:
+        m.close()
+
+
+def test_batch_eos_slots_stop_independently(tiny_eos_dir):
+    """Slots stop at their own EOS; finished slots keep their frame count."""
+    o = Oracle(tiny_eos_dir)
+    m = qtts.QwenTTS(tiny_eos_dir)
+    try:
+        prompts = [prompt_ids("short"), prompt_ids("p128", 1300), prompt_ids("p128", 1301), prompt_ids("short")]
+        m.set_params(max_tokens=32, fixed=0, seed=7, **DEFAULT)
+        rc, audio = m.generate_batch(prompts, ["aiden"] * 4, ["english"] * 4)
+        assert rc == 0
+        s, l = lookup_ids(o.cfg, "aiden", "english")
+        for b in range(4):
+            codes, _ = o.generate_codes(prompts[b], s, l, max_tokens=32, fixed=0, seed=7, **DEFAULT)
+            audio_close(audio[b], o.codec_decode(codes))
+    finally:
+        m.close()
+        o.close()
+
+
+def test_cli_eos_regression_like_reference(tiny_eos_dir):
+    """test/test_eos_regression.py's check on our CLI: greedy flags, the same
+    `Stop: eos at step N` line and WAV as the reference CLI (+-1 LSB)."""
+    man = manifest()["cli_eos"]
+    ids = ",".join(str(i) for i in prompt_ids("short"))
+    with tempfile.TemporaryDirectory() as d:
+        wav = os.path.join(d, "o.wav")
+        r = subprocess.run([qtts.CLI_PATH, "-d", tiny_eos_dir, "-t", ids, "-o", wav] + man["args"],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert man["stop_line"] in r.stderr
+        g = re.search(r"Generated (\d+) codec tokens in [\d.]+ ms \([\d.]+ ms/token\)", r.stderr)
+        assert g and int(g.group(1)) == man["generated"]
+        assert re.search(r"Total: [\d.]+ ms \([\d.]+ s audio, [\d.]+x realtime\)", r.stderr)
+        pcm = np.frombuffer(open(wav, "rb").read()[44:], np.int16)
+    ref = golden("wav.npz")["cli_eos_pcm"]
+    assert pcm.shape == ref.shape
+    assert np.abs(pcm.astype(np.int32) - ref).max() <= 1
+
+
+def test_cli_persistent_benchmark_lines(tiny_dir):
+    ids = ",".join(str(i) for i in prompt_ids("short"))
+    r = subprocess.run([qtts.CLI_PATH, "-d", tiny_dir, "-t", ids, "-o", os.devnull, "--fixed-codec-tokens", "8",
+                        "--benchmark-runs", "2", "--benchmark-warmup", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    runs = re.findall(r"\[persistent\] run (\d+)/(\d+): elapsed=[\d.]+ ms, audio=[\d.]+s, talker=[\d.]+ ms, "
+                      r"codec=[\d.]+ ms, total=[\d.]+ ms, tokens=(\d+)", r.stderr + r.stdout)
+    assert len(runs) == 2 and all(t == "8" for _, _, t in runs)
+
+
+def test_progress_callback_and_params(tts_tiny):
+    import ctypes as C
+    steps = []
+    cb = qtts.PROGRESS_CB(lambda s, t, u: steps.append((s, t)))
+    qtts.lib().qwen_tts_set_progress_callback(tts_tiny.ctx, cb, None)
+    try:
+        tts_tiny.set_params(max_tokens=4096, fixed=6, seed=1, **GREEDY)
+        a = tts_tiny.generate(prompt_ids("short"), "aiden", "english")
+        assert a is not None and len(a) == 6 * 1920
+        assert [s for s, _ in steps] == list(range(1, 7)) or len(steps) == 6
+    finally:
+        qtts.lib().qwen_tts_set_progress_callback(tts_tiny.ctx, C.cast(None, qtts.PROGRESS_CB), None)
+
+
+def test_unknown_speaker_warns_and_continues(tts_tiny):
+    tts_tiny.set_params(max_tokens=4096, fixed=3, seed=1, **GREEDY)
+    a = tts_tiny.generate(prompt_ids("short"), "nobody", "klingon")
+    assert a is not None and len(a) == 3 * 1920
