@@ -80,6 +80,14 @@ def lib():
     global _LIB
     if _LIB is not None:
         return _LIB
+    # torch bundles its own HIP runtime with the same soname (libamdhip64.so.7)
+    # as /opt/rocm's.  Loading torch first makes this library bind to that one
+    # runtime, so torch tensors, streams and our launches share it; loading
+    # ours first would put two HIP runtimes in the process and break torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C qwen3-tts-c_amd` (or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
