@@ -91,13 +91,12 @@ def test_e2e_codes_bit_exact_and_audio(name, request):
         m.close()
 
 
-def test_eos_stop_reported_like_reference(tts_tiny):
+def test_eos_stop_reported_like_reference(gpu):
     m = qtts.QwenTTS(model_dir("tiny", eos_gain=manifest()["eos_gain"]))
     try:
         _gen(m, "eosg")
         want = int(re.search(r"step (\d+)", manifest()["cli_eos"]["stop_line"]).group(1))
         assert m.c.last_stop_reason == 1 and m.c.last_stop_step == want
-        _gen(m, "eos")  # max_tokens stop on this model? (it may stop on EOS first)
     finally:
         m.close()
 
