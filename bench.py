@@ -26,6 +26,7 @@ Also reported:
                    on a bounded sample of the same workload, rank 0, N=1 only
 """
 import argparse
+import glob
 import json
 import os
 import re
@@ -95,37 +96,76 @@ def ensure_model_shared(md, preset, ws, local):
     barrier(ws)
 
 
+def _latest_profile(pattern):
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    return fs[-1] if fs else None
+
+
+def _rocprof_lookup(kname):
+    """Average duration (us) of `kname` in the newest committed rocprofv3
+    --stats summary and its HBM bytes per launch in the newest PMC summary
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/prof_summary.py)."""
+    avg_us = traffic = None
+    src = {}
+    f = _latest_profile("*kernel_stats.csv")
+    if f:
+        import csv
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kname + "(" in row.get("Name", "") or row.get("Name", "").endswith(kname):
+                    avg_us = float(row["AverageNs"]) / 1e3
+                    src["stats"] = os.path.relpath(f, ROOT)
+                    break
+    f = _latest_profile("*pmc.json")
+    if f:
+        with open(f) as fh:
+            pm = json.load(fh)
+        for name, e in pm.items():
+            if kname + "(" in name and "hbm_read_bytes_avg" in e:
+                traffic = e["hbm_read_bytes_avg"] + e.get("hbm_write_bytes_avg", 0.0)
+                src["pmc"] = os.path.relpath(f, ROOT)
+                break
+    return avg_us, traffic, src
+
+
 def profile_roofline(m, lib):
-    """One eager frame with HIP events around every kernel (qtts_dev_profile_frame)."""
+    """One eager frame with HIP events around every kernel launch on the
+    context stream (qtts_dev_profile_frame); the dominant kernel is the GEMV
+    instantiation with the largest share of the frame."""
     import ctypes as C
     n_max = 4096
     kind = (C.c_int * n_max)()
     byt = (C.c_double * n_max)()
     ms = (C.c_float * n_max)()
+    names = C.create_string_buffer(n_max * 64)
     lib.qtts_dev_profile_frame.restype = C.c_int
-    lib.qtts_dev_profile_frame.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
-    n = lib.qtts_dev_profile_frame(m.c.hip, 1, n_max, kind, byt, ms)
+    lib.qtts_dev_profile_frame.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]
+    n = lib.qtts_dev_profile_frame(m.c.hip, 1, n_max, kind, byt, ms, names)
     if n <= 0:
         return None
     k = np.array(kind[:n])
     b = np.array(byt[:n])
     t = np.array(ms[:n], dtype=np.float64)
-    names = {0: "gemv_talker", 1: "gemv_subtalker", 2: "attention", 3: "sampler", 4: "embed_sum"}
-    share = {names[i]: float(t[k == i].sum()) for i in names}
-    frame_ms = float(t.sum())
-    # dominant kernel: the GEMV class with the largest share of the frame
-    dom = 0 if share["gemv_talker"] >= share["gemv_subtalker"] else 1
-    sel = k == dom
-    avg_bytes = float(b[sel].mean())
-    avg_ms = float(t[sel].mean())
-    achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
-    # the largest single launch (talker gate|up GEMV) as a bandwidth probe
-    imax = int(np.argmax(np.where(k == 0, b, -1)))
-    big = {"bytes": float(b[imax]), "ms": float(t[imax]), "GBs": float(b[imax] / (t[imax] * 1e-3) / 1e9)}
-    return dict(kernel=("k_gemv<1,true> (talker weight stream)" if dom == 0
-                        else "k_gemv<1,false> (sub-talker weight stream)"),
-                launches_per_frame=int(sel.sum()), avg_bytes=avg_bytes, avg_ms=avg_ms, achieved_GBs=achieved,
-                frame_kernel_ms=frame_ms, share_ms=share, n_kernels=n, biggest_launch=big,
+    nm = [names.raw[i * 64:(i + 1) * 64].split(b"\0", 1)[0].decode() for i in range(n)]
+    classes = {0: "gemv_talker", 1: "gemv_subtalker", 2: "attention", 3: "sampler", 4: "embed_sum"}
+    share = {classes[i]: float(t[k == i].sum()) for i in classes}
+    per_kernel = {}
+    for i in range(n):
+        e = per_kernel.setdefault(nm[i], [0, 0.0, 0.0])
+        e[0] += 1
+        e[1] += t[i]
+        e[2] += b[i]
+    gemv = {x: e for x, e in per_kernel.items() if e[2] > 0}
+    dom = max(gemv, key=lambda x: gemv[x][1])
+    cnt, tot_ms, tot_b = gemv[dom]
+    avg_ms, avg_bytes = tot_ms / cnt, tot_b / cnt
+    rp_us, traffic, src = _rocprof_lookup(dom)
+    return dict(kernel=dom, launches_per_frame=cnt, avg_bytes=avg_bytes, avg_ms=avg_ms,
+                achieved_GBs=avg_bytes / (avg_ms * 1e-3) / 1e9, rocprof_avg_us=rp_us, traffic=traffic,
+                profile_src=src, frame_kernel_ms=float(t.sum()), share_ms=share, n_kernels=n,
+                kernels={x: {"launches": e[0], "ms": round(e[1], 4), "GBs": round(e[2] / (e[1] * 1e-3) / 1e9, 1)
+                             if e[2] else None} for x, e in sorted(per_kernel.items(), key=lambda kv: -kv[1][1])},
                 gemv_bytes_per_frame=float(b[(k == 0) | (k == 1)].sum()),
                 gemv_ms_per_frame=float(t[(k == 0) | (k == 1)].sum()))
 
@@ -258,15 +298,19 @@ def main():
         if roof:
             out["roofline"] = {"bound": "hbm", "achieved": round(roof["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(roof["achieved_GBs"] / HBM_PEAK_GBS, 4),
-                               "traffic": None, "kernel": roof["kernel"],
+                               "traffic": None if roof["traffic"] is None else int(roof["traffic"]),
+                               "kernel": roof["kernel"],
                                "avg_launch_us": round(roof["avg_ms"] * 1e3, 2),
+                               "rocprof_avg_us": None if roof["rocprof_avg_us"] is None
+                               else round(roof["rocprof_avg_us"], 2),
                                "avg_launch_bytes": int(roof["avg_bytes"]),
-                               "launches_per_frame": roof["launches_per_frame"]}
+                               "launches_per_frame": roof["launches_per_frame"],
+                               "profiles": roof["profile_src"]}
             out["frame_profile"] = {"kernel_ms_per_frame": round(roof["frame_kernel_ms"], 3),
                                     "share_ms": {k: round(v, 3) for k, v in roof["share_ms"].items()},
                                     "gemv_GBs_all": round(roof["gemv_bytes_per_frame"] /
                                                           (roof["gemv_ms_per_frame"] * 1e-3) / 1e9, 1),
-                                    "biggest_gemv": {k: round(v, 4) for k, v in roof["biggest_launch"].items()},
+                                    "kernels": roof["kernels"],
                                     "n_kernels": roof["n_kernels"]}
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

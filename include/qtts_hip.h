@@ -136,10 +136,12 @@ int qtts_hip_sync(void);
 /* Diagnostics: run ONE frame eagerly on the current generation state with an
  * event pair around every kernel launch on the context stream.  kind[i]:
  * 0 talker GEMV, 1 sub-talker GEMV, 2 attention, 3 sampler, 4 embed-sum;
- * bytes[i]: algorithmic bytes of GEMV launches; ms[i]: measured duration.
+ * bytes[i]: algorithmic bytes of GEMV launches; ms[i]: measured duration;
+ * names (optional, max*64 chars): kernel instantiation of launch i as
+ * rocprofv3 names it (e.g. "k_gemv1<8, 2, true>").
  * Returns the number of kernels (<0 on error).  Advances the state by one
  * frame, so call it after a generation, not in the middle of one. */
-int qtts_dev_profile_frame(qtts_dev_t *dev, int step, int max, int *kind, double *bytes, float *ms);
+int qtts_dev_profile_frame(qtts_dev_t *dev, int step, int max, int *kind, double *bytes, float *ms, char *names);
 
 #ifdef __cplusplus
 }

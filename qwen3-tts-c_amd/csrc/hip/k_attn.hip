@@ -175,15 +175,248 @@ __global__ __launch_bounds__(256) void k_qk_prep(AttnArgs a) {
     (void)red;
 }
 
+
+// ---------------------------------------------------------------------------
+// Decode attention, split over keys (flash-decoding) for one kv head per
+// workgroup: grid (KV, nsplit, rows).  A workgroup serves all GPH query heads
+// of its kv head (each K/V row is read once for them), keys
+// [split*CH, min(n, split*CH + CH)).  Per workgroup:
+//   prologue  one wave per head: per-head RMSNorm (T.c:150-156) -> LDS, then
+//             rotate-half RoPE from the host table (T.c:158-189); the split
+//             that holds the current token writes its k, v to the cache
+//             (T.c:191-196) and reads them from LDS.
+//   scores    LPK lanes per key (DPL dims each, float4 loads), GPH dots per
+//             key, lane-pair shuffles; one pass (CH = 256 / LPK keys).
+//   softmax   one wave per head: chunk max, exp, sum (K.c:371-378).
+//   P.V       HD/4 lanes x KG key groups, float4 V rows, LDS reduction.
+// With one active split the normalised result is written directly; otherwise
+// each split leaves (acc, max, sum) in scratch, and the last split to finish
+// (agent-scope acq_rel ticket) merges them in split order and resets the
+// ticket.  Grid size is fixed at graph capture (nsplit from the cache
+// capacity); splits past the live length exit at once.
+template <int HD, int GPH>
+__global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
+    constexpr int LPK = HD >= 32 ? HD / 32 : 1;   // lanes per key
+    constexpr int DPL = HD / LPK;                  // dims per lane
+    constexpr int CH = 256 / LPK;                  // keys per workgroup
+    constexpr int D4 = HD / 4;
+    constexpr int KG = 256 / D4;                   // key groups in P.V
+    constexpr int NO = GPH * HD;                   // outputs per workgroup
+    __shared__ __attribute__((aligned(16))) float xn[(GPH + 1) * HD];
+    __shared__ __attribute__((aligned(16))) float qk[(GPH + 1) * HD];   // rotated q heads, then k
+    __shared__ __attribute__((aligned(16))) float vv[HD];
+    __shared__ float sc[GPH][CH];
+    __shared__ float ml[GPH][2];
+    __shared__ __attribute__((aligned(16))) float red[KG * NO];
+    __shared__ int last;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int kvh = blockIdx.x, split = blockIdx.y, r = blockIdx.z;
+    const int KVD = a.KV * HD;
+    const int p = a.pos ? a.pos[r] : a.pos_const;
+    const int n = p + 1;
+    const int nact = (n + CH - 1) / CH;
+    if (split >= nact) return;
+    const int t0 = split * CH;
+    const int t1 = min(n, t0 + CH);
+    const bool owner = (split == nact - 1);        // holds the current token
+    const float *row = a.qkv + (size_t)r * a.ld_qkv;
+    const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
+    const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
+
+    // ---- prologue: q heads (waves 0..GPH-1), k head (wave GPH), v ----
+    for (int hh = w; hh <= GPH; hh += 4) {
+        const float *src = hh < GPH ? row + (kvh * GPH + hh) * HD : row + a.NH * HD + kvh * HD;
+        const float *nw = hh < GPH ? a.qn_w : a.kn_w;
+        float v[(HD + 63) / 64];
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < (HD + 63) / 64; ++j) {
+            const int i = lane + 64 * j;
+            v[j] = i < HD ? src[i] : 0.f;
+            ss += v[j] * v[j];
+        }
+        ss = wave_sum(ss);
+        const float iv = rms_inv(ss, HD, a.eps);
+#pragma unroll
+        for (int j = 0; j < (HD + 63) / 64; ++j) {
+            const int i = lane + 64 * j;
+            if (i < HD) xn[hh * HD + i] = v[j] * iv * nw[i];
+        }
+    }
+    if (owner && tid < HD) vv[tid] = row[(a.NH + a.KV) * HD + kvh * HD + tid];
+    __syncthreads();
+    {
+        const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
+        for (int i = tid; i < (GPH + 1) * HD; i += 256) {
+            const int e = i % HD, hb = i - e;
+            constexpr int half = HD / 2;
+            qk[i] = e < half ? xn[i] * cs[e] - xn[hb + e + half] * sn[e] : xn[i] * cs[e] + xn[hb + e - half] * sn[e];
+        }
+    }
+    __syncthreads();
+    if (owner && tid < HD && !(a.skip && a.skip[r])) {
+        a.kc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = qk[GPH * HD + tid];
+        a.vc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = vv[tid];
+    }
+
+    // ---- scores ----
+    const float scale = div_rn(1.0f, sqrt_rn((float)HD));
+    {
+        const int kl = tid / LPK, sub = tid - kl * LPK;
+        const int t = t0 + kl;
+        float d[GPH];
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) d[g] = 0.f;
+        if (t < t1) {
+            const float *kp = (t == p) ? qk + GPH * HD + sub * DPL : Kc + (size_t)t * KVD + sub * DPL;
+            float4 kv[DPL / 4];
+#pragma unroll
+            for (int j = 0; j < DPL / 4; ++j) kv[j] = reinterpret_cast<const float4 *>(kp)[j];
+#pragma unroll
+            for (int g = 0; g < GPH; ++g) {
+                const float4 *q4 = reinterpret_cast<const float4 *>(qk + g * HD + sub * DPL);
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < DPL / 4; ++j) {
+                    const float4 q = q4[j];
+                    s += q.x * kv[j].x + q.y * kv[j].y + q.z * kv[j].z + q.w * kv[j].w;
+                }
+                d[g] = s;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) {
+#pragma unroll
+            for (int o = LPK >> 1; o >= 1; o >>= 1) d[g] += __shfl_xor(d[g], o, 64);
+            if (sub == 0) sc[g][kl] = t < t1 ? d[g] * scale : -INFINITY;
+        }
+    }
+    __syncthreads();
+    // ---- chunk softmax (unnormalised) ----
+    for (int g = w; g < GPH; g += 4) {
+        float m = -INFINITY;
+        for (int k = lane; k < CH; k += 64) m = fmaxf(m, sc[g][k]);
+        m = wave_max(m);
+        float l = 0.f;
+        for (int k = lane; k < CH; k += 64) {
+            const float e = t0 + k < t1 ? expf(sc[g][k] - m) : 0.f;
+            sc[g][k] = e;
+            l += e;
+        }
+        l = wave_sum(l);
+        if (lane == 0) { ml[g][0] = m; ml[g][1] = l; }
+    }
+    __syncthreads();
+    // ---- P.V ----
+    {
+        const int d4 = tid % D4, kg = tid / D4;
+        float4 acc[GPH];
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) acc[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+        for (int k = kg; k < CH; k += KG) {
+            const int t = t0 + k;
+            if (t < t1) {
+                const float4 v4 = (t == p) ? reinterpret_cast<const float4 *>(vv)[d4]
+                                           : reinterpret_cast<const float4 *>(Vc + (size_t)t * KVD)[d4];
+#pragma unroll
+                for (int g = 0; g < GPH; ++g) {
+                    const float pw = sc[g][k];
+                    acc[g].x += pw * v4.x; acc[g].y += pw * v4.y; acc[g].z += pw * v4.z; acc[g].w += pw * v4.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) reinterpret_cast<float4 *>(red + kg * NO + g * HD)[d4] = acc[g];
+    }
+    __syncthreads();
+    float res[(NO + 255) / 256];
+#pragma unroll
+    for (int j = 0; j < (NO + 255) / 256; ++j) {
+        const int o = tid + 256 * j;
+        float s = 0.f;
+        if (o < NO)
+            for (int k = 0; k < KG; ++k) s += red[k * NO + o];
+        res[j] = s;
+    }
+    float *outr = a.out + (size_t)r * a.ld_out + kvh * GPH * HD;
+    if (nact == 1) {
+#pragma unroll
+        for (int j = 0; j < (NO + 255) / 256; ++j) {
+            const int o = tid + 256 * j;
+            if (o < NO) outr[o] = res[j] / ml[o / HD][1];
+        }
+        return;
+    }
+    // ---- multi-split: publish partials, last split merges ----
+    const int stride = NO + 2 * GPH;
+    float *base = a.part + (size_t)(r * a.KV + kvh) * a.nsplit * stride;
+    float *mine = base + (size_t)split * stride;
+#pragma unroll
+    for (int j = 0; j < (NO + 255) / 256; ++j) {
+        const int o = tid + 256 * j;
+        if (o < NO) mine[o] = res[j];
+    }
+    if (tid < GPH) { mine[NO + 2 * tid] = ml[tid][0]; mine[NO + 2 * tid + 1] = ml[tid][1]; }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(a.cnt + r * a.KV + kvh, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = (old == nact - 1);
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+#pragma unroll
+    for (int j = 0; j < (NO + 255) / 256; ++j) {
+        const int o = tid + 256 * j;
+        if (o < NO) {
+            const int g = o / HD;
+            float M = -INFINITY;
+            for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, __builtin_nontemporal_load(base + (size_t)s2 * stride + NO + 2 * g));
+            float num = 0.f, den = 0.f;
+            for (int s2 = 0; s2 < nact; ++s2) {
+                const float *ps = base + (size_t)s2 * stride;
+                const float f = expf(__builtin_nontemporal_load(ps + NO + 2 * g) - M);
+                num += f * __builtin_nontemporal_load(ps + o);
+                den += f * __builtin_nontemporal_load(ps + NO + 2 * g + 1);
+            }
+            outr[o] = num / den;
+        }
+    }
+    if (tid == 0) __hip_atomic_store(a.cnt + r * a.KV + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
+
+int qtts_attn_keys_per_split(int HD) { return HD >= 32 ? 256 / (HD / 32) : 256; }
 
 int qtts_attention(const AttnArgs &a, hipStream_t st) {
     if (a.HD > 128 || a.HD < 8 || (a.HD & 7) || a.NH % a.KV) {
         fprintf(stderr, "qtts_attention: unsupported head config NH=%d KV=%d HD=%d\n", a.NH, a.KV, a.HD);
         return -1;
     }
+    const int gph = a.NH / a.KV;
+    if (a.mode == 0 && a.win == 0 && gph == 2 && (a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16)) {
+        const int ch = qtts_attn_keys_per_split(a.HD);
+        const int nsplit = (a.S + ch - 1) / ch;
+        if (nsplit > 1 && (!a.part || !a.cnt || a.nsplit < nsplit)) {
+            fprintf(stderr, "qtts_attention: split scratch missing (need %d splits)\n", nsplit);
+            return -1;
+        }
+        const dim3 grid(a.KV, nsplit, a.nrows);
+        switch (a.HD) {
+            case 128: hipLaunchKernelGGL((k_attn_dec<128, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<128, 2>"; break;
+            case 64: hipLaunchKernelGGL((k_attn_dec<64, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<64, 2>"; break;
+            case 32: hipLaunchKernelGGL((k_attn_dec<32, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<32, 2>"; break;
+            default: hipLaunchKernelGGL((k_attn_dec<16, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<16, 2>"; break;
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     size_t smem = (size_t)(128 * 3 + 256 + 8 + 8 * 128 + a.S + 4) * sizeof(float);
     hipLaunchKernelGGL(k_attn, dim3(a.NH, a.nrows), dim3(256), smem, st, a);
+    qtts_last_kernel = "k_attn";
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

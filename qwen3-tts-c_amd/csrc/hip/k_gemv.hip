@@ -328,6 +328,8 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a) {
 
 }  // namespace
 
+thread_local const char *qtts_last_kernel = "";
+
 // KSPLIT: grow until the grid has >= `target` workgroups (>= 2 per CU for
 // the latency hiding of a weight stream; fewer, larger blocks leave CUs idle
 // in the tail), bounded by the row length and by SwiGLU's 8-row quads.
@@ -355,8 +357,13 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
         const size_t smem = (size_t)(a.C + 40) * sizeof(float);
 #define QTTS_G1(U, X)                                                                                 \
-        if (a.nt) hipLaunchKernelGGL((k_gemv1<U, X, true>), dim3(grid), dim3(256), smem, st, a);      \
-        else hipLaunchKernelGGL((k_gemv1<U, X, false>), dim3(grid), dim3(256), smem, st, a);
+        if (a.nt) {                                                                                   \
+            hipLaunchKernelGGL((k_gemv1<U, X, true>), dim3(grid), dim3(256), smem, st, a);            \
+            qtts_last_kernel = "k_gemv1<" #U ", " #X ", true>";                                       \
+        } else {                                                                                      \
+            hipLaunchKernelGGL((k_gemv1<U, X, false>), dim3(grid), dim3(256), smem, st, a);           \
+            qtts_last_kernel = "k_gemv1<" #U ", " #X ", false>";                                      \
+        }
         if (nblk >= 8) {
             switch (xv) { case 1: QTTS_G1(8, 1) break; case 2: QTTS_G1(8, 2) break;
                           case 4: QTTS_G1(8, 4) break; default: QTTS_G1(8, 8) break; }
@@ -382,6 +389,7 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     case n:                                                                                      \
         if (a.nt) hipLaunchKernelGGL((k_gemv<n, true>), dim3(grid), dim3(256), smem, st, a);     \
         else hipLaunchKernelGGL((k_gemv<n, false>), dim3(grid), dim3(256), smem, st, a);         \
+        qtts_last_kernel = a.nt ? "k_gemv<" #n ", true>" : "k_gemv<" #n ", false>";         \
         break;
     switch (NB) {
         QTTS_GEMV_CASE(1)

@@ -53,6 +53,7 @@ __global__ void k_copy_rows(float *dst, int ldd, const float *src, int lds, cons
 
 int qtts_embed_sum(const EmbedSumArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_embed_sum, dim3((a.H + 255) / 256, a.nb), dim3(256), 0, st, a);
+    qtts_last_kernel = "k_embed_sum";
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -385,5 +385,6 @@ int qtts_sample(const SampArgs &a, hipStream_t st) {
         return -1;
     }
     hipLaunchKernelGGL(k_sample, dim3(a.nb), dim3(256), sizeof(SampSmem), st, a);
+    qtts_last_kernel = "k_sample";
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -57,7 +57,16 @@ struct AttnArgs {
     int nrows = 0;
     const int *skip = nullptr;     // decode: per-b stop flags (skip the cache write)
     int win = 0;                   // >0: sliding window (keys t > pos - win), c/qwen_tts_codec.c:363-367
+    // decode split-K scratch: [rows][KV][nsplit][GPH*HD + 2*GPH] partials, [rows][KV] tickets (zeroed)
+    float *part = nullptr;
+    int *cnt = nullptr;
+    int nsplit = 0;
 };
+int qtts_attn_keys_per_split(int HD);
+
+// Name of the kernel instantiation the last launcher on this thread chose
+// (diagnostics: per-kernel profile rows match rocprofv3's kernel names).
+extern thread_local const char *qtts_last_kernel;
 int qtts_attention(const AttnArgs &a, hipStream_t st);
 // prefill helper: q/k RMSNorm + RoPE in place on qkv rows, k/v -> cache at (row_b, pos)
 int qtts_qk_prep(const AttnArgs &a, hipStream_t st);

@@ -96,6 +96,8 @@ struct qtts_dev {
     float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
     int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
     int *stop_step = nullptr, *kv_len = nullptr, *n_trailing = nullptr;
+    float *att_part = nullptr;   // split-K decode attention partials (talker)
+    int *att_cnt = nullptr, att_nsplit = 0;
     uint32_t *rng = nullptr, *st_rng = nullptr;
     float *trailing = nullptr, *prefill = nullptr, *pad_emb = nullptr;
     // prefill / prompt scratch
@@ -108,7 +110,7 @@ struct qtts_dev {
     hipGraphExec_t g0 = nullptr, gN = nullptr;
     int graph_key = -1;
     // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
-    struct Prof { int kind; double bytes; hipEvent_t a, b; };
+    struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
     bool profiling = false;
 
@@ -434,6 +436,13 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(ppos, int, R);
     A(psrc, int, R);
     A(plast, int, B);
+    {
+        const int gph = d.NH / d.KV;
+        dv->att_nsplit = (dv->S + qtts_attn_keys_per_split(d.HD) - 1) / qtts_attn_keys_per_split(d.HD);
+        A(att_part, float, B * d.KV * dv->att_nsplit * (gph * d.HD + 2 * gph));
+        A(att_cnt, int, B * d.KV);
+        CK(hipMemsetAsync(dv->att_cnt, 0, B * d.KV * sizeof(int), dv->st));
+    }
 #undef A
     dv->p_len_h.assign(nb, 0);
     dv->n_tr_h.assign(nb, 0);
@@ -480,7 +489,7 @@ struct ProfScope {  // brackets one launch with events when profiling is on
     size_t idx;
     ProfScope(qtts_dev *d, int kind, double bytes) : dv(d), idx((size_t)-1) {
         if (!dv->profiling) return;
-        qtts_dev::Prof p{kind, bytes, nullptr, nullptr};
+        qtts_dev::Prof p{kind, bytes, nullptr, nullptr, ""};
         hipEventCreate(&p.a);
         hipEventCreate(&p.b);
         hipEventRecord(p.a, dv->st);
@@ -488,7 +497,9 @@ struct ProfScope {  // brackets one launch with events when profiling is on
         idx = dv->prof.size() - 1;
     }
     ~ProfScope() {
-        if (idx != (size_t)-1) hipEventRecord(dv->prof[idx].b, dv->st);
+        if (idx == (size_t)-1) return;
+        hipEventRecord(dv->prof[idx].b, dv->st);
+        dv->prof[idx].name = qtts_last_kernel;
     }
 };
 static double gemv_bytes(const GemvArgs &a) {
@@ -519,6 +530,7 @@ static int talker_layers(qtts_dev *dv) {
         t.kc = dv->kc + (size_t)l * NBA * dv->S * KVD; t.vc = dv->vc + (size_t)l * NBA * dv->S * KVD; t.S = dv->S;
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
+        t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
         { ProfScope ps(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
         CKI(pgemv(dv, gv(ly.wo, d.H, AD, dv->att, AD, dv->x_tk, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, dv->x_tk, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
@@ -966,7 +978,8 @@ extern "C" int qtts_hip_sample_top_k(int *out, const float *logits, int vocab, i
 
 // One frame run eagerly with an event pair around every kernel launch on the
 // context stream; returns the number of kernels, fills kind/bytes/ms.
-extern "C" int qtts_dev_profile_frame(qtts_dev_t *dv, int step, int max, int *kind, double *bytes, float *ms) {
+extern "C" int qtts_dev_profile_frame(qtts_dev_t *dv, int step, int max, int *kind, double *bytes, float *ms,
+                                      char *names) {
     if (!dv || dv->nb < 1) return -1;
     hipSetDevice(dv->device);
     CK(hipStreamSynchronize(dv->st));
@@ -979,7 +992,10 @@ extern "C" int qtts_dev_profile_frame(qtts_dev_t *dv, int step, int max, int *ki
     for (auto &p : dv->prof) {
         float t = 0.f;
         hipEventElapsedTime(&t, p.a, p.b);
-        if (n < max) { kind[n] = p.kind; bytes[n] = p.bytes; ms[n] = t; }
+        if (n < max) {
+            kind[n] = p.kind; bytes[n] = p.bytes; ms[n] = t;
+            if (names) snprintf(names + (size_t)n * 64, 64, "%s", p.name ? p.name : "");
+        }
         ++n;
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
