@@ -4,19 +4,22 @@
 # Usage (via gpurun): bash tools/gpu_round.sh <tag>
 set -eo pipefail
 TAG=${1:-r01}
+MODE=${2:-all}   # all | prof (skip tests and the plain bench run)
 R=$GRAFT_REPO_ROOT
 [ -z "$R" ] && R=$(pwd)
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+if [ "$MODE" = all ]; then
 rc=0
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/gpu_tests.log 2>&1 || rc=$?
 # 1 = some test failed (keep measuring); anything else (timeout, abort, crash) ends the call
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc"; exit $rc; fi
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch.log 2>&1
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_write.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch.log 2>&1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_write.log 2>&1
 python3 $R/tools/prof_summary.py $O
 echo done
