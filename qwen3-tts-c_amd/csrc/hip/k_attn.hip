@@ -224,6 +224,27 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
     const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
 
+    // ---- issue every cache load of this split first: K rows for the scores,
+    // V rows for P.V (the current token's come from LDS later) ----
+    const int kl = tid / LPK, ksub = tid - kl * LPK;
+    const int tk = t0 + kl;
+    const bool kld = tk < t1 && tk != p;
+    float4 kreg[DPL / 4];
+    {
+        const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(kld ? tk : 0) * KVD + ksub * DPL);
+#pragma unroll
+        for (int j = 0; j < DPL / 4; ++j) kreg[j] = kld ? kp[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int d4 = tid % D4, kg = tid / D4;
+    constexpr int NV = (CH + KG - 1) / KG;
+    float4 vreg[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int t = t0 + kg + j * KG;
+        const bool ok = kg + j * KG < CH && t < t1 && t != p;
+        vreg[j] = ok ? reinterpret_cast<const float4 *>(Vc + (size_t)t * KVD)[d4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
     // ---- prologue: q heads (waves 0..GPH-1), k head (wave GPH), v ----
     for (int hh = w; hh <= GPH; hh += 4) {
         const float *src = hh < GPH ? row + (kvh * GPH + hh) * HD : row + a.NH * HD + kvh * HD;
@@ -263,16 +284,16 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     // ---- scores ----
     const float scale = div_rn(1.0f, sqrt_rn((float)HD));
     {
-        const int kl = tid / LPK, sub = tid - kl * LPK;
-        const int t = t0 + kl;
+        const int sub = ksub;
+        const int t = tk;
         float d[GPH];
 #pragma unroll
         for (int g = 0; g < GPH; ++g) d[g] = 0.f;
         if (t < t1) {
-            const float *kp = (t == p) ? qk + GPH * HD + sub * DPL : Kc + (size_t)t * KVD + sub * DPL;
             float4 kv[DPL / 4];
 #pragma unroll
-            for (int j = 0; j < DPL / 4; ++j) kv[j] = reinterpret_cast<const float4 *>(kp)[j];
+            for (int j = 0; j < DPL / 4; ++j)
+                kv[j] = (t == p) ? reinterpret_cast<const float4 *>(qk + GPH * HD + sub * DPL)[j] : kreg[j];
 #pragma unroll
             for (int g = 0; g < GPH; ++g) {
                 const float4 *q4 = reinterpret_cast<const float4 *>(qk + g * HD + sub * DPL);
@@ -310,16 +331,15 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     __syncthreads();
     // ---- P.V ----
     {
-        const int d4 = tid % D4, kg = tid / D4;
         float4 acc[GPH];
 #pragma unroll
         for (int g = 0; g < GPH; ++g) acc[g] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-        for (int k = kg; k < CH; k += KG) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int k = kg + j * KG;
             const int t = t0 + k;
-            if (t < t1) {
-                const float4 v4 = (t == p) ? reinterpret_cast<const float4 *>(vv)[d4]
-                                           : reinterpret_cast<const float4 *>(Vc + (size_t)t * KVD)[d4];
+            if (k < CH && t < t1) {
+                const float4 v4 = (t == p) ? reinterpret_cast<const float4 *>(vv)[d4] : vreg[j];
 #pragma unroll
                 for (int g = 0; g < GPH; ++g) {
                     const float pw = sc[g][k];
