@@ -22,10 +22,45 @@
 // combine through LDS.  KSPLIT is chosen on the host so the grid fills the 256
 // CUs.  Weight loads for the first block group are issued before the prologue
 // so HBM latency overlaps the norm.  Accumulation is fp32 (exact bf16->f32).
+#include "qtts_attn_dev.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 
 namespace {
+
+// Optional tail work of the batch-1 GEMV (TAIL = 1: decode attention of the
+// kv head whose q/k/v rows this grid just produced).
+template <int TAIL> struct TailA { int unused; };
+template <> struct TailA<1> { AttnArgs at; };
+
+// The last workgroup to finish the q/k/v rows of a kv head runs that head's
+// attention (acq_rel agent-scope ticket per kv head, MI355X_MICROARCH.md
+// "Correctness boundaries"; the ticket is reset by its user).
+__device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int RPW, float *smem) {
+    __shared__ int tail_last;
+    const int HD = t.HD, NH = t.NH, KV = t.KV, gph = NH / KV;
+    int kvg;
+    if (row0 < NH * HD) kvg = (row0 / HD) / gph;
+    else if (row0 < (NH + KV) * HD) kvg = (row0 - NH * HD) / HD;
+    else kvg = (row0 - (NH + KV) * HD) / HD;
+    const int need = (gph + 2) * HD / RPW;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(t.cnt + kvg, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        tail_last = (old == need - 1);
+    }
+    __syncthreads();
+    if (!tail_last) return;
+    __threadfence();
+    switch (HD) {
+        case 128: attn_full_wg<128, 2>(t, kvg, 0, smem); break;
+        case 64: attn_full_wg<64, 2>(t, kvg, 0, smem); break;
+        case 32: attn_full_wg<32, 2>(t, kvg, 0, smem); break;
+        default: attn_full_wg<16, 2>(t, kvg, 0, smem); break;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(t.cnt + kvg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 constexpr int U = 8;  // blocks per load group (16 B each per lane)
 
@@ -192,8 +227,8 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 // already in flight.  One barrier in the epilogue: each output thread sums
 // the KSPLIT partials it needs (for SwiGLU also its up row's) straight from
 // LDS.
-template <int U1, int XV, bool NT>
-__global__ __launch_bounds__(256) void k_gemv1(GemvArgs a) {
+template <int U1, int XV, bool NT, int TAIL>
+__global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
     const int ksn = a.ksplit, RPW = 32 / ksn;
@@ -324,6 +359,7 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a) {
             }
         }
     }
+    if constexpr (TAIL == 1) gemv_attn_tail(ta.at, row0, RPW, smem);
 }
 
 }  // namespace
@@ -356,13 +392,14 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         const int nblk = a.C / 64 / a.ksplit;
         const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
         const size_t smem = (size_t)(a.C + 40) * sizeof(float);
+        const TailA<0> t0{0};
 #define QTTS_G1(U, X)                                                                                 \
         if (a.nt) {                                                                                   \
-            hipLaunchKernelGGL((k_gemv1<U, X, true>), dim3(grid), dim3(256), smem, st, a);            \
-            qtts_last_kernel = "k_gemv1<" #U ", " #X ", true>";                                       \
+            hipLaunchKernelGGL((k_gemv1<U, X, true, 0>), dim3(grid), dim3(256), smem, st, a, t0);     \
+            qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 0>";                                    \
         } else {                                                                                      \
-            hipLaunchKernelGGL((k_gemv1<U, X, false>), dim3(grid), dim3(256), smem, st, a);           \
-            qtts_last_kernel = "k_gemv1<" #U ", " #X ", false>";                                      \
+            hipLaunchKernelGGL((k_gemv1<U, X, false, 0>), dim3(grid), dim3(256), smem, st, a, t0);    \
+            qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 0>";                                   \
         }
         if (nblk >= 8) {
             switch (xv) { case 1: QTTS_G1(8, 1) break; case 2: QTTS_G1(8, 2) break;
@@ -399,5 +436,46 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         QTTS_GEMV_CASE(16)
     }
 #undef QTTS_GEMV_CASE
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// QKV GEMV with the decode attention fused as its tail (batch 1).  Returns 1
+// when the configuration is not covered (the caller launches the two
+// kernels), 0 on success, -1 on a launch error.
+int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st) {
+    const int HD = t.HD;
+    const bool hd_ok = HD == 128 || HD == 64 || HD == 32 || HD == 16;
+    if (!(a.nb == 1 && t.nrows == 1 && a.C <= 2048 && a.ldx_ok1() && hd_ok && t.KV > 0 && t.NH == 2 * t.KV &&
+          t.mode == 0 && t.win == 0 && t.cnt && a.epi == EPI_STORE && a.R == (t.NH + 2 * t.KV) * HD))
+        return 1;
+    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
+    while (32 / a.ksplit > HD && a.ksplit < a.C / 64) a.ksplit *= 2;   // one kv head per workgroup
+    if (32 / a.ksplit > HD || (a.C / 64) % a.ksplit) return 1;
+    const int rpw = 32 / a.ksplit;
+    const int grid = a.R / rpw;
+    const int nblk = a.C / 64 / a.ksplit;
+    int pool = 0;
+    switch (HD) {
+        case 128: pool = AttnWG<128, 2>::POOL; break;
+        case 64: pool = AttnWG<64, 2>::POOL; break;
+        case 32: pool = AttnWG<32, 2>::POOL; break;
+        default: pool = AttnWG<16, 2>::POOL; break;
+    }
+    const size_t smem = (size_t)(a.C + 40 > pool ? a.C + 40 : pool) * sizeof(float);
+    const TailA<1> ta{t};
+#define QTTS_GT(U, X)                                                                                 \
+    if (a.nt) {                                                                                       \
+        hipLaunchKernelGGL((k_gemv1<U, X, true, 1>), dim3(grid), dim3(256), smem, st, a, ta);         \
+        qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 1>";                                        \
+    } else {                                                                                          \
+        hipLaunchKernelGGL((k_gemv1<U, X, false, 1>), dim3(grid), dim3(256), smem, st, a, ta);        \
+        qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 1>";                                       \
+    }
+    if (nblk >= 8) {
+        if (a.C <= 1024) { QTTS_GT(8, 1) } else { QTTS_GT(8, 2) }
+    } else {
+        if (a.C <= 1024) { QTTS_GT(4, 1) } else { QTTS_GT(4, 2) }
+    }
+#undef QTTS_GT
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -63,6 +63,7 @@ struct AttnArgs {
     int nsplit = 0;
 };
 int qtts_attn_keys_per_split(int HD);
+int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st);
 
 // Name of the kernel instantiation the last launcher on this thread chose
 // (diagnostics: per-kernel profile rows match rocprofv3's kernel names).

@@ -113,6 +113,7 @@ struct qtts_dev {
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
     bool profiling = false;
+    bool fuse_attn = true;   // QTTS_HIP_NO_FUSE=1: separate attention kernels (A/B diagnostics)
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
     int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
@@ -306,6 +307,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     }
     dv->tl.resize(dims->L);
     dv->sl.resize(dims->Ls);
+    const char *nf = getenv("QTTS_HIP_NO_FUSE");
+    dv->fuse_attn = !(nf && atoi(nf));
     codec_init(&dv->codec, dims, dv->st);
     return dv;
 }
@@ -440,8 +443,9 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         const int gph = d.NH / d.KV;
         dv->att_nsplit = (dv->S + qtts_attn_keys_per_split(d.HD) - 1) / qtts_attn_keys_per_split(d.HD);
         A(att_part, float, B * d.KV * dv->att_nsplit * (gph * d.HD + 2 * gph));
-        A(att_cnt, int, B * d.KV);
-        CK(hipMemsetAsync(dv->att_cnt, 0, B * d.KV * sizeof(int), dv->st));
+        const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
+        A(att_cnt, int, B * kvmax);
+        CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
     }
 #undef A
     dv->p_len_h.assign(nb, 0);
@@ -496,6 +500,13 @@ struct ProfScope {  // brackets one launch with events when profiling is on
         dv->prof.push_back(p);
         idx = dv->prof.size() - 1;
     }
+    void cancel() {
+        if (idx == (size_t)-1) return;
+        hipEventDestroy(dv->prof[idx].a);
+        hipEventDestroy(dv->prof[idx].b);
+        dv->prof.pop_back();
+        idx = (size_t)-1;
+    }
     ~ProfScope() {
         if (idx == (size_t)-1) return;
         hipEventRecord(dv->prof[idx].b, dv->st);
@@ -508,6 +519,22 @@ static double gemv_bytes(const GemvArgs &a) {
 static int pgemv(qtts_dev *dv, const GemvArgs &a, int kind) {
     ProfScope ps(dv, kind, gemv_bytes(a));
     return qtts_gemv(a, dv->st);
+}
+// QKV projection + decode attention: one fused kernel at batch 1 (the
+// attention runs as the GEMV's tail, k_gemv.hip), else two launches.
+static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
+    if (dv->nrun == 1 && dv->fuse_attn) {
+        int rc;
+        {
+            ProfScope ps(dv, kind, gemv_bytes(a));
+            rc = qtts_gemv_qkv_attn(a, t, dv->st);
+            if (rc == 1) ps.cancel();
+        }
+        if (rc != 1) return rc;
+    }
+    CKI(pgemv(dv, a, kind));
+    ProfScope ps(dv, PK_ATTN, 0);
+    return qtts_attention(t, dv->st);
 }
 static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float *y, int ldy, int nb, int epi) {
     GemvArgs a;
@@ -523,7 +550,6 @@ static int talker_layers(qtts_dev *dv) {
         Layer &ly = dv->tl[l];
         GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->x_tk, d.H, dv->qkv, QKV, nb, EPI_STORE);
         a.norm_w = ly.in; a.eps = d.eps;
-        CKI(pgemv(dv, a, PK_GEMV_TALKER));
         AttnArgs t;
         t.mode = 0; t.qkv = dv->qkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
         t.rope_cos = dv->rope_cos; t.rope_sin = dv->rope_sin;
@@ -531,7 +557,7 @@ static int talker_layers(qtts_dev *dv) {
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
         t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
-        { ProfScope ps(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
+        CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
         CKI(pgemv(dv, gv(ly.wo, d.H, AD, dv->att, AD, dv->x_tk, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, dv->x_tk, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
@@ -596,14 +622,14 @@ static int subtalker(qtts_dev *dv) {
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, dv->x_st, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             if (l == 0 && !proj) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
-            CKI(pgemv(dv, a, PK_GEMV_SUB));
             AttnArgs t;
             t.mode = 0; t.qkv = dv->qkv_s; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
             t.rope_cos = dv->rope_cos_s; t.rope_sin = dv->rope_sin_s;
             t.kc = dv->kcs + (size_t)l * NBA * d.G * KVD; t.vc = dv->vcs + (size_t)l * NBA * d.G * KVD; t.S = d.G;
             t.pos = nullptr; t.pos_const = g; t.NH = d.NHs; t.KV = d.KVs; t.HD = d.HDs; t.out = dv->att_s;
             t.ld_out = AD; t.nrows = nb; t.skip = dv->stopped;
-            { ProfScope ps(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
+            t.cnt = dv->att_cnt;
+            CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
             a = gv(ly.wo, d.Hs, AD, dv->att_s, AD, dv->x_st, d.Hs, nb, EPI_RESID);
             a.nt = 0;
             CKI(pgemv(dv, a, PK_GEMV_SUB));
