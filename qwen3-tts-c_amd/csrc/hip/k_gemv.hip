@@ -25,6 +25,7 @@
 #include "qtts_attn_dev.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
+#include "qtts_sample_dev.h"
 
 namespace {
 
@@ -32,6 +33,24 @@ namespace {
 // kv head whose q/k/v rows this grid just produced).
 template <int TAIL> struct TailA { int unused; };
 template <> struct TailA<1> { AttnArgs at; };
+template <> struct TailA<2> { SampArgs sa; int *cnt; };
+
+// The last workgroup of the logit-head GEMV draws the token (qtts_sample_dev.h),
+// so sampling costs no kernel of its own.
+__device__ __forceinline__ void gemv_sample_tail(const SampArgs &sa, int *cnt, float *smem) {
+    __shared__ int tail_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        tail_last = (old == (int)gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!tail_last) return;
+    __threadfence();
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qtts_samp::sample_row<true>(sa, 0, reinterpret_cast<unsigned char *>(smem));
+}
 
 // The last workgroup to finish the q/k/v rows of a kv head runs that head's
 // attention (acq_rel agent-scope ticket per kv head, MI355X_MICROARCH.md
@@ -360,6 +379,7 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
         }
     }
     if constexpr (TAIL == 1) gemv_attn_tail(ta.at, row0, RPW, smem);
+    if constexpr (TAIL == 2) gemv_sample_tail(ta.sa, ta.cnt, smem);
 }
 
 }  // namespace
@@ -477,5 +497,40 @@ int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st) {
         if (a.C <= 1024) { QTTS_GT(4, 1) } else { QTTS_GT(4, 2) }
     }
 #undef QTTS_GT
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Logit-head GEMV with the sampler fused as its tail (batch 1).  Returns 1
+// when not covered (the caller launches the sampler), 0 ok, -1 error.
+int qtts_gemv_sample(GemvArgs a, const SampArgs &sa, int *cnt, hipStream_t st) {
+    if (!(a.nb == 1 && sa.nb == 1 && a.C <= 8192 && a.ldx_ok1() && cnt && a.epi == EPI_STORE && sa.n == a.R &&
+          qtts_samp::fast_path(sa) && sa.logits == a.y))
+        return 1;
+    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
+    const int rpw = 32 / a.ksplit;
+    const int grid = (a.R + rpw - 1) / rpw;
+    const int nblk = a.C / 64 / a.ksplit;
+    const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
+    size_t smem = (size_t)(a.C + 40) * sizeof(float);
+    if (smem < sizeof(qtts_samp::FastSmem)) smem = sizeof(qtts_samp::FastSmem);
+    TailA<2> ta;
+    ta.sa = sa;
+    ta.cnt = cnt;
+#define QTTS_GS(U, X)                                                                                 \
+    if (a.nt) {                                                                                       \
+        hipLaunchKernelGGL((k_gemv1<U, X, true, 2>), dim3(grid), dim3(256), smem, st, a, ta);         \
+        qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 2>";                                        \
+    } else {                                                                                          \
+        hipLaunchKernelGGL((k_gemv1<U, X, false, 2>), dim3(grid), dim3(256), smem, st, a, ta);        \
+        qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 2>";                                       \
+    }
+    if (nblk >= 8) {
+        switch (xv) { case 1: QTTS_GS(8, 1) break; case 2: QTTS_GS(8, 2) break;
+                      case 4: QTTS_GS(8, 4) break; default: QTTS_GS(8, 8) break; }
+    } else {
+        switch (xv) { case 1: QTTS_GS(4, 1) break; case 2: QTTS_GS(4, 2) break;
+                      case 4: QTTS_GS(4, 4) break; default: QTTS_GS(4, 8) break; }
+    }
+#undef QTTS_GS
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1,448 +1,22 @@
-// k_sample.hip - on-device sampling for the talker (group 0) and sub-talker
-// (groups 1..15), one workgroup per batch row.  Keeping this on the device is
-// what lets a whole frame run without a host round trip.
-//
-// Reproduces c/qwen_tts_kernels.c:384-558 and the loop around it
-// (c/qwen_tts.c:1302-1340) EXACTLY given identical logits:
-//   * suppress ids [V-1024, V) except EOS to -1e9 (Q.c:1272-1305), talker only
-//   * repetition penalty once per OCCURRENCE (K.c:395-405, Q.c:1308): an id
-//     seen c times is divided / multiplied c times
-//   * fast path (top_p >= 1, 0 < top_k < n): v = logit / T, the top-k in
-//     (value desc, index asc) order -- the order the reference's strict '>'
-//     insertion list produces -- p_j = expf(v_j - v_0) summed sequentially,
-//     r = u * sum, first j with cumsum >= r
-//   * full path otherwise: softmax, keep p >= k-th largest, nucleus over the
-//     stable descending order, renormalise, inverse CDF in index order
-//   * xorshift32 over the bits of a float state (K.c:384-393); the sub-talker
-//     state is reset to (float)seed at every frame (T.c:718)
-//   * fixed-length mode: an EOS draw is masked and redrawn (Q.c:1315-1321)
-// Sequential sums run on one lane in the reference's order; expf is the
-// glibc-exact replica (qtts_common.h); divisions are correctly rounded.
-//
-// Fast path: each thread keeps its ids in registers; top-k is an MSB radix
-// select over order-preserving u32 keys (per-wave 256-bin LDS histograms, one
-// barrier per pass, early exit), then an exact rank of the k selected (value
-// desc, index asc).  Full path: bitonic sort in LDS.
-#include <float.h>
-#include "qtts_common.h"
-#include "qtts_kernels.h"
+// k_sample.hip - the sampler as a kernel of its own: one workgroup per batch
+// row (the device code and its derivation are in qtts_sample_dev.h).
+#include "qtts_sample_dev.h"
 
 namespace {
 
-constexpr int NMAX = 4096;
-
-struct SampSmem {
-    float lg[NMAX];        // (penalised) logits
-    float v[NMAX];         // logits / T  (or probabilities in the full path)
-    unsigned long long srt[NMAX];  // sort buffer (key desc, index asc)
-    int misc[16];
-    float fmisc[8];
-};
-
-__device__ __forceinline__ uint32_t okey(float v) {
-    if (v == 0.0f) v = 0.0f;  // -0 == +0 for the comparisons
-    const uint32_t u = __float_as_uint(v);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
-__device__ __forceinline__ float rand_uniform(uint32_t &s) {
-#pragma clang fp contract(off)
-    s ^= s << 13;
-    s ^= s >> 17;
-    s ^= s << 5;
-    return div_rn((float)(s & 0x7FFFFFFFu), (float)0x7FFFFFFF);
-}
-
-// bitonic sort of sm.srt[0..N2) descending
-__device__ void bitonic_desc(SampSmem &sm, int N2) {
-    const int tid = threadIdx.x;
-    for (int size = 2; size <= N2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < N2 / 2; i += 256) {
-                const int lo = 2 * i - (i & (stride - 1));
-                const int hi = lo + stride;
-                const bool desc = ((lo & size) == 0);
-                const unsigned long long x = sm.srt[lo], y = sm.srt[hi];
-                if ((x < y) == desc) { sm.srt[lo] = y; sm.srt[hi] = x; }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// Full path (K.c:486-557).
-__device__ __forceinline__ int sample_full(SampSmem &sm, int n, int k, float top_p, float temp, uint32_t &rng) {
-#pragma clang fp contract(off)
-    const int tid = threadIdx.x;
-    for (int i = tid; i < n; i += 256) sm.v[i] = div_rn(sm.lg[i], temp);
-    __syncthreads();
-    // softmax (K.c:371-378): max, e = expf(x - max), sequential sum, scale
-    if (tid == 0) {
-        float mx = sm.v[0];
-        for (int i = 1; i < n; ++i) if (sm.v[i] > mx) mx = sm.v[i];
-        sm.fmisc[0] = mx;
-    }
-    __syncthreads();
-    const float mx = sm.fmisc[0];
-    for (int i = tid; i < n; i += 256) sm.v[i] = expf_glibc(sm.v[i] - mx);
-    __syncthreads();
-    if (tid == 0) {
-        float s = 0.0f;
-        for (int i = 0; i < n; ++i) s += sm.v[i];
-        sm.fmisc[1] = div_rn(1.0f, s);
-    }
-    __syncthreads();
-    const float inv = sm.fmisc[1];
-    for (int i = tid; i < n; i += 256) sm.v[i] *= inv;
-    __syncthreads();
-    int N2 = 1;
-    while (N2 < n) N2 <<= 1;
-    const bool need_sort = (k > 0 && k < n) || top_p < 1.0f;
-    if (need_sort) {
-        // composite (key desc, index asc): key<<32 | ~index
-        for (int i = tid; i < N2; i += 256)
-            sm.srt[i] = i < n ? (((unsigned long long)okey(sm.v[i]) << 32) | (0xFFFFFFFFu - (uint32_t)i)) : 0ull;
-        __syncthreads();
-        bitonic_desc(sm, N2);
-    }
-    if (k > 0 && k < n) {
-        const uint32_t thr_key = (uint32_t)(sm.srt[k - 1] >> 32);
-        for (int i = tid; i < n; i += 256)
-            if (okey(sm.v[i]) < thr_key) sm.v[i] = 0.0f;   // p < k-th largest -> 0
-        __syncthreads();
-        if (top_p < 1.0f) {  // re-sort with the zeroed values (ties stay in index order)
-            for (int i = tid; i < N2; i += 256)
-                sm.srt[i] = i < n ? (((unsigned long long)okey(sm.v[i]) << 32) | (0xFFFFFFFFu - (uint32_t)i)) : 0ull;
-            __syncthreads();
-            bitonic_desc(sm, N2);
-        }
-    }
-    if (top_p < 1.0f) {
-        if (tid == 0) {
-            float c = 0.0f;
-            int cut = n;
-            for (int i = 0; i < n; ++i) {
-                c += sm.v[0xFFFFFFFFu - (uint32_t)(sm.srt[i] & 0xFFFFFFFFull)];
-                if (c >= top_p) { cut = i + 1; break; }
-            }
-            sm.misc[7] = cut;
-        }
-        __syncthreads();
-        const int cut = sm.misc[7];
-        for (int i = cut + tid; i < n; i += 256) sm.v[0xFFFFFFFFu - (uint32_t)(sm.srt[i] & 0xFFFFFFFFull)] = 0.0f;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        float s = 0.0f;
-        for (int i = 0; i < n; ++i) s += sm.v[i];
-        sm.fmisc[2] = s;
-    }
-    __syncthreads();
-    const float s = sm.fmisc[2];
-    if (s > 0.0f) {
-        const float iv = div_rn(1.0f, s);
-        for (int i = tid; i < n; i += 256) sm.v[i] *= iv;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const float r = rand_uniform(rng);
-        float c = 0.0f;
-        int out = 0;
-        for (int i = 0; i < n; ++i) {
-            c += sm.v[i];
-            if (c >= r) { out = i; break; }
-        }
-        sm.misc[8] = out;
-    }
-    __syncthreads();
-    return sm.misc[8];
-}
-
-__device__ __forceinline__ int sample_any(SampSmem &sm, int n, int k, float top_p, float temp, uint32_t &rng) {
-    if (temp <= 0.0f) temp = 1e-5f;
-    return sample_full(sm, n, k, top_p, temp, rng);
-}
-
-// ---------------------------------------------------------------------------
-// Fast path on registers (top_p >= 1, 0 < k < n): thread t owns the
-// contiguous ids [t*E, t*E + E), E = ceil(n / 256) <= EMAX.
-constexpr int EMAX = NMAX / 256;
-
-struct FastSmem {
-    int hist[2][4][256];   // per-wave radix histograms, double-buffered by pass
-    int scan[2][4];
-    float sel_v[NMAX];
-    int sel_i[NMAX];
-    float top_v[NMAX];
-    int top_i[NMAX];
-    int misc[4];
-};
-
-// k-th largest eligible key (value desc): 8-bit MSB radix select over
-// per-wave LDS histograms, one barrier per pass, early exit once the bin that
-// holds the k-th key fits entirely.  Returns T (threshold key prefix, low
-// bits 0 after an early exit), take_eq = how many keys == T to take in index
-// order when the select ran to the last digit; ne = number of eligible keys.
-__device__ __forceinline__ void radix_select_regs(FastSmem &fs, const uint32_t (&kk)[EMAX], int E, int k, uint32_t &T,
-                                  uint32_t &Tmask, int &take_eq, int &ne) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { fs.hist[0][w][lane + 64 * i] = 0; fs.hist[1][w][lane + 64 * i] = 0; }
-    uint32_t prefix = 0, mask = 0;
-    int rem = k;
-    ne = -1;
-    int par = 0;
-    for (int shift = 24; shift >= 0; shift -= 8, par ^= 1) {
-        int *h = fs.hist[par][w];
-#pragma unroll
-        for (int j = 0; j < EMAX; ++j)
-            if (j < E && kk[j] != 0u && (kk[j] & mask) == prefix) atomicAdd(&h[(kk[j] >> shift) & 255u], 1);
-        __syncthreads();
-        // every wave scans the merged histogram from the top (same result in all waves)
-        int c[4], tot = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int bin = 255 - 4 * lane - i;
-            c[i] = fs.hist[par][0][bin] + fs.hist[par][1][bin] + fs.hist[par][2][bin] + fs.hist[par][3][bin];
-            tot += c[i];
-        }
-        int inc = tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-        }
-        if (ne < 0) {
-            ne = __shfl(inc, 63, 64);
-            if (k > ne) k = ne;
-            rem = k;
-        }
-        const int exc = inc - tot;
-        int bin = -1, nrem = 0, cbin = 0;
-        if (exc < rem && inc >= rem) {
-            int cum = exc;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (bin < 0 && cum + c[i] >= rem) { bin = 255 - 4 * lane - i; nrem = rem - cum; cbin = c[i]; }
-                cum += c[i];
-            }
-        }
-        const unsigned long long hit = __ballot(bin >= 0);
-        const int src = hit ? __ffsll((long long)hit) - 1 : 0;
-        bin = __shfl(bin, src, 64);
-        nrem = __shfl(nrem, src, 64);
-        cbin = __shfl(cbin, src, 64);
-        // clear this wave's other buffer for the next pass (its readers finished before this barrier)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fs.hist[par ^ 1][w][lane + 64 * i] = 0;
-        if (k == 0) { T = 0xFFFFFFFFu; Tmask = 0xFFFFFFFFu; take_eq = 0; return; }
-        prefix |= (uint32_t)bin << shift;
-        mask |= 255u << shift;
-        rem = nrem;
-        if (cbin == nrem || shift == 0) {   // the whole bin is taken, or the key is exact
-            T = prefix; Tmask = mask; take_eq = nrem;
-            return;
-        }
-    }
-}
-
-__device__ __forceinline__ void block_scan2(FastSmem &fs, int x, int y, int &ex, int &ey) {
-    // exclusive scans of two small per-thread counts packed in one int (16 | 16 bits)
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int v = x | (y << 16);
-    int inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int z = __shfl_up(inc, o, 64);
-        if (l >= o) inc += z;
-    }
-    if (l == 63) fs.scan[0][w] = inc;
-    __syncthreads();
-    int base = 0;
-    for (int i = 0; i < w; ++i) base += fs.scan[0][i];
-    const int e = base + inc - v;
-    ex = e & 0xFFFF;
-    ey = e >> 16;
-}
-
-// Returns the sampled id (all threads).  v[]: logits / temperature.
-__device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[EMAX], int E, int n, int k, uint32_t &rng) {
-#pragma clang fp contract(off)
-    const int tid = threadIdx.x;
-    uint32_t kk[EMAX];
-#pragma unroll
-    for (int j = 0; j < EMAX; ++j) kk[j] = (j < E && tid * E + j < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
-    uint32_t T, Tm;
-    int take_eq, ne;
-    radix_select_regs(fs, kk, E, k, T, Tm, take_eq, ne);
-    const int ke = k < ne ? k : ne;
-    if (ke == 0) return 0;                       // nothing eligible: the reference returns 0
-    // taken: (key & Tm) > T, or == T for the first take_eq of those in index order
-    int ngt = 0, neq = 0;
-#pragma unroll
-    for (int j = 0; j < EMAX; ++j) {
-        if (j < E && kk[j] != 0u) {
-            const uint32_t m = kk[j] & Tm;
-            ngt += m > T;
-            neq += m == T;
-        }
-    }
-    int gt0, eq0;
-    block_scan2(fs, ngt, neq, gt0, eq0);
-    int pos = gt0 + min(eq0, take_eq);
-    int eqc = eq0;
-#pragma unroll
-    for (int j = 0; j < EMAX; ++j) {
-        if (j < E && kk[j] != 0u) {
-            const uint32_t m = kk[j] & Tm;
-            bool take = m > T;
-            if (m == T) { take = eqc < take_eq; ++eqc; }
-            if (take) { fs.sel_v[pos] = v[j]; fs.sel_i[pos] = tid * E + j; ++pos; }
-        }
-    }
-    __syncthreads();
-    // exact rank among the ke selected (value desc, index asc); sel_* is in index order
-    for (int s2 = tid; s2 < ke; s2 += 256) {
-        const float vs = fs.sel_v[s2];
-        const uint32_t ks = okey(vs);
-        int rk = 0;
-        for (int t = 0; t < ke; ++t) {
-            const uint32_t kt = okey(fs.sel_v[t]);
-            rk += (kt > ks) || (kt == ks && t < s2);
-        }
-        fs.top_v[rk] = vs;
-        fs.top_i[rk] = fs.sel_i[s2];
-    }
-    __syncthreads();
-    const float mx = fs.top_v[0];
-    for (int j = tid; j < ke; j += 256) fs.sel_v[j] = expf_glibc(fs.top_v[j] - mx);
-    __syncthreads();
-    if (tid == 0) {
-        float sum = 0.0f;
-        for (int j = 0; j < ke; ++j) sum += fs.sel_v[j];
-        int out = 0;
-        if (sum > 0.0f) {
-            const float r = rand_uniform(rng) * sum;
-            float c = 0.0f;
-            for (int j = 0; j < ke; ++j) {
-                c += fs.sel_v[j];
-                if (c >= r) { out = fs.top_i[j]; break; }
-            }
-        } else {
-            out = fs.top_i[0];
-        }
-        fs.misc[0] = out;
-    }
-    __syncthreads();
-    const int out = fs.misc[0];
-    __syncthreads();   // fs is reused by a second draw (fixed-mode EOS re-sample)
-    return out;
-}
-
-union KSmem {
-    SampSmem full;
-    FastSmem fast;
-};
-
 __global__ __launch_bounds__(256) void k_sample(SampArgs a) {
-#pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    KSmem &U = *reinterpret_cast<KSmem *>(smraw);
-    const int b = blockIdx.x, tid = threadIdx.x, n = a.n;
-    // every global read of this kernel is issued up front (one round trip)
-    int stopped = 0, ng = 0;
-    uint32_t rng = 0;
-    if (tid == 0) {
-        stopped = a.stopped ? a.stopped[b] : 0;
-        rng = a.mode == 1 ? a.rng[b] : a.st_rng[b];
-        if (a.mode == 1) ng = a.n_gen[b];
-    }
-    const int E = (n + 255) / 256;
-    const float *lg = a.logits + (size_t)b * a.ld;
-    const int i0 = tid * E;
-    float x[EMAX];
-    int cnt[EMAX];
-    const bool pen = a.mode == 1 && a.rep != 1.0f && a.counts;
-#pragma unroll
-    for (int j = 0; j < EMAX; ++j) {
-        const int i = i0 + j;
-        const bool ok = j < E && i < n;
-        x[j] = ok ? lg[i] : -INFINITY;
-        cnt[j] = (ok && pen) ? a.counts[(size_t)b * n + i] : 0;
-    }
-    if (tid == 0) { U.fast.misc[1] = stopped; U.fast.misc[2] = ng; }
-    __syncthreads();
-    if (U.fast.misc[1]) return;
-    ng = U.fast.misc[2];
-    __syncthreads();
-    if (a.mode == 1) {
-#pragma unroll
-        for (int j = 0; j < EMAX; ++j) {
-            const int i = i0 + j;
-            float v = x[j];
-            if (i >= a.suppress_lo && i != a.eos) v = -1e9f;
-            for (int c = 0; c < cnt[j]; ++c) v = v > 0 ? div_rn(v, a.rep) : v * a.rep;
-            x[j] = (j < E && i < n) ? v : -INFINITY;
-        }
-    }
-    float temp = a.temp;
-    if (temp <= 0.0f) temp = 1e-5f;
-    const bool fast = a.top_p >= 1.0f && a.top_k > 0 && a.top_k < n && E <= EMAX;
-    int tok;
-    if (fast) {
-        float v[EMAX];
-#pragma unroll
-        for (int j = 0; j < EMAX; ++j) v[j] = div_rn(x[j], temp);
-        tok = sample_fast_regs(U.fast, v, E, n, a.top_k, rng);
-        if (a.mode == 1 && a.fixed > 0 && tok == a.eos && ng < a.fixed) {   // Q.c:1315-1321
-#pragma unroll
-            for (int j = 0; j < EMAX; ++j)
-                if (i0 + j == a.eos) v[j] = div_rn(-1e9f, temp);
-            tok = sample_fast_regs(U.fast, v, E, n, a.top_k, rng);
-        }
-    } else {
-        SampSmem &sm = U.full;
-#pragma unroll
-        for (int j = 0; j < EMAX; ++j)
-            if (j < E && i0 + j < n) sm.lg[i0 + j] = x[j];
-        __syncthreads();
-        tok = sample_any(sm, n, a.top_k, a.top_p, a.temp, rng);
-        if (a.mode == 1 && a.fixed > 0 && tok == a.eos && ng < a.fixed) {
-            if (tid == 0) sm.lg[a.eos] = -1e9f;
-            __syncthreads();
-            tok = sample_any(sm, n, a.top_k, a.top_p, a.temp, rng);
-        }
-    }
-    if (tid == 0) {
-        if (a.mode == 1) {
-            a.rng[b] = rng;
-            if (a.fixed == 0 && tok == a.eos) {
-                a.stopped[b] = 1;
-                if (a.stop_step) a.stop_step[b] = ng;
-            } else {
-                a.cur_row[b] = ng;
-                a.codes[(size_t)b * a.codes_bstride + (size_t)ng * a.G + 0] = tok;
-                if (a.counts) a.counts[(size_t)b * n + tok] += 1;
-                a.n_gen[b] = ng + 1;
-                a.st_rng[b] = a.seed_bits;
-            }
-            if (a.out_tok) a.out_tok[b] = tok;
-        } else {
-            a.st_rng[b] = rng;
-            if (a.codes) a.codes[(size_t)b * a.codes_bstride + (size_t)a.cur_row[b] * a.G + a.g] = tok;
-            if (a.out_tok) a.out_tok[b] = tok;
-        }
-    }
+    qtts_samp::sample_row<false>(a, blockIdx.x, smraw);
 }
 
 }  // namespace
 
 int qtts_sample(const SampArgs &a, hipStream_t st) {
-    if (a.n > NMAX || a.n < 1) {
-        fprintf(stderr, "qtts_sample: vocab %d unsupported (max %d)\n", a.n, NMAX);
+    if (a.n > qtts_samp::NMAX || a.n < 1) {
+        fprintf(stderr, "qtts_sample: vocab %d unsupported (max %d)\n", a.n, qtts_samp::NMAX);
         return -1;
     }
-    hipLaunchKernelGGL(k_sample, dim3(a.nb), dim3(256), sizeof(KSmem), st, a);
+    hipLaunchKernelGGL(k_sample, dim3(a.nb), dim3(256), sizeof(qtts_samp::KSmem), st, a);
     qtts_last_kernel = "k_sample";
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

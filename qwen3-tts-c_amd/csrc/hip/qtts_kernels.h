@@ -92,6 +92,7 @@ struct SampArgs {
     int codes_bstride = 0, G = 16, g = 0;
     int *out_tok = nullptr;        // optional plain output [b]
 };
+int qtts_gemv_sample(GemvArgs a, const SampArgs &sa, int *cnt, hipStream_t st);
 int qtts_sample(const SampArgs &a, hipStream_t st);
 
 struct EmbedSumArgs {

@@ -98,6 +98,7 @@ struct qtts_dev {
     int *stop_step = nullptr, *kv_len = nullptr, *n_trailing = nullptr;
     float *att_part = nullptr;   // split-K decode attention partials (talker)
     int *att_cnt = nullptr, att_nsplit = 0;
+    int *samp_cnt = nullptr;     // ticket of the GEMV + sampler fusion
     uint32_t *rng = nullptr, *st_rng = nullptr;
     float *trailing = nullptr, *prefill = nullptr, *pad_emb = nullptr;
     // prefill / prompt scratch
@@ -445,6 +446,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         A(att_part, float, B * d.KV * dv->att_nsplit * (gph * d.HD + 2 * gph));
         const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
         A(att_cnt, int, B * kvmax);
+        A(samp_cnt, int, 16);
+        CK(hipMemsetAsync(dv->samp_cnt, 0, 16 * sizeof(int), dv->st));
         CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
     }
 #undef A
@@ -567,16 +570,37 @@ static int talker_layers(qtts_dev *dv) {
     return 0;
 }
 
+// Logit head + sampler: one fused kernel at batch 1 when the sampling
+// parameters take the register fast path (the draw runs as the GEMV's tail),
+// else two launches.
+static int head_sample(qtts_dev *dv, const GemvArgs &a, const SampArgs &s, int kind) {
+    if (dv->nrun == 1 && dv->fuse_attn) {
+        int rc;
+        {
+            ProfScope ps(dv, kind, gemv_bytes(a));
+            rc = qtts_gemv_sample(a, s, dv->samp_cnt, dv->st);
+            if (rc == 1) ps.cancel();
+        }
+        if (rc != 1) return rc;
+    }
+    CKI(pgemv(dv, a, kind));
+    ProfScope ps(dv, PK_SAMPLE, 0);
+    return qtts_sample(s, dv->st);
+}
+
 // final norm + codec head; normed hidden -> tk_hid (T.c:526-530, Q.c:1295)
-static int talker_tail(qtts_dev *dv) {
+static GemvArgs talker_head_args(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     GemvArgs a = gv(dv->head, d.V, d.H, dv->x_tk, d.H, dv->logits, d.V, dv->nrun, EPI_STORE);
     a.norm_w = dv->tk_norm; a.eps = d.eps; a.xcopy = dv->tk_hid; a.ldxc = d.H; a.xcopy_normed = 1;
-    return pgemv(dv, a, PK_GEMV_TALKER);
+    return a;
 }
+static int talker_tail(qtts_dev *dv) { return pgemv(dv, talker_head_args(dv), PK_GEMV_TALKER); }
 
-static int talker_sample(qtts_dev *dv) {
+// codec head, then the group-0 draw with suppression / repetition penalty / EOS rules
+static int talker_head_sample(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
+    const GemvArgs a = talker_head_args(dv);
     SampArgs s;
     s.logits = dv->logits; s.ld = d.V; s.n = d.V; s.nb = dv->nrun;
     s.top_k = dv->par.top_k; s.top_p = dv->par.top_p; s.temp = dv->par.temperature;
@@ -585,8 +609,7 @@ static int talker_sample(qtts_dev *dv) {
     s.n_gen = dv->n_gen; s.stopped = dv->stopped; s.cur_row = dv->cur_row; s.stop_step = dv->stop_step;
     s.st_rng = dv->st_rng; s.seed_bits = seed_bits(dv->par.seed);
     s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G;
-    ProfScope ps(dv, PK_SAMPLE, 0);
-    return qtts_sample(s, dv->st);
+    return head_sample(dv, a, s, PK_GEMV_TALKER);
 }
 
 // 16 sub-talker passes (T.c:539-736)
@@ -644,13 +667,12 @@ static int subtalker(qtts_dev *dv) {
         GemvArgs a = gv(dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, dv->x_st, d.Hs, dv->logits_s, d.Vs, nb,
                         EPI_STORE);
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
-        CKI(pgemv(dv, a, PK_GEMV_SUB));
         SampArgs s;
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
         s.mode = 0; s.st_rng = dv->st_rng; s.stopped = dv->stopped; s.cur_row = dv->cur_row;
         s.codes = dv->codes; s.codes_bstride = cstride; s.G = d.G; s.g = g;
-        { ProfScope ps(dv, PK_SAMPLE, 0); CKI(qtts_sample(s, st)); }
+        CKI(head_sample(dv, a, s, PK_GEMV_SUB));
     }
     return 0;
 }
@@ -668,8 +690,7 @@ static int embed_sum(qtts_dev *dv, int advance) {
 
 static int record_frame(qtts_dev *dv, bool with_talker) {
     if (with_talker) CKI(talker_layers(dv));
-    CKI(talker_tail(dv));
-    CKI(talker_sample(dv));
+    CKI(talker_head_sample(dv));
     CKI(subtalker(dv));
     CKI(embed_sum(dv, with_talker ? 1 : 0));
     return 0;
