@@ -24,7 +24,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 16;
+constexpr int BM = 64, BN = 64, BK = 32;
 
 __device__ __forceinline__ float snake1(float x, float a, float ib) {
     const float s = sinf(x * a);
@@ -62,35 +62,92 @@ __device__ __forceinline__ float gelu_tanh(float v) {
     return 0.5f * v * (1.0f + tanhf(0.7978845608028654f * (v + 0.044715f * v * v * v)));
 }
 
+__device__ __forceinline__ void xg_epi(const XGemm &g, int m, int n, float v) {
+    switch (g.emode) {
+        case XE_STORE: g.C[(size_t)m * g.ldc + n] = v; break;
+        case XE_BIAS_N: g.C[(size_t)m * g.ldc + n] = v + g.bias[n]; break;
+        case XE_BIAS_N_GELU: g.C[(size_t)m * g.ldc + n] = gelu_tanh(v + g.bias[n]); break;
+        case XE_SILU_MUL: {
+            const float gt = g.aux[(size_t)m * g.ldaux + n];
+            g.C[(size_t)m * g.ldc + n] = (gt / (1.0f + expf(-gt))) * v;
+            break;
+        }
+        case XE_SCALE_RESID_N: g.C[(size_t)m * g.ldc + n] += v * g.vec[n]; break;
+        case XE_BIAS_T: g.C[(size_t)n * g.ldc + m] = v + g.bias[n]; break;
+        case XE_BIAS_GAMMA_RES_T:
+            g.C[(size_t)n * g.ldc + m] = (v + g.bias[n]) * g.vec[n] + g.res[(size_t)n * g.ldres + m];
+            break;
+        case XE_BIAS_M: {
+            float y = v + (g.bias ? g.bias[m] : 0.f);
+            if (g.stride > 1 || g.phase > 0) g.C[(size_t)m * g.ldc + (size_t)n * g.stride + g.phase] = y;
+            else g.C[(size_t)m * g.ldc + n] = y;
+            break;
+        }
+        case XE_BIAS_M_RES: g.C[(size_t)m * g.ldc + n] = v + g.bias[m] + g.res[(size_t)m * g.ldres + n]; break;
+        case XE_BIAS_M_SNAKE: g.C[(size_t)m * g.ldc + n] = snake1(v + g.bias[m], g.ea[m], g.eb[m]); break;
+    }
+}
+
+// 64x64 output tile per workgroup (2x2 waves of 32x32 on v_mfma_f32_32x32x2f32),
+// K in steps of BK = 32 staged through LDS; the next step's operands are
+// loaded into registers while the MFMAs consume the current one.  With
+// gridDim.z > 1 (split-K for small output tiles) each z covers one K range and
+// writes raw partials to g.part[z][M][N]; k_xg_reduce sums them in z order and
+// applies the epilogue.
 __global__ __launch_bounds__(256) void k_xgemm(XGemm g) {
     __shared__ float As[BM][BK + 1];
     __shared__ float Bs[BN][BK + 1];
+    constexpr int NA = (BM * BK) / 256, NB_ = (BN * BK) / 256;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    const int nz = gridDim.z, z = blockIdx.z;
+    const int ksteps = (g.K + BK - 1) / BK;
+    const int s0 = (int)((long)ksteps * z / nz), s1 = (int)((long)ksteps * (z + 1) / nz);
     floatx16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     const bool a_k_fast = g.amode == XA_ROWS;   // consecutive threads along k
     const bool b_k_fast = g.bmode == XB_WT;
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
+    float ra[NA], rb[NB_];
+    auto load = [&](int k0) {
 #pragma unroll
-        for (int j = 0; j < (BM * BK) / 256; ++j) {
+        for (int j = 0; j < NA; ++j) {
             const int e = tid + 256 * j;
             int mi, ki;
             if (a_k_fast) { mi = e / BK; ki = e % BK; }
             else { ki = e / BM; mi = e % BM; }
-            As[mi][ki] = loadA(g, m0 + mi, k0 + ki);
+            ra[j] = loadA(g, m0 + mi, k0 + ki);
         }
 #pragma unroll
-        for (int j = 0; j < (BN * BK) / 256; ++j) {
+        for (int j = 0; j < NB_; ++j) {
             const int e = tid + 256 * j;
             int ni, ki;
             if (b_k_fast) { ni = e / BK; ki = e % BK; }
             else { ki = e / BN; ni = e % BN; }
-            Bs[ni][ki] = loadB(g, k0 + ki, n0 + ni);
+            rb[j] = loadB(g, k0 + ki, n0 + ni);
+        }
+    };
+    if (s0 < s1) load(s0 * BK);
+    for (int s2 = s0; s2 < s1; ++s2) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+            const int e = tid + 256 * j;
+            int mi, ki;
+            if (a_k_fast) { mi = e / BK; ki = e % BK; }
+            else { ki = e / BM; mi = e % BM; }
+            As[mi][ki] = ra[j];
+        }
+#pragma unroll
+        for (int j = 0; j < NB_; ++j) {
+            const int e = tid + 256 * j;
+            int ni, ki;
+            if (b_k_fast) { ni = e / BK; ki = e % BK; }
+            else { ki = e / BN; ni = e % BN; }
+            Bs[ni][ki] = rb[j];
         }
         __syncthreads();
+        if (s2 + 1 < s1) load((s2 + 1) * BK);
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 2) {
             const float a = As[wm + (lane & 31)][kk + (lane >> 5)];
@@ -104,35 +161,17 @@ __global__ __launch_bounds__(256) void k_xgemm(XGemm g) {
         const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int n = n0 + wn + (lane & 31);
         if (m >= g.M || n >= g.N) continue;
-        const float v = acc[r];
-        switch (g.emode) {
-            case XE_STORE: g.C[(size_t)m * g.ldc + n] = v; break;
-            case XE_BIAS_N: g.C[(size_t)m * g.ldc + n] = v + g.bias[n]; break;
-            case XE_BIAS_N_GELU: g.C[(size_t)m * g.ldc + n] = gelu_tanh(v + g.bias[n]); break;
-            case XE_SILU_MUL: {
-                const float gt = g.aux[(size_t)m * g.ldaux + n];
-                g.C[(size_t)m * g.ldc + n] = (gt / (1.0f + expf(-gt))) * v;
-                break;
-            }
-            case XE_SCALE_RESID_N: g.C[(size_t)m * g.ldc + n] += v * g.vec[n]; break;
-            case XE_BIAS_T: g.C[(size_t)n * g.ldc + m] = v + g.bias[n]; break;
-            case XE_BIAS_GAMMA_RES_T:
-                g.C[(size_t)n * g.ldc + m] = (v + g.bias[n]) * g.vec[n] + g.res[(size_t)n * g.ldres + m];
-                break;
-            case XE_BIAS_M: {
-                float y = v + (g.bias ? g.bias[m] : 0.f);
-                if (g.stride > 1 || g.phase > 0) g.C[(size_t)m * g.ldc + (size_t)n * g.stride + g.phase] = y;
-                else g.C[(size_t)m * g.ldc + n] = y;
-                break;
-            }
-            case XE_BIAS_M_RES:
-                g.C[(size_t)m * g.ldc + n] = v + g.bias[m] + g.res[(size_t)m * g.ldres + n];
-                break;
-            case XE_BIAS_M_SNAKE:
-                g.C[(size_t)m * g.ldc + n] = snake1(v + g.bias[m], g.ea[m], g.eb[m]);
-                break;
-        }
+        if (nz > 1) g.part[((size_t)z * g.M + m) * g.N + n] = acc[r];
+        else xg_epi(g, m, n, acc[r]);
     }
+}
+
+__global__ void k_xg_reduce(XGemm g, int nz) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)g.M * g.N) return;
+    float v = 0.f;
+    for (int z = 0; z < nz; ++z) v += g.part[(size_t)z * g.M * g.N + idx];
+    xg_epi(g, (int)(idx / g.N), (int)(idx % g.N), v);
 }
 
 // RVQ gather-sums (Cd.c:166-227), bit-identical order: sem = 0 + e0[c0];
@@ -247,8 +286,23 @@ __global__ void k_iota(int *p, int n, int zero) {
 
 int qtts_xgemm(const XGemm &g, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
-    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, 1);
+    // split-K when the output has too few tiles to fill the chip (first-packet
+    // sized decodes): z ranges of >= 8 K-steps, partials in g.part
+    const int tiles = grid.x * grid.y, ksteps = (g.K + BK - 1) / BK;
+    int nz = 1;
+    if (g.part && tiles < 192 && ksteps >= 16) {
+        nz = (256 + tiles - 1) / tiles;
+        if (nz > ksteps / 8) nz = ksteps / 8;
+        if (nz > 32) nz = 32;
+        while (nz > 1 && (size_t)nz * g.M * g.N > g.part_elems) --nz;
+    }
+    grid.z = nz;
     hipLaunchKernelGGL(k_xgemm, grid, dim3(256), 0, st, g);
+    if (nz > 1) {
+        const size_t n = (size_t)g.M * g.N;
+        hipLaunchKernelGGL(k_xg_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, nz);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -442,6 +496,9 @@ static int ensure_codec_state(CodecModel *m, int T) {
     m->tg = (float *)scratch_alloc(m, (size_t)cap * d.cinter * 4);
     m->tu = (float *)scratch_alloc(m, (size_t)cap * d.cinter * 4);
     m->codes_tmp = (int *)scratch_alloc(m, (size_t)cap * 2 * 4);  // [0..cap) positions, [cap..2cap) zeros
+    m->xg_part_elems = (size_t)8 << 20;
+    m->xg_part = (float *)scratch_alloc(m, m->xg_part_elems * 4);
+    if (!m->xg_part) return -1;
     if (!m->bufA || !m->bufB || !m->bufC || !m->bufD || !m->tx || !m->txn || !m->tq || !m->tatt || !m->tg || !m->tu ||
         !m->codes_tmp)
         return -1;
@@ -468,6 +525,13 @@ static int ensure_codec_state(CodecModel *m, int T) {
 
 #define KCK(x) do { if ((x) != 0) return -1; } while (0)
 
+// codec GEMMs get the split-K workspace
+static int xgm(CodecModel *m, XGemm g, hipStream_t st) {
+    g.part = m->xg_part;
+    g.part_elems = m->xg_part_elems;
+    return qtts_xgemm(g, st);
+}
+
 static XGemm lin(const float *A, int M, int K, const float *W, int N, float *C, int emode) {
     XGemm g;
     g.M = M; g.N = N; g.K = K; g.amode = XA_ROWS; g.A = A; g.lda = K; g.bmode = XB_WT; g.B = W; g.ldb = K;
@@ -487,7 +551,7 @@ static int conv(CodecModel *m, const float *x, int ci, int L, const std::string 
     g.C = out; g.ldc = L; g.emode = emode; g.bias = bn.empty() ? nullptr : cw(m, bn); g.res = res; g.ldres = L;
     g.ea = ea; g.eb = eb;
     if (!g.A) return -1;
-    return qtts_xgemm(g, m->st);
+    return xgm(m, g, m->st);
 }
 
 // transposed conv (stride s, kernel Kw = s * ntap) as s phase GEMMs
@@ -499,7 +563,7 @@ static int tconv(CodecModel *m, const float *x, int ci, int L, const float *w, c
         g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s; g.phase = ph;
         g.bmode = XB_TCONV; g.B = x; g.ldb = L; g.L = L; g.sa = sa; g.sb = sb;
         g.C = out; g.ldc = L * s; g.emode = XE_BIAS_M; g.bias = bias;
-        KCK(qtts_xgemm(g, st));
+        KCK(xgm(m, g, st));
     }
     return 0;
 }
@@ -514,15 +578,15 @@ static int codec_transformer(CodecModel *m, const float *pc /*[lat][T]*/, int T,
     g.B = cw(m, P + "input_proj.weight"); g.ldb = lat; g.C = m->tx; g.ldc = hid;
     g.bias = cw(m, P + "input_proj.bias");
     g.emode = g.bias ? XE_BIAS_N : XE_STORE;
-    KCK(qtts_xgemm(g, st));
+    KCK(xgm(m, g, st));
     float *q = m->tq, *k = m->tq + (size_t)T * hid, *v = k + (size_t)T * kvd;
     for (int l = 0; l < d.clayers; ++l) {
         const std::string p = P + "layers." + std::to_string(l) + ".";
         hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, m->tx, hid, cw(m, p + "input_layernorm.weight"),
                            d.ceps, m->txn);
-        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "self_attn.q_proj.weight"), hid, q, XE_STORE), st));
-        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "self_attn.k_proj.weight"), kvd, k, XE_STORE), st));
-        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "self_attn.v_proj.weight"), kvd, v, XE_STORE), st));
+        KCK(xgm(m, lin(m->txn, T, hid, cw(m, p + "self_attn.q_proj.weight"), hid, q, XE_STORE), st));
+        KCK(xgm(m, lin(m->txn, T, hid, cw(m, p + "self_attn.k_proj.weight"), kvd, k, XE_STORE), st));
+        KCK(xgm(m, lin(m->txn, T, hid, cw(m, p + "self_attn.v_proj.weight"), kvd, v, XE_STORE), st));
         hipLaunchKernelGGL(k_rope_rows, dim3(T), dim3(256), 0, st, q, hid, nh, hd, m->rope_cos, m->rope_sin);
         hipLaunchKernelGGL(k_rope_rows, dim3(T), dim3(256), 0, st, k, kvd, nkv, hd, m->rope_cos, m->rope_sin);
         AttnArgs a;
@@ -534,18 +598,18 @@ static int codec_transformer(CodecModel *m, const float *pc /*[lat][T]*/, int T,
         XGemm o = lin(m->tatt, T, hid, cw(m, p + "self_attn.o_proj.weight"), hid, m->tx, XE_SCALE_RESID_N);
         o.vec = ls1;
         if (!ls1) return -1;
-        KCK(qtts_xgemm(o, st));
+        KCK(xgm(m, o, st));
         hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, m->tx, hid,
                            cw(m, p + "post_attention_layernorm.weight"), d.ceps, m->txn);
-        KCK(qtts_xgemm(lin(m->txn, T, hid, cw(m, p + "mlp.gate_proj.weight"), I, m->tg, XE_STORE), st));
+        KCK(xgm(m, lin(m->txn, T, hid, cw(m, p + "mlp.gate_proj.weight"), I, m->tg, XE_STORE), st));
         XGemm u = lin(m->txn, T, hid, cw(m, p + "mlp.up_proj.weight"), I, m->tu, XE_SILU_MUL);
         u.aux = m->tg; u.ldaux = I;
-        KCK(qtts_xgemm(u, st));
+        KCK(xgm(m, u, st));
         const float *ls2 = cw(m, p + "mlp_layer_scale.scale");
         XGemm dn = lin(m->tu, T, I, cw(m, p + "mlp.down_proj.weight"), hid, m->tx, XE_SCALE_RESID_N);
         dn.vec = ls2;
         if (!ls2) return -1;
-        KCK(qtts_xgemm(dn, st));
+        KCK(xgm(m, dn, st));
     }
     const float *fn = cw(m, P + "norm.weight");
     const float *xin = m->tx;
@@ -557,7 +621,7 @@ static int codec_transformer(CodecModel *m, const float *pc /*[lat][T]*/, int T,
     og.bias = cw(m, P + "output_proj.bias");
     og.ldc = T;
     if (!og.bias) return -1;
-    return qtts_xgemm(og, st);
+    return xgm(m, og, st);
 }
 
 float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
@@ -597,12 +661,12 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
                            cw(m, p + "1.norm.bias"), 1e-6f, D);
         XGemm g1 = lin(D, L, lat, cw(m, p + "1.pwconv1.weight"), 4 * lat, Cb, XE_BIAS_N_GELU);
         g1.bias = cw(m, p + "1.pwconv1.bias");
-        DCK(qtts_xgemm(g1, st));
+        DCK(xgm(m, g1, st));
         XGemm g2 = lin(Cb, L, 4 * lat, cw(m, p + "1.pwconv2.weight"), lat, cur, XE_BIAS_GAMMA_RES_T);
         g2.bias = cw(m, p + "1.pwconv2.bias");
         g2.vec = cw(m, p + "1.gamma");
         g2.res = cur; g2.ldres = L; g2.ldc = L;
-        DCK(qtts_xgemm(g2, st));
+        DCK(xgm(m, g2, st));
     }
     // 5. vocoder
     float *voc = cur == A ? B : A;

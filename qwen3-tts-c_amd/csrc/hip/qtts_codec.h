@@ -27,6 +27,8 @@ struct CodecModel {
     int t_cap = 0, rope_cap = 0;
     int *codes_tmp = nullptr;
     float *wav = nullptr;
+    float *xg_part = nullptr;                  // split-K workspace of the codec GEMMs
+    size_t xg_part_elems = 0;
 };
 
 void codec_init(CodecModel *m, const qtts_dims_t *d, hipStream_t st);
@@ -67,5 +69,7 @@ struct XGemm {
     const float *bias = nullptr, *vec = nullptr, *aux = nullptr, *res = nullptr;
     int ldaux = 0, ldres = 0;
     const float *ea = nullptr, *eb = nullptr;  // epilogue snake params (XE_BIAS_M_SNAKE)
+    float *part = nullptr;                     // split-K workspace (nullptr: no split)
+    size_t part_elems = 0;
 };
 int qtts_xgemm(const XGemm &g, hipStream_t st);
