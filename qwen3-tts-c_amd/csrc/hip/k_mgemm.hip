@@ -1,0 +1,165 @@
+// k_mgemm.hip - skinny GEMM on the bf16 matrix cores for the multi-row
+// projections: talker prefill over the prompt rows (T.c:254-472, the
+// reference's kernel_matmul_bf16, K.c:185-207) and the text projection
+// (Q.c:823-847).  M <= 64 activation rows x bf16 weights [R, C].
+//
+// Exact-product "3 x bf16" split: each fp32 activation x is written as
+// x1 + x2 + x3 with x1 = bf16(x), x2 = bf16(x - x1), x3 = bf16(x - x1 - x2)
+// (24 significand bits = 3 x 8), and y = W.x1 + W.x2 + W.x3 on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation.  bf16 x bf16 products are
+// exact in fp32, so the result differs from an fp32 GEMV only in summation
+// order (the bar the decode GEMV already meets), at 3/16 of the f32-MFMA
+// instruction count.
+//
+// Mapping: one workgroup = 16 weight rows (the MFMA N side) x all M rows
+// (up to 4 tiles of 16 on the MFMA M side); the four waves take K steps of 32
+// round-robin, then reduce their partial tiles through LDS in wave order.
+// Lane l of a wave loads W[row l&15][k0 + 8(l>>4) .. +7] (one 16 B load) and
+// x[t = l&15][same k] (two float4), which are exactly the B and A operand
+// fragments of mfma_f32_16x16x32_bf16 (cdna_hip_programming.md section 3).
+// RMSNorm (K.c:27-39) is applied while loading x, with per-row 1/rms from
+// k_row_rms.  Epilogues: store / +bias / +bias then SiLU / residual add /
+// SwiGLU over the interleaved gate|up row quads (the up value comes from
+// lane + 4).
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__device__ __forceinline__ short f2bf_rn(float f) {
+    uint32_t u = __float_as_uint(f);
+    u = u + 0x7FFFu + ((u >> 16) & 1u);
+    return (short)(u >> 16);
+}
+__device__ __forceinline__ float bf2f_s(short b) { return __uint_as_float(((uint32_t)(uint16_t)b) << 16); }
+
+// per-row 1/rms of x rows (grid = rows)
+__global__ __launch_bounds__(256) void k_row_rms(const float *x, int ldx, int C, float eps, float *inv) {
+    __shared__ float red[4];
+    const float *xr = x + (size_t)blockIdx.x * ldx;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) s += xr[c] * xr[c];
+    s = block_sum256(s, red);
+    if (threadIdx.x == 0) inv[blockIdx.x] = rms_inv(s, C, eps);
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
+    __shared__ floatx4 red[4][MT][64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r0 = blockIdx.x * 16;
+    const int rl = lane & 15, kq = 8 * (lane >> 4);
+    const int row = r0 + rl < a.R ? r0 + rl : a.R - 1;
+    const int M = a.nb, C = a.C;
+    const bf16_t *wr = a.W + (size_t)row * C + kq;
+    floatx4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int nsteps = C / 32;
+    for (int s = w; s < nsteps; s += 4) {
+        const int k0 = 32 * s;
+        const v4u wq = *reinterpret_cast<const v4u *>(wr + k0);
+        const bf16x8 bw = __builtin_bit_cast(bf16x8, wq);
+        float nw[8];
+        if (a.norm_w) {
+            const float4 n0 = *reinterpret_cast<const float4 *>(a.norm_w + k0 + kq);
+            const float4 n1 = *reinterpret_cast<const float4 *>(a.norm_w + k0 + kq + 4);
+            nw[0] = n0.x; nw[1] = n0.y; nw[2] = n0.z; nw[3] = n0.w;
+            nw[4] = n1.x; nw[5] = n1.y; nw[6] = n1.z; nw[7] = n1.w;
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int t = mt * 16 + rl;
+            float xv[8];
+            if (t < M) {
+                if (a.table) {
+                    const int id = a.ids[(size_t)t * a.ids_bstride];
+                    const v4u q = *reinterpret_cast<const v4u *>(a.table + (size_t)id * C + k0 + kq);
+                    float f[8];
+                    unpack8(q, f);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xv[j] = f[j];
+                } else {
+                    const float *xr = a.x + (size_t)t * a.ldx + k0 + kq;
+                    const float4 x0 = *reinterpret_cast<const float4 *>(xr);
+                    const float4 x1 = *reinterpret_cast<const float4 *>(xr + 4);
+                    xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w;
+                    xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
+                }
+                if (a.norm_w) {
+                    const float iv = inv[t];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xv[j] = xv[j] * iv * nw[j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = 0.f;
+            }
+            bf16x8 h1, h2, h3;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const short b1 = f2bf_rn(xv[j]);
+                const float e1 = xv[j] - bf2f_s(b1);
+                const short b2 = f2bf_rn(e1);
+                const float e2 = e1 - bf2f_s(b2);
+                h1[j] = b1;
+                h2[j] = b2;
+                h3[j] = f2bf_rn(e2);
+            }
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h1, bw, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h2, bw, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h3, bw, acc[mt], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[w][mt][lane] = acc[mt];
+    __syncthreads();
+    // wave mt' finishes M tile mt' (sum over waves in order)
+    for (int mt = w; mt < MT; mt += 4) {
+        floatx4 v = red[0][mt][lane];
+        for (int ww = 1; ww < 4; ++ww) v += red[ww][mt][lane];
+        const int r = r0 + rl;   // C/D: col = lane & 15 (weight row), row = (lane >> 4) * 4 + i (token)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = mt * 16 + (lane >> 4) * 4 + i;
+            float val = v[i];
+            const float up = __shfl(val, lane + 4 < 64 ? lane + 4 : lane, 64);
+            if (t >= M || r >= a.R) continue;
+            float *yr = a.y + (size_t)t * a.ldy;
+            switch (a.epi) {
+                case EPI_STORE: yr[r] = val; break;
+                case EPI_BIAS: yr[r] = val + a.bias[r]; break;
+                case EPI_BIAS_SILU: {
+                    const float z = val + a.bias[r];
+                    yr[r] = z / (1.0f + expf(-z));
+                    break;
+                }
+                case EPI_RESID: yr[r] += val; break;
+                case EPI_SWIGLU:
+                    if ((r & 7) < 4) yr[(r >> 3) * 4 + (r & 3)] = (val / (1.0f + expf(-val))) * up;
+                    break;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// Multi-row projection on the matrix cores.  `inv_scratch` (>= nb floats)
+// receives the per-row 1/rms when a.norm_w is set.  Returns 1 when the shape
+// is not covered (caller uses qtts_gemv), 0 ok, -1 error.
+int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st) {
+    if (a.nb < 2 || a.nb > 64 || a.C % 32 || a.R % 16 || a.xcopy || (a.norm_w && !inv_scratch) ||
+        (a.table && a.norm_w) || (!a.table && (a.ldx % 4 || ((uintptr_t)a.x & 15))) || (a.C % 8))
+        return 1;
+    if (a.norm_w) hipLaunchKernelGGL(k_row_rms, dim3(a.nb), dim3(256), 0, st, a.x, a.ldx, a.C, a.eps, inv_scratch);
+    const dim3 grid(a.R / 16);
+    if (a.nb <= 16) hipLaunchKernelGGL((k_mgemm<1>), grid, dim3(256), 0, st, a, inv_scratch);
+    else if (a.nb <= 32) hipLaunchKernelGGL((k_mgemm<2>), grid, dim3(256), 0, st, a, inv_scratch);
+    else hipLaunchKernelGGL((k_mgemm<4>), grid, dim3(256), 0, st, a, inv_scratch);
+    qtts_last_kernel = a.nb <= 16 ? "k_mgemm<1>" : a.nb <= 32 ? "k_mgemm<2>" : "k_mgemm<4>";
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -38,6 +38,8 @@ struct GemvArgs {
     }
 };
 int qtts_gemv(const GemvArgs &a, hipStream_t st);
+// multi-row (2..64) projection on the bf16 matrix cores (k_mgemm.hip); 1 = not covered
+int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st);
 
 struct AttnArgs {
     int mode = 0;                  // 0 decode (fused q/k norm + rope + cache write), 1 cached

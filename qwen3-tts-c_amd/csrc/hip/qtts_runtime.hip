@@ -115,6 +115,8 @@ struct qtts_dev {
     std::vector<Prof> prof;
     bool profiling = false;
     bool fuse_attn = true;   // QTTS_HIP_NO_FUSE=1: separate attention kernels (A/B diagnostics)
+    bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
+    float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
     int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
@@ -310,6 +312,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->sl.resize(dims->Ls);
     const char *nf = getenv("QTTS_HIP_NO_FUSE");
     dv->fuse_attn = !(nf && atoi(nf));
+    const char *nm = getenv("QTTS_HIP_NO_MFMA");
+    dv->use_mfma = !(nm && atoi(nm));
     codec_init(&dv->codec, dims, dv->st);
     return dv;
 }
@@ -440,6 +444,7 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(ppos, int, R);
     A(psrc, int, R);
     A(plast, int, B);
+    A(pinv, float, 64);
     {
         const int gph = d.NH / d.KV;
         dv->att_nsplit = (dv->S + qtts_attn_keys_per_split(d.HD) - 1) / qtts_attn_keys_per_split(d.HD);
@@ -523,6 +528,31 @@ static int pgemv(qtts_dev *dv, const GemvArgs &a, int kind) {
     ProfScope ps(dv, kind, gemv_bytes(a));
     return qtts_gemv(a, dv->st);
 }
+// Multi-row projection over `rows` activation rows (prefill, text
+// projection): the matrix-core kernel in chunks of 64 rows, else the GEMV in
+// chunks of 16.  Row r of x / y / ids is at r*ldx / r*ldy / r*ids_bstride.
+static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
+    const int xs = a.ldx, ys = a.ldy;
+    for (int r0 = 0; r0 < rows;) {
+        GemvArgs c = a;
+        int nr = rows - r0 < 64 ? rows - r0 : 64;
+        if (c.x) c.x = a.x + (size_t)r0 * xs;
+        if (c.ids) c.ids = a.ids + (size_t)r0 * a.ids_bstride;
+        c.y = a.y + (size_t)r0 * ys;
+        c.nb = nr;
+        int rc = 1;
+        if (nr >= 2 && dv->use_mfma) rc = qtts_mgemm(c, dv->pinv, dv->st);
+        if (rc < 0) return -1;
+        if (rc == 1) {
+            nr = nr < 16 ? nr : 16;
+            c.nb = nr;
+            CKI(qtts_gemv(c, dv->st));
+        }
+        r0 += nr;
+    }
+    return 0;
+}
+
 // QKV projection + decode attention: one fused kernel at batch 1 (the
 // attention runs as the GEMV's tail, k_gemv.hip), else two launches.
 static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
@@ -780,17 +810,14 @@ extern "C" int qtts_dev_prompt(qtts_dev_t *dv, int b, const int *text_ids, int n
     CK(hipMemcpy(dv->pids, text_ids, (size_t)n_text * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dv->pplan, plan, (size_t)nplan * 5 * 4, hipMemcpyHostToDevice));
     // text_embedding -> fc1 (+b, SiLU) -> fc2 (+b), 16 rows per launch (Q.c:823-847)
-    for (int r0 = 0; r0 < n_text; r0 += 16) {
-        const int nr = n_text - r0 < 16 ? n_text - r0 : 16;
-        GemvArgs a = gv(dv->fc1w, d.TH, d.TH, nullptr, 0, dv->pt1 + (size_t)r0 * d.TH, d.TH, nr,
-                        dv->fc1b ? EPI_BIAS_SILU : EPI_STORE);
-        a.table = dv->text_emb; a.ids = dv->pids + r0; a.ids_bstride = 1; a.bias = dv->fc1b;
+    {
         if (!dv->fc1b) { fprintf(stderr, "qtts: text projection without fc1 bias unsupported\n"); return -1; }
-        CKI(qtts_gemv(a, dv->st));
-        a = gv(dv->fc2w, d.H, d.TH, dv->pt1 + (size_t)r0 * d.TH, d.TH, dv->pproj + (size_t)r0 * d.H, d.H, nr,
-               dv->fc2b ? EPI_BIAS : EPI_STORE);
+        GemvArgs a = gv(dv->fc1w, d.TH, d.TH, nullptr, 0, dv->pt1, d.TH, 1, EPI_BIAS_SILU);
+        a.table = dv->text_emb; a.ids = dv->pids; a.ids_bstride = 1; a.bias = dv->fc1b;
+        CKI(rows_proj(dv, a, n_text));
+        a = gv(dv->fc2w, d.H, d.TH, dv->pt1, d.TH, dv->pproj, d.H, 1, dv->fc2b ? EPI_BIAS : EPI_STORE);
         a.bias = dv->fc2b;
-        CKI(qtts_gemv(a, dv->st));
+        CKI(rows_proj(dv, a, n_text));
     }
     PromptArgs pa;
     pa.proj = dv->pproj; pa.plan = dv->pplan; pa.nplan = nplan; pa.H = d.H; pa.codec_emb = dv->codec_emb;
@@ -829,12 +856,10 @@ extern "C" int qtts_dev_prefill(qtts_dev_t *dv) {
     const int QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
     for (int l = 0; l < d.L; ++l) {
         Layer &ly = dv->tl[l];
-        for (int r0 = 0; r0 < R; r0 += 16) {
-            const int nr = R - r0 < 16 ? R - r0 : 16;
-            GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->px + (size_t)r0 * d.H, d.H, dv->pqkv + (size_t)r0 * QKV, QKV, nr,
-                            EPI_STORE);
+        {
+            GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->px, d.H, dv->pqkv, QKV, 1, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
-            CKI(qtts_gemv(a, st));
+            CKI(rows_proj(dv, a, R));
         }
         AttnArgs t;
         t.mode = 1; t.qkv = dv->pqkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
@@ -844,19 +869,16 @@ extern "C" int qtts_dev_prefill(qtts_dev_t *dv) {
         t.out = dv->patt; t.ld_out = AD; t.nrows = R;
         CKI(qtts_qk_prep(t, st));
         CKI(qtts_attention(t, st));
-        for (int r0 = 0; r0 < R; r0 += 16) {
-            const int nr = R - r0 < 16 ? R - r0 : 16;
-            GemvArgs a = gv(ly.wo, d.H, AD, dv->patt + (size_t)r0 * AD, AD, dv->px + (size_t)r0 * d.H, d.H, nr,
-                            EPI_RESID);
+        {
+            GemvArgs a = gv(ly.wo, d.H, AD, dv->patt, AD, dv->px, d.H, 1, EPI_RESID);
             a.nt = 0;
-            CKI(qtts_gemv(a, st));
-            a = gv(ly.wgu, 2 * d.I, d.H, dv->px + (size_t)r0 * d.H, d.H, dv->ph + (size_t)r0 * d.I, d.I, nr,
-                   EPI_SWIGLU);
+            CKI(rows_proj(dv, a, R));
+            a = gv(ly.wgu, 2 * d.I, d.H, dv->px, d.H, dv->ph, d.I, 1, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
-            CKI(qtts_gemv(a, st));
-            a = gv(ly.wdown, d.H, d.I, dv->ph + (size_t)r0 * d.I, d.I, dv->px + (size_t)r0 * d.H, d.H, nr, EPI_RESID);
+            CKI(rows_proj(dv, a, R));
+            a = gv(ly.wdown, d.H, d.I, dv->ph, d.I, dv->px, d.H, 1, EPI_RESID);
             a.nt = 0;
-            CKI(qtts_gemv(a, st));
+            CKI(rows_proj(dv, a, R));
         }
     }
     // last raw hidden of each slot -> x_tk; kv_len = prefill length
@@ -1002,17 +1024,28 @@ extern "C" int qtts_hip_device_count(void) {
 
 extern "C" int qtts_hip_sync(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }
 
+// batch >= 2 goes to the matrix-core kernel (as prefill does), else the GEMV
+static int matvec_any(const GemvArgs &a, hipStream_t st) {
+    static float *inv = nullptr;   // per-row 1/rms scratch of this test-level entry
+    if (a.nb >= 2) {
+        if (!inv && hipMalloc(&inv, 64 * sizeof(float)) != hipSuccess) return -1;
+        const int rc = qtts_mgemm(a, inv, st);
+        if (rc != 1) return rc;
+    }
+    return qtts_gemv(a, st);
+}
+
 extern "C" int qtts_hip_matvec_bf16(float *out, const uint16_t *A, const float *x, int rows, int cols, int batch,
                                     void *stream) {
     GemvArgs a = gv(A, rows, cols, x, cols, out, rows, batch, EPI_STORE);
-    return qtts_gemv(a, (hipStream_t)stream);
+    return matvec_any(a, (hipStream_t)stream);
 }
 
 extern "C" int qtts_hip_rmsnorm_matvec_bf16(float *out, const uint16_t *A, const float *x, const float *w, float eps,
                                             int rows, int cols, int batch, void *stream) {
     GemvArgs a = gv(A, rows, cols, x, cols, out, rows, batch, EPI_STORE);
     a.norm_w = w; a.eps = eps;
-    return qtts_gemv(a, (hipStream_t)stream);
+    return matvec_any(a, (hipStream_t)stream);
 }
 
 extern "C" int qtts_hip_sample_top_k(int *out, const float *logits, int vocab, int top_k, float top_p, float temp,

@@ -56,7 +56,9 @@ def test_matvec_golden(gpu, i):
 # decode shapes of the 1.7B talker / sub-talker + ragged ones
 SHAPES = [(4096, 2048, 1), (2048, 2048, 1), (12288, 2048, 1), (2048, 6144, 1), (3072, 2048, 1), (4096, 1024, 1),
           (1024, 2048, 1), (6144, 1024, 1), (1024, 3072, 1), (2048, 1024, 1), (100, 64, 1), (37, 8192, 1),
-          (2048, 2048, 2), (4096, 1024, 4), (1000, 192, 3), (3072, 2048, 8), (257, 1024, 16)]
+          (2048, 2048, 2), (4096, 1024, 4), (1000, 192, 3), (3072, 2048, 8), (257, 1024, 16),
+          # matrix-core path (batch 2..64: prefill / text projection rows)
+          (12288, 2048, 10), (2048, 6144, 33), (4096, 2048, 64), (2048, 2048, 17), (96, 64, 5)]
 
 
 @pytest.mark.parametrize("R,Cc,B", SHAPES)
@@ -69,7 +71,8 @@ def test_matvec_shapes(gpu, R, Cc, B):
     assert np.all(np.abs(got - ref) <= gemv_bound(A, x)), np.abs(got - ref).max()
 
 
-@pytest.mark.parametrize("R,Cc,B", [(4096, 2048, 1), (2048, 1024, 1), (512, 128, 1), (1024, 2048, 4)])
+@pytest.mark.parametrize("R,Cc,B", [(4096, 2048, 1), (2048, 1024, 1), (512, 128, 1), (1024, 2048, 4),
+                                     (4096, 2048, 40)])
 def test_rmsnorm_matvec(gpu, R, Cc, B):
     import torch
     rng = np.random.default_rng(5 + B)
