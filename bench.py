@@ -211,18 +211,26 @@ def main():
 
     ws, rank, local = dist_setup()
     import torch
+    # one process per GPU; QTTS_BENCH_BACKEND=gloo rehearses N ranks on fewer
+    # GPUs (ranks share devices round-robin), RCCL ("nccl") otherwise
+    backend = os.environ.get("QTTS_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = local % ndev if ndev else local
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import qtts
     from synth_model import prompt_ids
 
     md = args.model_dir or f"/tmp/qtts_bench_{args.preset}"
     ensure_model_shared(md, args.preset, ws, local)
     t = time.time()
-    m = qtts.QwenTTS(md, device=local)
-    log(f"[bench] rank {rank}: model loaded on HIP device {local} in {time.time() - t:.1f}s")
+    m = qtts.QwenTTS(md, device=dev)
+    log(f"[bench] rank {rank}: model loaded on HIP device {dev} in {time.time() - t:.1f}s")
     m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
     prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
 

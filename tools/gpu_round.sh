@@ -4,12 +4,18 @@
 # Usage (via gpurun): bash tools/gpu_round.sh <tag>
 set -eo pipefail
 TAG=${1:-r01}
-MODE=${2:-all}   # all | prof (skip tests and the plain bench run)
+MODE=${2:-all}   # all | prof (skip tests and the plain bench run) | dist (2-rank gloo rehearsal only)
 R=$GRAFT_REPO_ROOT
 [ -z "$R" ] && R=$(pwd)
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+if [ "$MODE" = dist ]; then
+  QTTS_BENCH_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline \
+    --no-profile > $O/dist2.json 2> $O/dist2.err
+  echo done; exit 0
+fi
 if [ "$MODE" = all ]; then
 rc=0
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/gpu_tests.log 2>&1 || rc=$?
