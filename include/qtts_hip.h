@@ -102,6 +102,16 @@ int qtts_dev_get_codes(qtts_dev_t *dev, int b, int *host_codes, int max_frames);
  * host buffer of T*1920 samples (caller frees). */
 float *qtts_dev_codec_slot(qtts_dev_t *dev, int b, int T, int *out_samples);
 
+/* Streaming codec decode, exact and incremental (every codec op is causal:
+ * conv histories, transposed-conv tails and the window-72 transformer K/V are
+ * carried between pushes).  begin resets the stream (max_frames bounds the
+ * total frames); a push decodes T more frames into T * 1920 host samples and
+ * returns the sample count (< 0 on error).  push_slot reads slot b's generated
+ * codes [frame0, frame0 + T) on the device (no host round trip). */
+int qtts_dev_codec_stream_begin(qtts_dev_t *dev, int max_frames);
+int qtts_dev_codec_stream_push_slot(qtts_dev_t *dev, int b, int frame0, int T, float *host_out);
+int qtts_dev_codec_stream_push_host(qtts_dev_t *dev, const int *codes, int T, float *host_out);
+
 /* ---- host-pointer stage wrappers (oracle-level tests, c/qwen_tts.h:483-502) ---- */
 int qtts_dev_talker_prefill_host(qtts_dev_t *dev, const float *embeds, int n, float *hidden_out);
 int qtts_dev_talker_forward_host(qtts_dev_t *dev, const float *embed, float *logits, float *hidden_out);

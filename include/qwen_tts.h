@@ -174,6 +174,7 @@ typedef struct {
     int last_frames;
     int last_stop_reason;        /* 1 eos, 2 max_tokens */
     int last_stop_step;
+    double perf_first_packet_ms; /* qwen_tts_generate_stream(): entry -> first audio chunk delivered */
 } qwen_tts_ctx_t;
 
 qwen_tts_ctx_t *qwen_tts_load(const char *model_dir);
@@ -210,6 +211,22 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
+/* Streaming generation (the reference has only a per-step
+ * progress callback, c/qwen_tts.h:356): audio is decoded incrementally and
+ * exactly (qtts_hip.h codec stream) and handed to `cb` as it is produced --
+ * the first chunk after frame 0 (1920 samples, 80 ms), then every
+ * `chunk_frames` frames, then the tail.  Returns the whole utterance like
+ * qwen_tts_generate (malloc'd, caller frees); NULL on error. */
+typedef void (*qwen_tts_audio_cb)(const float *pcm, int n_samples, void *userdata);
+float *qwen_tts_generate_stream(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
+                                int chunk_frames, qwen_tts_audio_cb cb, void *userdata, int *out_samples);
+/* Incremental codec decode of host codes [time_steps][16]: begin, then push
+ * any number of frames at a time; each push writes time_steps * 1920 samples
+ * to `out` and returns that count (-1 on error).  The concatenation equals
+ * qwen_tts_codec_decode of all frames at once. */
+int qwen_tts_codec_stream_begin(qwen_tts_ctx_t *ctx, int max_frames);
+int qwen_tts_codec_stream_push(qwen_tts_ctx_t *ctx, const int *codes, int time_steps, float *out);
+
 /* sizeof(qwen_tts_ctx_t) as compiled into the library (FFI layout check) */
 size_t qwen_tts_abi_sizeof_ctx(void);
 

@@ -44,7 +44,7 @@ __device__ __forceinline__ float loadB(const XGemm &g, int k, int n) {
         ic = k / ntap;
         t = n - (k - ic * ntap);
     }
-    if (t < 0 || t >= g.L) return 0.f;
+    if (t < g.tmin || t >= g.L) return 0.f;
     const float x = g.B[(size_t)ic * g.ldb + t];
     return g.sa ? snake1(x, g.sa[ic], g.sb[ic]) : x;
 }
@@ -193,7 +193,7 @@ __global__ void k_rvq_sum(const int *codes, int T, int Q, int CB, int vq, const 
 }
 // output projections (1x1, no bias) summed (Cd.c:178-255), sequential sums
 __global__ void k_rvq_proj(const float *ps, const float *pa, const float *ss, const float *as, int vq, int half, int T,
-                           float *out) {
+                           int ldo, float *out) {
 #pragma clang fp contract(off)
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= half * T) return;
@@ -201,10 +201,12 @@ __global__ void k_rvq_proj(const float *ps, const float *pa, const float *ss, co
     float s1 = 0.f, s2 = 0.f;
     for (int k = 0; k < vq; ++k) s1 += ps[(size_t)o * vq + k] * ss[(size_t)k * T + t];
     for (int k = 0; k < vq; ++k) s2 += pa[(size_t)o * vq + k] * as[(size_t)k * T + t];
-    out[idx] = s1 + s2;
+    out[(size_t)o * ldo + t] = s1 + s2;
 }
 // depthwise causal conv k=7 (ConvNeXt dwconv), reference order b + sum_k
-__global__ void k_dwconv(const float *x, const float *w, const float *b, int C, int L, int K, float *y) {
+// (ldx / ldy: row strides; tmin < 0 reads the streaming history in the margin)
+__global__ void k_dwconv(const float *x, int ldx, int tmin, const float *w, const float *b, int C, int L, int K,
+                         float *y, int ldy) {
 #pragma clang fp contract(off)
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (size_t)C * L) return;
@@ -212,24 +214,31 @@ __global__ void k_dwconv(const float *x, const float *w, const float *b, int C, 
     float acc = b ? b[c] : 0.f;
     for (int k = 0; k < K; ++k) {
         const int ti = t - (K - 1) + k;
-        if (ti >= 0) acc += w[(size_t)c * K + k] * x[(size_t)c * L + ti];
+        if (ti >= tmin) acc += w[(size_t)c * K + k] * x[(size_t)c * ldx + ti];
     }
-    y[idx] = acc;
+    y[(size_t)c * ldy + t] = acc;
+}
+// strided 2-D copy (streaming history in / out)
+__global__ void k_copy2d(float *dst, int ldd, const float *src, int lds, int rows, int cols) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)rows * cols) return;
+    const int r = (int)(idx / cols), c = (int)(idx - (size_t)r * cols);
+    dst[(size_t)r * ldd + c] = src[(size_t)r * lds + c];
 }
 // LayerNorm over channels of a channel-major [C][L] tensor, written time-major [L][C] (Cd.c:480-488)
-__global__ __launch_bounds__(256) void k_ln_t(const float *x, int C, int L, const float *w, const float *b, float eps,
-                                              float *y) {
+__global__ __launch_bounds__(256) void k_ln_t(const float *x, int ldx, int C, const float *w, const float *b,
+                                              float eps, float *y) {
     __shared__ float red[8];
     const int t = blockIdx.x;
     float s = 0.f;
-    for (int c = threadIdx.x; c < C; c += 256) s += x[(size_t)c * L + t];
+    for (int c = threadIdx.x; c < C; c += 256) s += x[(size_t)c * ldx + t];
     const float mean = block_sum256(s, red) / (float)C;
     float v = 0.f;
-    for (int c = threadIdx.x; c < C; c += 256) { const float d = x[(size_t)c * L + t] - mean; v += d * d; }
+    for (int c = threadIdx.x; c < C; c += 256) { const float d = x[(size_t)c * ldx + t] - mean; v += d * d; }
     const float var = block_sum256(v, red + 4) / (float)C;
     const float inv = div_rn(1.0f, sqrt_rn(var + eps));
     for (int c = threadIdx.x; c < C; c += 256) {
-        float o = (x[(size_t)c * L + t] - mean) * inv;
+        float o = (x[(size_t)c * ldx + t] - mean) * inv;
         o *= w[c];
         y[(size_t)t * C + c] = o + b[c];
     }
@@ -328,6 +337,7 @@ void codec_free_state(CodecModel *m) {
 }
 
 void codec_destroy(CodecModel *m) {
+    codec_stream_free(m);
     codec_free_state(m);
     for (auto &kv : m->w) hipFree(kv.second);
     m->w.clear();
@@ -637,7 +647,7 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
                        m->cb, B, Cb);
     hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 255) / 256), dim3(256), 0, st,
                        cw(m, "decoder.quantizer.rvq_first.output_proj.weight"),
-                       cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), B, Cb, vq, half, T, A);
+                       cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), B, Cb, vq, half, T, T, A);
     // 2. pre-conv k=3 -> B [lat][T]
     DCK(conv(m, A, d.ccbdim, T, "decoder.pre_conv.conv.weight", "decoder.pre_conv.conv.bias", lat, 3, 1, B, XE_BIAS_M,
              nullptr, nullptr, nullptr));
@@ -655,9 +665,9 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
         L *= f;
         cur = up;
         // ConvNeXt: dwconv -> LN (time-major) -> pw1+GELU -> pw2*gamma (+res, channel-major)
-        hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)lat * L + 255) / 256)), dim3(256), 0, st, cur,
-                           cw(m, p + "1.dwconv.conv.weight"), cw(m, p + "1.dwconv.conv.bias"), lat, L, 7, Cb);
-        hipLaunchKernelGGL(k_ln_t, dim3(L), dim3(256), 0, st, Cb, lat, L, cw(m, p + "1.norm.weight"),
+        hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)lat * L + 255) / 256)), dim3(256), 0, st, cur, L, 0,
+                           cw(m, p + "1.dwconv.conv.weight"), cw(m, p + "1.dwconv.conv.bias"), lat, L, 7, Cb, L);
+        hipLaunchKernelGGL(k_ln_t, dim3(L), dim3(256), 0, st, Cb, L, lat, cw(m, p + "1.norm.weight"),
                            cw(m, p + "1.norm.bias"), 1e-6f, D);
         XGemm g1 = lin(D, L, lat, cw(m, p + "1.pwconv1.weight"), 4 * lat, Cb, XE_BIAS_N_GELU);
         g1.bias = cw(m, p + "1.pwconv1.bias");
@@ -717,8 +727,8 @@ extern "C" int qtts_hip_causal_conv1d(float *out, const float *in, const float *
     hipStream_t st = (hipStream_t)stream;
     if (groups == ci && ci == co) {
         if (dilation != 1) return -1;
-        hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)co * L + 255) / 256)), dim3(256), 0, st, in, w, b, co, L,
-                           k, out);
+        hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)co * L + 255) / 256)), dim3(256), 0, st, in, L, 0, w, b, co,
+                           L, k, out, L);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (groups != 1) return -1;
@@ -747,4 +757,332 @@ extern "C" int qtts_hip_snake_beta(float *out, const float *x, const float *alph
 extern "C" int qtts_hip_expf_glibc(float *out, const float *in, int n, void *stream) {
     hipLaunchKernelGGL(k_expf_glibc, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, out, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ===================================================================== streaming decode
+// Exact incremental decode.  Channel-major activations live
+// in buffers with a left margin of `hm` columns; before a convolution runs,
+// its history slot ((K-1)*dil input columns, or the last input frame of a
+// K = 2s transposed conv) is copied into the margin and read through
+// XGemm::tmin < 0; right after it, the last H columns of [history | new] are
+// saved back.  The transformer keeps the last window-1 K/V rows per layer and
+// continues the absolute positions (RoPE table offset by pos0).
+namespace {
+constexpr int kStreamChunk = 16;   // frames per internal chunk
+
+void *salloc(CodecStream &S, size_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    hipMemset(p, 0, bytes ? bytes : 16);
+    S.allocs.push_back(p);
+    return p;
+}
+
+void copy2d(hipStream_t st, float *dst, int ldd, const float *src, int lds, int rows, int cols) {
+    const size_t n = (size_t)rows * cols;
+    if (n) hipLaunchKernelGGL(k_copy2d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dst, ldd, src, lds, rows, cols);
+}
+
+// history in: slot -> margin of x;  history out: last H columns of [margin | x[0, L)) -> slot
+void hist_in(CodecModel *m, int slot, float *x, int ldx) {
+    CodecStream &S = m->cs;
+    const int H = S.hist_h[slot];
+    copy2d(m->st, x - H, ldx, S.hist[slot], H, S.hist_c[slot], H);
+}
+void hist_out(CodecModel *m, int slot, const float *x, int ldx, int L) {
+    CodecStream &S = m->cs;
+    const int H = S.hist_h[slot];
+    copy2d(m->st, S.hist[slot], H, x + L - H, ldx, S.hist_c[slot], H);
+}
+
+int sconv(CodecModel *m, int slot, float *x, int ldx, int ci, int L, const std::string &wn, const std::string &bn,
+          int co, int K, int dil, float *out, int ldo, int emode, const float *sa, const float *sb, const float *res,
+          const float *ea = nullptr, const float *eb = nullptr) {
+    const int H = (K - 1) * dil;
+    if (H > 0) hist_in(m, slot, x, ldx);
+    XGemm g;
+    g.M = co; g.N = L; g.K = ci * K;
+    g.amode = XA_ROWS; g.A = cw(m, wn); g.lda = ci * K;
+    g.bmode = XB_CONV; g.B = x; g.ldb = ldx; g.Kw = K; g.dil = dil; g.pad = H; g.L = L; g.tmin = -H;
+    g.sa = sa; g.sb = sb;
+    g.C = out; g.ldc = ldo; g.emode = emode; g.bias = bn.empty() ? nullptr : cw(m, bn); g.res = res; g.ldres = ldo;
+    g.ea = ea; g.eb = eb;
+    if (!g.A) return -1;
+    KCK(xgm(m, g, m->st));
+    if (H > 0) hist_out(m, slot, x, ldx, L);
+    return 0;
+}
+
+int stconv(CodecModel *m, int slot, float *x, int ldx, int ci, int L, const float *w, const float *bias, int co, int Kw,
+           int s, float *out, int ldo, const float *sa, const float *sb) {
+    const int H = Kw / s - 1;
+    if (H > 0) hist_in(m, slot, x, ldx);
+    for (int ph = 0; ph < s; ++ph) {
+        XGemm g;
+        g.M = co; g.N = L; g.K = ci * (Kw / s);
+        g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s; g.phase = ph;
+        g.bmode = XB_TCONV; g.B = x; g.ldb = ldx; g.L = L; g.tmin = -H; g.sa = sa; g.sb = sb;
+        g.C = out; g.ldc = ldo; g.emode = XE_BIAS_M; g.bias = bias;
+        KCK(xgm(m, g, m->st));
+    }
+    if (H > 0) hist_out(m, slot, x, ldx, L);
+    return 0;
+}
+
+int stransformer(CodecModel *m, const float *pc, int ldp, int T, float *out, int ldo) {
+    CodecStream &S = m->cs;
+    const qtts_dims_t &d = m->d;
+    const int lat = d.clat, hid = d.chid, nh = d.cheads, nkv = d.ckv, hd = hid / nh, kvd = nkv * hd, I = d.cinter;
+    const int keepmax = d.cwin - 1;
+    hipStream_t st = m->st;
+    const std::string P = "decoder.pre_transformer.";
+    XGemm g;
+    g.M = T; g.N = hid; g.K = lat; g.amode = XA_TRANS; g.A = pc; g.lda = ldp; g.bmode = XB_WT;
+    g.B = cw(m, P + "input_proj.weight"); g.ldb = lat; g.C = S.tx; g.ldc = hid;
+    g.bias = cw(m, P + "input_proj.bias");
+    g.emode = g.bias ? XE_BIAS_N : XE_STORE;
+    KCK(xgm(m, g, st));
+    const float *cs = S.rope_cos + (size_t)S.pos0 * hd, *sn = S.rope_sin + (size_t)S.pos0 * hd;
+    const int hl = S.hl;
+    for (int l = 0; l < d.clayers; ++l) {
+        const std::string p = P + "layers." + std::to_string(l) + ".";
+        float *kcl = S.kc[l], *vcl = S.vc[l];
+        hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, S.tx, hid, cw(m, p + "input_layernorm.weight"),
+                           d.ceps, S.txn);
+        KCK(xgm(m, lin(S.txn, T, hid, cw(m, p + "self_attn.q_proj.weight"), hid, S.tq, XE_STORE), st));
+        KCK(xgm(m, lin(S.txn, T, hid, cw(m, p + "self_attn.k_proj.weight"), kvd, kcl + (size_t)hl * kvd, XE_STORE), st));
+        KCK(xgm(m, lin(S.txn, T, hid, cw(m, p + "self_attn.v_proj.weight"), kvd, vcl + (size_t)hl * kvd, XE_STORE), st));
+        hipLaunchKernelGGL(k_rope_rows, dim3(T), dim3(256), 0, st, S.tq, hid, nh, hd, cs, sn);
+        hipLaunchKernelGGL(k_rope_rows, dim3(T), dim3(256), 0, st, kcl + (size_t)hl * kvd, kvd, nkv, hd, cs, sn);
+        AttnArgs a;
+        a.mode = 1; a.qkv = S.tq; a.ld_qkv = hid; a.kc = kcl; a.vc = vcl; a.S = hl + T; a.pos = S.iota + hl;
+        a.row_b = S.zeros; a.NH = nh; a.KV = nkv; a.HD = hd; a.out = S.tatt; a.ld_out = hid;
+        a.nrows = T; a.win = d.cwin;
+        KCK(qtts_attention(a, st));
+        const float *ls1 = cw(m, p + "self_attn_layer_scale.scale");
+        if (!ls1) return -1;
+        XGemm o = lin(S.tatt, T, hid, cw(m, p + "self_attn.o_proj.weight"), hid, S.tx, XE_SCALE_RESID_N);
+        o.vec = ls1;
+        KCK(xgm(m, o, st));
+        hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, S.tx, hid,
+                           cw(m, p + "post_attention_layernorm.weight"), d.ceps, S.txn);
+        KCK(xgm(m, lin(S.txn, T, hid, cw(m, p + "mlp.gate_proj.weight"), I, S.tg, XE_STORE), st));
+        XGemm u = lin(S.txn, T, hid, cw(m, p + "mlp.up_proj.weight"), I, S.tu, XE_SILU_MUL);
+        u.aux = S.tg; u.ldaux = I;
+        KCK(xgm(m, u, st));
+        const float *ls2 = cw(m, p + "mlp_layer_scale.scale");
+        if (!ls2) return -1;
+        XGemm dn = lin(S.tu, T, I, cw(m, p + "mlp.down_proj.weight"), hid, S.tx, XE_SCALE_RESID_N);
+        dn.vec = ls2;
+        KCK(xgm(m, dn, st));
+        // keep the last window-1 rows for the next chunk
+        const int tot = hl + T, keep = tot < keepmax ? tot : keepmax;
+        if (keep > 0 && tot > keep) {
+            copy2d(st, S.kvtmp, kvd, kcl + (size_t)(tot - keep) * kvd, kvd, keep, kvd);
+            copy2d(st, kcl, kvd, S.kvtmp, kvd, keep, kvd);
+            copy2d(st, S.kvtmp, kvd, vcl + (size_t)(tot - keep) * kvd, kvd, keep, kvd);
+            copy2d(st, vcl, kvd, S.kvtmp, kvd, keep, kvd);
+        }
+    }
+    {
+        const int tot = hl + T;
+        S.hl = tot < keepmax ? tot : keepmax;
+    }
+    const float *fn = cw(m, P + "norm.weight");
+    const float *xin = S.tx;
+    if (fn) {
+        hipLaunchKernelGGL(k_rms_rows, dim3(T), dim3(256), 0, st, S.tx, hid, fn, d.ceps, S.txn);
+        xin = S.txn;
+    }
+    XGemm og = lin(xin, T, hid, cw(m, P + "output_proj.weight"), lat, out, XE_BIAS_T);
+    og.bias = cw(m, P + "output_proj.bias");
+    og.ldc = ldo;
+    if (!og.bias) return -1;
+    return xgm(m, og, st);
+}
+
+int add_slot(CodecStream &S, int c, int h) {
+    S.hist_c.push_back(c);
+    S.hist_h.push_back(h);
+    S.hist.push_back((float *)salloc(S, (size_t)c * (h > 0 ? h : 1) * 4));
+    return S.hist.back() ? (int)S.hist.size() - 1 : -1;
+}
+}  // namespace
+
+void codec_stream_free(CodecModel *m) {
+    CodecStream &S = m->cs;
+    for (void *p : S.allocs) hipFree(p);
+    S = CodecStream();
+}
+
+int codec_stream_begin(CodecModel *m, int max_frames) {
+    const qtts_dims_t &d = m->d;
+    codec_stream_free(m);
+    if (ensure_codec_state(m, 1)) return -1;   // split-K workspace
+    CodecStream &S = m->cs;
+    S.tc = kStreamChunk;
+    const int hm = S.hm, tc = S.tc;
+    // activation buffers: largest C x (hm + L) over the stages at tc frames
+    size_t L = (size_t)tc * d.ratios[0] * d.ratios[1];
+    size_t mx = (size_t)d.clat * L * 4 + (size_t)4 * d.clat * hm;
+    if ((size_t)d.cdec * (L + hm) > mx) mx = (size_t)d.cdec * (L + hm);
+    int C = d.cdec;
+    for (int b = 0; b < 4; ++b) {
+        L *= d.rates[b];
+        C /= 2;
+        if ((size_t)C * (L + hm) > mx) mx = (size_t)C * (L + hm);
+    }
+    if ((size_t)d.clat * (tc + hm) > mx) mx = (size_t)d.clat * (tc + hm);
+    S.buf_elems = mx + hm;
+    S.bufA = (float *)salloc(S, S.buf_elems * 4);
+    S.bufB = (float *)salloc(S, S.buf_elems * 4);
+    S.bufC = (float *)salloc(S, S.buf_elems * 4);
+    S.bufD = (float *)salloc(S, S.buf_elems * 4);
+    const int hid = d.chid, hd = hid / d.cheads, kvd = d.ckv * hd, keep = d.cwin - 1;
+    S.tx = (float *)salloc(S, (size_t)tc * hid * 4);
+    S.txn = (float *)salloc(S, (size_t)tc * hid * 4);
+    S.tq = (float *)salloc(S, (size_t)tc * hid * 4);
+    S.tatt = (float *)salloc(S, (size_t)tc * hid * 4);
+    S.tg = (float *)salloc(S, (size_t)tc * d.cinter * 4);
+    S.tu = (float *)salloc(S, (size_t)tc * d.cinter * 4);
+    const int vq = d.ccbdim / 2;
+    S.rvq_s = (float *)salloc(S, (size_t)vq * tc * 4);
+    S.rvq_a = (float *)salloc(S, (size_t)vq * tc * 4);
+    for (int l = 0; l < d.clayers; ++l) {
+        S.kc.push_back((float *)salloc(S, (size_t)(keep + tc) * kvd * 4));
+        S.vc.push_back((float *)salloc(S, (size_t)(keep + tc) * kvd * 4));
+    }
+    S.kvtmp = (float *)salloc(S, (size_t)(keep > 0 ? keep : 1) * kvd * 4);
+    // RoPE table for absolute positions [0, max_frames + tc) (theta 1e4, Cd.c:309)
+    S.rope_cap = max_frames + tc;
+    const int half = hd / 2;
+    std::vector<float> c((size_t)S.rope_cap * hd), s((size_t)S.rope_cap * hd);
+    for (int p = 0; p < S.rope_cap; ++p)
+        for (int i = 0; i < half; ++i) {
+            float freq = 1.0f / powf(10000.0f, (float)(2 * i) / (float)hd);
+            float ang = (float)p * freq;
+            c[(size_t)p * hd + i] = c[(size_t)p * hd + i + half] = cosf(ang);
+            s[(size_t)p * hd + i] = s[(size_t)p * hd + i + half] = sinf(ang);
+        }
+    S.rope_cos = (float *)salloc(S, c.size() * 4);
+    S.rope_sin = (float *)salloc(S, s.size() * 4);
+    std::vector<int> io(keep + tc + 1);
+    for (size_t i = 0; i < io.size(); ++i) io[i] = (int)i;
+    S.iota = (int *)salloc(S, io.size() * 4);
+    S.zeros = (int *)salloc(S, (size_t)tc * 4);
+    for (void *p : S.allocs)
+        if (!p) return -1;
+    if (!S.bufA || !S.bufB || !S.bufC || !S.bufD || !S.rope_cos || !S.rope_sin || !S.iota || !S.zeros) return -1;
+    if (hipMemcpy(S.rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    if (hipMemcpy(S.rope_sin, s.data(), s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    if (hipMemcpy(S.iota, io.data(), io.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    // history slots, in the order codec_stream_push consumes them
+    add_slot(S, d.ccbdim, 2);                  // 0 pre-conv k3
+    add_slot(S, d.clat, 6);                    // 1 upsample 0 dwconv k7
+    add_slot(S, d.clat, 6);                    // 2 upsample 1 dwconv k7
+    add_slot(S, d.clat, 6);                    // 3 vocoder conv0 k7
+    C = d.cdec;
+    static const int dil[3] = {1, 3, 9};
+    for (int b = 0; b < 4; ++b) {
+        add_slot(S, C, 1);                     // block tconv (K = 2r): last input frame
+        for (int u = 0; u < 3; ++u) add_slot(S, C / 2, 6 * dil[u]);   // ResUnit conv1 k7 dil
+        C /= 2;
+    }
+    add_slot(S, C, 6);                         // final conv k7
+    for (float *h : S.hist)
+        if (!h) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    S.active = true;
+    return 0;
+}
+
+int codec_stream_push(CodecModel *m, const int *codes, int ldc_codes, int Ttot, float *host_out) {
+    CodecStream &S = m->cs;
+    const qtts_dims_t &d = m->d;
+    if (!S.active || ldc_codes != d.cq) return -1;
+    if (S.pos0 + Ttot > S.rope_cap - S.tc) {
+        fprintf(stderr, "qtts codec stream: %d frames exceed the stream capacity\n", S.pos0 + Ttot);
+        return -1;
+    }
+    hipStream_t st = m->st;
+    const int lat = d.clat, vq = d.ccbdim / 2, half = lat / 2, hm = S.hm;
+    int written = 0;
+    for (int t0 = 0; t0 < Ttot; t0 += S.tc) {
+        const int T = Ttot - t0 < S.tc ? Ttot - t0 : S.tc;
+        float *A = S.bufA + hm, *B = S.bufB + hm, *Cb = S.bufC, *D = S.bufD;
+        int L = T, ld = hm + L;
+        // 1. RVQ dequantise -> A [half][T]
+        hipLaunchKernelGGL(k_rvq_sum, dim3(T), dim3(vq < 64 ? 64 : (vq + 63) / 64 * 64), 0, st,
+                           codes + (size_t)t0 * d.cq, T, d.cq, d.ccb, vq, m->cb, S.rvq_s, S.rvq_a);
+        hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 255) / 256), dim3(256), 0, st,
+                           cw(m, "decoder.quantizer.rvq_first.output_proj.weight"),
+                           cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), S.rvq_s, S.rvq_a, vq, half, T, ld, A);
+        // 2. pre-conv k3 -> B
+        KCK(sconv(m, 0, A, ld, d.ccbdim, L, "decoder.pre_conv.conv.weight", "decoder.pre_conv.conv.bias", lat, 3, 1, B,
+                  ld, XE_BIAS_M, nullptr, nullptr, nullptr));
+        // 3. transformer -> A
+        KCK(stransformer(m, B, ld, T, A, ld));
+        // 4. upsample x2: tconv (K = s, no history) + ConvNeXt
+        float *cur = A;
+        for (int s = 0; s < 2; ++s) {
+            const int f = d.ratios[s];
+            const std::string p = "decoder.upsample." + std::to_string(s) + ".";
+            float *up = cur == A ? B : A;
+            const int ldu = hm + L * f;
+            KCK(stconv(m, -1, cur, ld, lat, L, cw(m, p + "0.conv.weight"), cw(m, p + "0.conv.bias"), lat, f, f, up, ldu,
+                       nullptr, nullptr));
+            L *= f;
+            ld = ldu;
+            cur = up;
+            hist_in(m, 1 + s, cur, ld);
+            hipLaunchKernelGGL(k_dwconv, dim3((unsigned)(((size_t)lat * L + 255) / 256)), dim3(256), 0, st, cur, ld, -6,
+                               cw(m, p + "1.dwconv.conv.weight"), cw(m, p + "1.dwconv.conv.bias"), lat, L, 7, Cb, L);
+            hist_out(m, 1 + s, cur, ld, L);
+            hipLaunchKernelGGL(k_ln_t, dim3(L), dim3(256), 0, st, Cb, L, lat, cw(m, p + "1.norm.weight"),
+                               cw(m, p + "1.norm.bias"), 1e-6f, D);
+            XGemm g1 = lin(D, L, lat, cw(m, p + "1.pwconv1.weight"), 4 * lat, Cb, XE_BIAS_N_GELU);
+            g1.bias = cw(m, p + "1.pwconv1.bias");
+            KCK(xgm(m, g1, st));
+            XGemm g2 = lin(Cb, L, 4 * lat, cw(m, p + "1.pwconv2.weight"), lat, cur, XE_BIAS_GAMMA_RES_T);
+            g2.bias = cw(m, p + "1.pwconv2.bias");
+            g2.vec = cw(m, p + "1.gamma");
+            g2.res = cur; g2.ldres = ld; g2.ldc = ld;
+            KCK(xgm(m, g2, st));
+        }
+        // 5. vocoder
+        float *voc = cur == A ? B : A;
+        KCK(sconv(m, 3, cur, ld, lat, L, "decoder.decoder.0.conv.weight", "decoder.decoder.0.conv.bias", d.cdec, 7, 1,
+                  voc, ld, XE_BIAS_M, nullptr, nullptr, nullptr));
+        int C = d.cdec, slot = 4;
+        static const int dil[3] = {1, 3, 9};
+        for (int b = 0; b < 4; ++b) {
+            const int r = d.rates[b], co = C / 2;
+            const std::string p = "decoder.decoder." + std::to_string(b + 1) + ".block.";
+            float *nx = voc == A ? B : A;
+            const int ldn = hm + L * r;
+            KCK(stconv(m, slot++, voc, ld, C, L, cw(m, p + "1.conv.weight"), cw(m, p + "1.conv.bias"), co, 2 * r, r, nx,
+                       ldn, cw(m, p + "0.alpha"), cw(m, p + "0.beta")));
+            L *= r;
+            ld = ldn;
+            C = co;
+            voc = nx;
+            for (int u = 0; u < 3; ++u) {
+                const std::string q = p + std::to_string(u + 2) + ".";
+                KCK(sconv(m, slot++, voc, ld, C, L, q + "conv1.conv.weight", q + "conv1.conv.bias", C, 7, dil[u], Cb, L,
+                          XE_BIAS_M_SNAKE, cw(m, q + "act1.alpha"), cw(m, q + "act1.beta"), nullptr,
+                          cw(m, q + "act2.alpha"), cw(m, q + "act2.beta")));
+                KCK(sconv(m, -1, Cb, L, C, L, q + "conv2.conv.weight", q + "conv2.conv.bias", C, 1, 1, voc, ld,
+                          XE_BIAS_M_RES, nullptr, nullptr, voc));
+            }
+        }
+        float *wav = voc == A ? B : A;
+        KCK(sconv(m, slot, voc, ld, C, L, "decoder.decoder.6.conv.weight", "decoder.decoder.6.conv.bias", 1, 7, 1, wav,
+                  ld, XE_BIAS_M, cw(m, "decoder.decoder.5.alpha"), cw(m, "decoder.decoder.5.beta"), nullptr));
+        hipLaunchKernelGGL(k_clamp, dim3((L + 255) / 256), dim3(256), 0, st, wav, L);
+        if (hipMemcpyAsync(host_out + written, wav, (size_t)L * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+        written += L;
+        S.pos0 += T;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return -1;
+    return written;
 }

@@ -9,6 +9,32 @@
 
 #include "../../../include/qtts_hip.h"
 
+// Exact streaming decode state (codec_stream_*): every codec op is causal, so
+// decoding frames chunk by chunk with (a) the last (K-1)*dil input columns of
+// every convolution, (b) the last input frame of every transposed conv with
+// K = 2s and (c) the last window-1 K/V rows of every transformer layer
+// carried across chunks equals the full decode (Cd.c:581-749) up to fp order.
+struct CodecStream {
+    bool active = false;
+    int pos0 = 0;              // frames decoded so far (absolute transformer position)
+    int tc = 0;                // max frames per internal chunk
+    int hm = 64;               // left margin (columns) of every channel-major buffer
+    std::vector<float *> hist; // history slots [C][H]
+    std::vector<int> hist_c, hist_h;
+    std::vector<float *> kc, vc;  // transformer layer caches [(win-1) + tc][kvd]
+    float *kvtmp = nullptr;
+    int hl = 0;                // valid history rows in the K/V caches
+    float *bufA = nullptr, *bufB = nullptr, *bufC = nullptr, *bufD = nullptr;
+    size_t buf_elems = 0;
+    float *tx = nullptr, *txn = nullptr, *tq = nullptr, *tatt = nullptr, *tg = nullptr, *tu = nullptr;
+    float *rvq_s = nullptr, *rvq_a = nullptr;
+    float *rope_cos = nullptr, *rope_sin = nullptr;
+    int rope_cap = 0;
+    int *iota = nullptr;       // [0 .. win + tc)
+    int *zeros = nullptr;
+    std::vector<void *> allocs;
+};
+
 struct CodecModel {
     qtts_dims_t d{};
     hipStream_t st = nullptr;
@@ -29,6 +55,7 @@ struct CodecModel {
     float *wav = nullptr;
     float *xg_part = nullptr;                  // split-K workspace of the codec GEMMs
     size_t xg_part_elems = 0;
+    CodecStream cs;
 };
 
 void codec_init(CodecModel *m, const qtts_dims_t *d, hipStream_t st);
@@ -40,6 +67,12 @@ int codec_put_tensor(CodecModel *m, const std::string &name, const void *host, i
 int codec_finalize(CodecModel *m);
 // codes: device int32 [T][cq] (time-major).  Returns malloc'd host audio.
 float *codec_decode(CodecModel *m, const int *codes_dev, int T, int *out_samples);
+// streaming decode: begin resets the state (max_frames bounds the absolute
+// position); push decodes T more frames (device codes, rows of stride ldc
+// ints) and writes T * 1920 samples to host_out.  Returns samples or -1.
+int codec_stream_begin(CodecModel *m, int max_frames);
+int codec_stream_push(CodecModel *m, const int *codes_dev, int ldc, int T, float *host_out);
+void codec_stream_free(CodecModel *m);
 
 // ---- generic fp32 implicit GEMM (exported for the kernel-level C-ABI) ----
 // C(m, n) = sum_k A(m, k) * B(k, n), fp32 products on v_mfma_f32_32x32x2_f32.
@@ -71,5 +104,7 @@ struct XGemm {
     const float *ea = nullptr, *eb = nullptr;  // epilogue snake params (XE_BIAS_M_SNAKE)
     float *part = nullptr;                     // split-K workspace (nullptr: no split)
     size_t part_elems = 0;
+    int tmin = 0;                              // conv/tconv input columns t >= tmin are read (t < 0: the
+                                               // streaming history kept in the buffer's left margin)
 };
 int qtts_xgemm(const XGemm &g, hipStream_t st);

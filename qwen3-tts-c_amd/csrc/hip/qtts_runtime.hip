@@ -929,6 +929,33 @@ extern "C" float *qtts_dev_codec_slot(qtts_dev_t *dv, int b, int T, int *out_sam
     return codec_decode(&dv->codec, dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G, T, out_samples);
 }
 
+// ----------------------------------------------------------------- streaming codec (exact, incremental)
+extern "C" int qtts_dev_codec_stream_begin(qtts_dev_t *dv, int max_frames) {
+    if (!dv || max_frames < 1) return -1;
+    hipSetDevice(dv->device);
+    CK(hipStreamSynchronize(dv->st));
+    return codec_stream_begin(&dv->codec, max_frames);
+}
+
+extern "C" int qtts_dev_codec_stream_push_slot(qtts_dev_t *dv, int b, int frame0, int T, float *host_out) {
+    if (!dv || b < 0 || b >= dv->nb || T < 1 || frame0 < 0 || frame0 + T > dv->max_frames + 1) return -1;
+    hipSetDevice(dv->device);
+    const int *codes = dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G + (size_t)frame0 * dv->d.G;
+    return codec_stream_push(&dv->codec, codes, dv->d.G, T, host_out);
+}
+
+extern "C" int qtts_dev_codec_stream_push_host(qtts_dev_t *dv, const int *codes, int T, float *host_out) {
+    if (!dv || T < 1) return -1;
+    hipSetDevice(dv->device);
+    int *dc = nullptr;
+    if (hipMalloc(&dc, (size_t)T * dv->d.cq * 4) != hipSuccess) return -1;
+    int r = -1;
+    if (hipMemcpy(dc, codes, (size_t)T * dv->d.cq * 4, hipMemcpyHostToDevice) == hipSuccess)
+        r = codec_stream_push(&dv->codec, dc, dv->d.cq, T, host_out);
+    hipFree(dc);
+    return r;
+}
+
 // ----------------------------------------------------------------- host-pointer stage wrappers
 static int ensure_slot0(qtts_dev *dv) {
     if (dv->nb >= 1) return 0;

@@ -9,7 +9,9 @@
  *   --fixed-codec-tokens --seed --subtalker-temperature --subtalker-top-k
  *   --subtalker-top-p --benchmark-runs --benchmark-warmup
  * Additions: --device N (HIP device), --batch N (N copies of the prompt in
- * one lock-step batch; the first one's audio is written).
+ * one lock-step batch; the first one's audio is written), --stream N (exact
+ * streaming decode: audio delivered after frame 0 and then every N frames;
+ * prints "First packet: X ms").
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,7 +39,8 @@ static void usage(const char *prog) {
             "  --max-tokens N (4096)   --fixed-codec-tokens N   --seed N (42)\n"
             "  --subtalker-temperature F (0.9)   --subtalker-top-k N (50)   --subtalker-top-p F (1.0)\n"
             "  --benchmark-runs N (1)  --benchmark-warmup N (0)\n"
-            "  --device N (HIP device, default 0)   --batch N (lock-step batch of N copies, default 1)\n",
+            "  --device N (HIP device, default 0)   --batch N (lock-step batch of N copies, default 1)\n"
+            "  --stream N (streaming decode, audio chunks every N frames after the first)\n",
             prog);
 }
 
@@ -74,7 +77,7 @@ static void progress(int step, int total, void *u) {
 
 int main(int argc, char **argv) {
     const char *dir = NULL, *ids = NULL, *ids_file = NULL, *spk = NULL, *lang = NULL, *out = "output.wav";
-    int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1;
+    int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1, stream_chunk = 0;
     float temp = -1, st_temp = -1, top_p = -1, st_top_p = -1, rep = -1;
     int top_k = -1, st_top_k = -1, max_tokens = -1, fixed = -1, seed = -1;
     for (int i = 1; i < argc; i++) {
@@ -102,6 +105,7 @@ int main(int argc, char **argv) {
         else if (ARG("--benchmark-warmup")) warmup = (int)strtol(argv[++i], NULL, 10);
         else if (ARG("--device")) device = (int)strtol(argv[++i], NULL, 10);
         else if (ARG("--batch")) batch = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--stream")) stream_chunk = (int)strtol(argv[++i], NULL, 10);
         else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); return 0; }
         else {
             fprintf(stderr, "Unknown option: %s\n", a);
@@ -156,7 +160,10 @@ int main(int argc, char **argv) {
         float *ra = NULL;
         int rn = 0;
         long total_samples = 0;
-        if (batch == 1) {
+        if (batch == 1 && stream_chunk > 0) {
+            ra = qwen_tts_generate_stream(ctx, ids, spk, lang, stream_chunk, NULL, NULL, &rn);
+            total_samples = rn;
+        } else if (batch == 1) {
             ra = qwen_tts_generate(ctx, ids, spk, lang, &rn);
             total_samples = rn;
         } else {

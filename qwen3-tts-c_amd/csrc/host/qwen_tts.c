@@ -431,8 +431,15 @@ static void params_of(const qwen_tts_ctx_t *ctx, qtts_gen_params_t *p) {
 /* ------------------------------------------------------------- generation */
 /* Runs nb utterances in lock-step frames.  Fills per-slot frame counts and
  * stop info; audio[i] decoded per slot.  Returns 0 on success. */
+typedef struct {                 /* streaming output of run_batch (nb == 1) */
+    qwen_tts_audio_cb cb;
+    void *user;
+    int chunk;
+} stream_t;
+
 static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
-                     const char *const *languages, float **audio, int *samples, double t_start) {
+                     const char *const *languages, float **audio, int *samples, double t_start,
+                     const stream_t *stream) {
     qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
     const qwen_tts_config_t *c = &ctx->config;
     const int G = c->num_code_groups;
@@ -479,18 +486,39 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     }
     int *stopped = (int *)calloc(nb, sizeof(int)), *ngen = (int *)calloc(nb, sizeof(int));
     int *sstep = (int *)calloc(nb, sizeof(int));
+    /* streaming: exact incremental codec decode of the frames produced so far */
+    float *sbuf = NULL;
+    int streamed = 0;
+    double t_stream = 0;
+    if (stream) {
+        sbuf = (float *)malloc((size_t)max_tokens * 1920 * sizeof(float));
+        if (!sbuf || qtts_dev_codec_stream_begin(dev, max_tokens) != 0) {
+            free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
+        }
+    }
     double t_gen = now_ms();
     const int poll_every = fixed > 0 ? 0 : 8;
     int step = 0;
     for (; step < max_tokens; step++) {
-        if (qtts_dev_frame(dev, step) != 0) { free(stopped); free(ngen); free(sstep); goto out; }
+        if (qtts_dev_frame(dev, step) != 0) { free(sbuf); free(stopped); free(ngen); free(sstep); goto out; }
         if (step == 0) {
             qtts_dev_poll(dev, NULL, NULL, NULL);
             ctx->perf_first_frame_ms = now_ms() - t_start;
         }
         if (ctx->progress_cb) ctx->progress_cb(step + 1, max_tokens, ctx->progress_cb_userdata);
-        if (poll_every && ((step + 1) % poll_every == 0 || step + 1 == max_tokens)) {
+        const int want_stream = stream && (step == 0 || step + 1 - streamed >= stream->chunk || step + 1 == max_tokens);
+        if (want_stream || (poll_every && ((step + 1) % poll_every == 0 || step + 1 == max_tokens))) {
             qtts_dev_poll(dev, stopped, ngen, sstep);
+            if (stream && ngen[0] > streamed) {
+                const double t0 = now_ms();
+                const int n = qtts_dev_codec_stream_push_slot(dev, 0, streamed, ngen[0] - streamed,
+                                                              sbuf + (size_t)streamed * 1920);
+                if (n < 0) { free(sbuf); free(stopped); free(ngen); free(sstep); goto out; }
+                t_stream += now_ms() - t0;
+                if (stream->cb) stream->cb(sbuf + (size_t)streamed * 1920, n, stream->user);
+                if (streamed == 0) ctx->perf_first_packet_ms = now_ms() - t_start;
+                streamed = ngen[0];
+            }
             int all = 1;
             for (int b = 0; b < nb; b++) all &= stopped[b];
             if (qwen_tts_verbose >= 1 && ngen[0] > 0 && ngen[0] % 10 < poll_every)
@@ -499,8 +527,18 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
         }
     }
     qtts_dev_poll(dev, stopped, ngen, sstep);
+    if (stream && ngen[0] > streamed) {
+        const double t0 = now_ms();
+        const int n = qtts_dev_codec_stream_push_slot(dev, 0, streamed, ngen[0] - streamed,
+                                                      sbuf + (size_t)streamed * 1920);
+        if (n < 0) { free(sbuf); free(stopped); free(ngen); free(sstep); goto out; }
+        t_stream += now_ms() - t0;
+        if (stream->cb) stream->cb(sbuf + (size_t)streamed * 1920, n, stream->user);
+        if (streamed == 0) ctx->perf_first_packet_ms = now_ms() - t_start;
+        streamed = ngen[0];
+    }
     double t_gen_done = now_ms();
-    ctx->perf_talker_ms = t_gen_done - t_gen;
+    ctx->perf_talker_ms = t_gen_done - t_gen - t_stream;
     ctx->perf_codec_tokens = ngen[0];
     ctx->last_stop_reason = stopped[0] ? 1 : 2;
     ctx->last_stop_step = stopped[0] ? sstep[0] : max_tokens;
@@ -522,14 +560,21 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     }
     double t_codec = now_ms();
     rc = 0;
-    for (int b = 0; b < nb; b++) {
-        audio[b] = NULL;
-        samples[b] = 0;
-        if (ngen[b] <= 0) { rc = -1; continue; }
-        audio[b] = qtts_dev_codec_slot(dev, b, ngen[b], &samples[b]);
-        if (!audio[b] || samples[b] <= 0) rc = -1;
+    if (stream) {   /* the streamed chunks already are the utterance */
+        audio[0] = sbuf;
+        samples[0] = streamed * 1920;
+        if (streamed <= 0) { free(sbuf); audio[0] = NULL; rc = -1; }
+        ctx->perf_codec_ms = t_stream;
+    } else {
+        for (int b = 0; b < nb; b++) {
+            audio[b] = NULL;
+            samples[b] = 0;
+            if (ngen[b] <= 0) { rc = -1; continue; }
+            audio[b] = qtts_dev_codec_slot(dev, b, ngen[b], &samples[b]);
+            if (!audio[b] || samples[b] <= 0) rc = -1;
+        }
+        ctx->perf_codec_ms = now_ms() - t_codec;
     }
-    ctx->perf_codec_ms = now_ms() - t_codec;
     ctx->perf_total_ms = now_ms() - t_start;
     free(stopped); free(ngen); free(sstep);
 out:
@@ -546,7 +591,7 @@ float *qwen_tts_generate(qwen_tts_ctx_t *ctx, const char *text, const char *spea
     float *audio = NULL;
     int n = 0;
     const char *texts[1] = {text}, *spk[1] = {speaker}, *lang[1] = {language};
-    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start);
+    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start, NULL);
     if (rc != 0 || !audio || n <= 0) {
         free(audio);
         *out_samples = 0;
@@ -564,7 +609,41 @@ float *qwen_tts_generate(qwen_tts_ctx_t *ctx, const char *text, const char *spea
 int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                             const char *const *languages, float **out_audio, int *out_samples) {
     if (!ctx || nb < 1 || !texts || !out_audio || !out_samples) return -1;
-    return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms());
+    return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms(), NULL);
+}
+
+float *qwen_tts_generate_stream(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
+                                int chunk_frames, qwen_tts_audio_cb cb, void *userdata, int *out_samples) {
+    if (!ctx || !out_samples) return NULL;
+    *out_samples = 0;
+    double t_start = now_ms();
+    stream_t st = {cb, userdata, chunk_frames > 0 ? chunk_frames : 1};
+    float *audio = NULL;
+    int n = 0;
+    const char *texts[1] = {text}, *spk[1] = {speaker}, *lang[1] = {language};
+    ctx->perf_first_packet_ms = 0;
+    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start, &st);
+    if (rc != 0 || !audio || n <= 0) {
+        free(audio);
+        return NULL;
+    }
+    if (qwen_tts_verbose >= 1) {
+        fprintf(stderr, "First packet: %.1f ms\n", ctx->perf_first_packet_ms);
+        fprintf(stderr, "Total: %.1f ms (%.2f s audio, %.2fx realtime)\n", ctx->perf_total_ms,
+                (float)n / QWEN_TTS_SAMPLE_RATE, ((float)n / QWEN_TTS_SAMPLE_RATE) / (ctx->perf_total_ms / 1000.0));
+    }
+    *out_samples = n;
+    return audio;
+}
+
+int qwen_tts_codec_stream_begin(qwen_tts_ctx_t *ctx, int max_frames) {
+    if (!ctx || !ctx->hip) return -1;
+    return qtts_dev_codec_stream_begin((qtts_dev_t *)ctx->hip, max_frames);
+}
+
+int qwen_tts_codec_stream_push(qwen_tts_ctx_t *ctx, const int *codes, int time_steps, float *out) {
+    if (!ctx || !ctx->hip || !codes || !out || time_steps < 1) return -1;
+    return qtts_dev_codec_stream_push_host((qtts_dev_t *)ctx->hip, codes, time_steps, out);
 }
 
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames) {

@@ -22,6 +22,7 @@ _fp = C.POINTER(C.c_float)
 _ip = C.POINTER(C.c_int)
 
 PROGRESS_CB = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p)
+AUDIO_CB = C.CFUNCTYPE(None, C.POINTER(C.c_float), C.c_int, C.c_void_p)
 
 
 class Config(C.Structure):  # qwen_tts_config_t (include/qwen_tts.h)
@@ -54,6 +55,7 @@ class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
         ("perf_total_ms", C.c_double), ("perf_talker_ms", C.c_double), ("perf_codec_ms", C.c_double),
         ("perf_codec_tokens", C.c_int), ("perf_prefill_ms", C.c_double), ("perf_first_frame_ms", C.c_double),
         ("last_codes", _ip), ("last_frames", C.c_int), ("last_stop_reason", C.c_int), ("last_stop_step", C.c_int),
+        ("perf_first_packet_ms", C.c_double),
     ]
 
 
@@ -62,14 +64,16 @@ EXPORTS = [
     "qwen_tts_load", "qwen_tts_free", "qwen_tts_set_progress_callback", "qwen_tts_generate", "qwen_tts_write_wav",
     "qwen_tts_talker_prefill", "qwen_tts_talker_forward", "qwen_tts_subtalker_generate", "qwen_tts_codec_decode",
     "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
-    "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose",
+    "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
+    "qwen_tts_codec_stream_push",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
     "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
     "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
     "qtts_hip_transposed_conv1d", "qtts_hip_snake_beta", "qtts_hip_expf_glibc", "qtts_hip_sync",
-    "qtts_dev_profile_frame",
+    "qtts_dev_profile_frame", "qtts_dev_codec_stream_begin", "qtts_dev_codec_stream_push_slot",
+    "qtts_dev_codec_stream_push_host",
 ]
 
 _LIB = None
@@ -111,6 +115,11 @@ def lib():
     L.qwen_tts_set_progress_callback.argtypes = [C.POINTER(Ctx), PROGRESS_CB, C.c_void_p]
     L.qwen_tts_write_wav.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
     L.qwen_tts_abi_sizeof_ctx.restype = C.c_size_t
+    L.qwen_tts_generate_stream.restype = C.c_void_p
+    L.qwen_tts_generate_stream.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, AUDIO_CB,
+                                           C.c_void_p, _ip]
+    L.qwen_tts_codec_stream_begin.argtypes = [C.POINTER(Ctx), C.c_int]
+    L.qwen_tts_codec_stream_push.argtypes = [C.POINTER(Ctx), _ip, C.c_int, _fp]
     L.qtts_hip_device_count.restype = C.c_int
     vp = C.c_void_p
     L.qtts_hip_matvec_bf16.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
@@ -187,6 +196,36 @@ class QwenTTS:
         rc = lib().qwen_tts_generate_batch(self.ctx, nb, tx, sp, lg, out, ns)
         audio = [_take_audio(out[i], ns[i]) for i in range(nb)]
         return rc, audio
+
+    def generate_stream(self, ids, speaker=None, language=None, chunk_frames=4, on_chunk=None):
+        """Streaming generation; on_chunk(np.ndarray) gets each audio chunk as
+        it is decoded.  Returns the whole utterance."""
+        csv = ",".join(str(int(i)) for i in ids).encode()
+        n = C.c_int(0)
+
+        def _cb(p, k, u):
+            if on_chunk is not None:
+                on_chunk(np.ctypeslib.as_array(p, shape=(k,)).copy())
+        cb = AUDIO_CB(_cb)
+        p = lib().qwen_tts_generate_stream(self.ctx, csv, speaker.encode() if speaker else None,
+                                           language.encode() if language else None, int(chunk_frames), cb, None,
+                                           C.byref(n))
+        return _take_audio(p, n.value)
+
+    def codec_stream(self, chunks, max_frames=4096):
+        """Exact incremental codec decode of a list of [t, 16] code arrays."""
+        L = lib()
+        if L.qwen_tts_codec_stream_begin(self.ctx, int(max_frames)) != 0:
+            raise RuntimeError("codec stream begin failed")
+        outs = []
+        for c in chunks:
+            c = np.ascontiguousarray(c, np.int32)
+            o = np.zeros(c.shape[0] * 1920, np.float32)
+            k = L.qwen_tts_codec_stream_push(self.ctx, c.ctypes.data_as(_ip), c.shape[0], o.ctypes.data_as(_fp))
+            if k != len(o):
+                raise RuntimeError(f"codec stream push failed ({k})")
+            outs.append(o)
+        return outs
 
     def last_codes(self):
         G = self.cfg.num_code_groups

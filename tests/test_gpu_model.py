@@ -189,3 +189,65 @@ def test_unknown_speaker_warns_and_continues(tts_tiny):
     tts_tiny.set_params(max_tokens=4096, fixed=3, seed=1, **GREEDY)
     a = tts_tiny.generate(prompt_ids("short"), "nobody", "klingon")
     assert a is not None and len(a) == 3 * 1920
+
+
+# ---------------------------------------------------------------- streaming
+@pytest.mark.parametrize("T,chunks", [(50, [1, 3, 7, 16, 23]), (150, [1, 40, 16, 5, 88])])
+def test_codec_stream_equals_full_decode(tts_tiny, oracle, T, chunks):
+    """Incremental decode with carried state (conv histories, transposed-conv
+    tails, window-72 K/V) reproduces the full decode; T=150 crosses the
+    attention window."""
+    rng = np.random.default_rng(T)
+    codes = rng.integers(0, 2048, size=(T, 16)).astype(np.int32)
+    full = tts_tiny.codec_decode(codes)
+    parts, t = [], 0
+    for c in chunks:
+        parts.append(codes[t:t + c])
+        t += c
+    assert t == T
+    outs = tts_tiny.codec_stream(parts)
+    for p, o in zip(parts, outs):
+        assert len(o) == len(p) * 1920
+    s = np.concatenate(outs)
+    assert s.shape == full.shape
+    assert np.abs(s - full).max() < 1e-5, np.abs(s - full).max()
+    audio_close(s, oracle.codec_decode(codes))
+
+
+def test_generate_stream_equals_generate(tiny_dir):
+    m = qtts.QwenTTS(tiny_dir)
+    try:
+        m.set_params(max_tokens=4096, fixed=16, seed=42, **GREEDY)
+        full = m.generate(prompt_ids("short"), "aiden", "english")
+        chunks = []
+        s = m.generate_stream(prompt_ids("short"), "aiden", "english", chunk_frames=4, on_chunk=chunks.append)
+        assert [len(c) for c in chunks] == [1920, 4 * 1920, 4 * 1920, 4 * 1920, 3 * 1920]
+        np.testing.assert_array_equal(np.concatenate(chunks), s)
+        assert s.shape == full.shape and np.abs(s - full).max() < 1e-5
+        np.testing.assert_array_equal(m.last_codes(), E["greedy_codes"])
+        assert 0 < m.c.perf_first_packet_ms < m.c.perf_total_ms
+    finally:
+        m.close()
+
+
+def test_generate_stream_eos(tiny_eos_dir):
+    """Streaming in EOS mode stops with the reference's stop step and yields
+    the same audio as the non-streaming call."""
+    m = qtts.QwenTTS(tiny_eos_dir)
+    try:
+        _gen(m, "eosg")
+        full = m.generate(prompt_ids("short"), "aiden", "english")
+        s = m.generate_stream(prompt_ids("short"), "aiden", "english", chunk_frames=5)
+        np.testing.assert_array_equal(m.last_codes(), E["eosg_codes"])
+        assert s.shape == full.shape and np.abs(s - full).max() < 1e-5
+    finally:
+        m.close()
+
+
+def test_cli_stream_flag(tiny_dir):
+    ids = ",".join(str(i) for i in prompt_ids("short"))
+    with tempfile.TemporaryDirectory() as d:
+        r = subprocess.run([qtts.CLI_PATH, "-d", tiny_dir, "-t", ids, "-o", os.path.join(d, "o.wav"), "-v",
+                            "--fixed-codec-tokens", "8", "--stream", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert re.search(r"First packet: [\d.]+ ms", r.stderr)
