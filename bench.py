@@ -261,18 +261,18 @@ def main():
     value = audio_total / el_max
     ms_per_step = el_max / args.steps * 1e3
 
-    # ---- first packet: prefill + frame 0 + codec decode of frame 0 ----
+    # ---- first packet (BASELINE.json metric, configs[2]): streaming generation,
+    # wall time from the call to the first audio chunk (frame 0 decoded by the
+    # exact streaming codec and on the host) ----
     fp = None
     if args.batch == 1:
-        m.generate(prompts[0], "aiden", "english")
-        first_frame_ms = m.c.perf_first_frame_ms
-        codes = m.last_codes()
-        t1 = time.perf_counter()
-        a1 = m.codec_decode(codes[:1])
-        codec1_ms = (time.perf_counter() - t1) * 1e3
-        fp = dict(first_packet_ms=first_frame_ms + codec1_ms, first_frame_ms=first_frame_ms,
-                  first_codec_ms=codec1_ms, first_packet_samples=int(len(a1)),
-                  prefill_ms=m.c.perf_prefill_ms, talker_ms=m.c.perf_talker_ms, codec_ms=m.c.perf_codec_ms)
+        m.generate(prompts[0], "aiden", "english")       # non-streaming breakdown
+        prefill_ms, talker_ms, codec_ms = m.c.perf_prefill_ms, m.c.perf_talker_ms, m.c.perf_codec_ms
+        first = []
+        m.generate_stream(prompts[0], "aiden", "english", chunk_frames=8, on_chunk=first.append)
+        fp = dict(first_packet_ms=m.c.perf_first_packet_ms, first_frame_ms=m.c.perf_first_frame_ms,
+                  first_packet_samples=int(len(first[0])) if first else 0, stream_chunk_frames=8,
+                  prefill_ms=prefill_ms, talker_ms=talker_ms, codec_ms=codec_ms)
 
     roof = None if args.no_profile else profile_roofline(m, qtts.lib())
     m.close()
