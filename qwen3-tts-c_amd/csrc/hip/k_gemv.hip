@@ -35,26 +35,31 @@ template <int TAIL> struct TailA { int unused; };
 template <> struct TailA<1> { AttnArgs at; };
 template <> struct TailA<2> { SampArgs sa; int *cnt; };
 
+// Tail hand-off (cdna_hip_programming.md Guideline 16, R1 counter form): the
+// GEMV epilogue stores the rows the tail reads with write-through (sc1)
+// stores; every wave drains vmcnt, the workgroup barriers, lane 0 takes a
+// relaxed agent-scope ticket; the last arriver reads the rows with sc1 loads
+// (no release / acquire fences: a per-workgroup __threadfence() here cost
+// ~10x the kernel).  The last arriver resets the ticket (zeroed at alloc).
+
 // The last workgroup of the logit-head GEMV draws the token (qtts_sample_dev.h),
 // so sampling costs no kernel of its own.
 __device__ __forceinline__ void gemv_sample_tail(const SampArgs &sa, int *cnt, float *smem) {
     __shared__ int tail_last;
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tail_last = (old == (int)gridDim.x - 1);
     }
     __syncthreads();
     if (!tail_last) return;
-    __threadfence();
     if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     qtts_samp::sample_row<true>(sa, 0, reinterpret_cast<unsigned char *>(smem));
 }
 
 // The last workgroup to finish the q/k/v rows of a kv head runs that head's
-// attention (acq_rel agent-scope ticket per kv head, MI355X_MICROARCH.md
-// "Correctness boundaries"; the ticket is reset by its user).
+// attention (one ticket per kv head).
 __device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int RPW, float *smem) {
     __shared__ int tail_last;
     const int HD = t.HD, NH = t.NH, KV = t.KV, gph = NH / KV;
@@ -63,20 +68,19 @@ __device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int 
     else if (row0 < (NH + KV) * HD) kvg = (row0 - NH * HD) / HD;
     else kvg = (row0 - (NH + KV) * HD) / HD;
     const int need = (gph + 2) * HD / RPW;
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(t.cnt + kvg, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const int old = __hip_atomic_fetch_add(t.cnt + kvg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tail_last = (old == need - 1);
     }
     __syncthreads();
     if (!tail_last) return;
-    __threadfence();
     switch (HD) {
-        case 128: attn_full_wg<128, 2>(t, kvg, 0, smem); break;
-        case 64: attn_full_wg<64, 2>(t, kvg, 0, smem); break;
-        case 32: attn_full_wg<32, 2>(t, kvg, 0, smem); break;
-        default: attn_full_wg<16, 2>(t, kvg, 0, smem); break;
+        case 128: attn_full_wg<128, 2, true>(t, kvg, 0, smem); break;
+        case 64: attn_full_wg<64, 2, true>(t, kvg, 0, smem); break;
+        case 32: attn_full_wg<32, 2, true>(t, kvg, 0, smem); break;
+        default: attn_full_wg<16, 2, true>(t, kvg, 0, smem); break;
     }
     if (threadIdx.x == 0) __hip_atomic_store(t.cnt + kvg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -360,7 +364,10 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
             float v = red[tid];
             for (int k = 1; k < ksn; ++k) v += red[k * RPW + tid];
             switch (a.epi) {
-                case EPI_STORE: a.y[r] = v; break;
+                case EPI_STORE:
+                    if constexpr (TAIL != 0) st_sc1(a.y + r, v);   // handed to this launch's tail
+                    else a.y[r] = v;
+                    break;
                 case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
                 case EPI_BIAS_SILU: {
                     const float z = v + a.bias[r];

@@ -31,7 +31,9 @@ struct AttnWG {
                          ML = SC + GPH * CH, RED = ML + 8, POOL = RED + KG * NO;
 };
 
-template <int HD, int GPH>
+// SC1: the q/k/v row was written by other workgroups of this launch with
+// write-through stores; read it with sc1 loads (no acquire fence needed).
+template <int HD, int GPH, bool SC1>
 __device__ __forceinline__ void attn_full_wg(const AttnArgs &a, int kvh, int r, float *pool) {
     using W = AttnWG<HD, GPH>;
     constexpr int LPK = W::LPK, DPL = W::DPL, CH = W::CH, D4 = W::D4, KG = W::KG, NO = W::NO, NJ = W::NJ,
@@ -55,7 +57,7 @@ __device__ __forceinline__ void attn_full_wg(const AttnArgs &a, int kvh, int r, 
 #pragma unroll
         for (int j = 0; j < (HD + 63) / 64; ++j) {
             const int i = lane + 64 * j;
-            v[j] = i < HD ? src[i] : 0.f;
+            v[j] = i < HD ? (SC1 ? ld_sc1(src + i) : src[i]) : 0.f;
             ss += v[j] * v[j];
         }
         ss = wave_sum(ss);
@@ -66,7 +68,10 @@ __device__ __forceinline__ void attn_full_wg(const AttnArgs &a, int kvh, int r, 
             if (i < HD) xn[hh * HD + i] = v[j] * iv * nw[i];
         }
     }
-    if (tid < HD) vv[tid] = row[(a.NH + a.KV) * HD + kvh * HD + tid];
+    if (tid < HD) {
+        const float *vp = row + (a.NH + a.KV) * HD + kvh * HD + tid;
+        vv[tid] = SC1 ? ld_sc1(vp) : *vp;
+    }
     __syncthreads();
     {
         const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;

@@ -105,3 +105,14 @@ __device__ __forceinline__ float expf_glibc(float x) {
     y = y * s;
     return (float)y;
 }
+
+// Write-through ("sc1") 4-byte store / load at agent scope: the hand-off form
+// of cdna_hip_programming.md Guideline 16 R1 for data another workgroup of the
+// SAME launch consumes (no release fence; every storing wave drains vmcnt
+// before the ticket; the consumer reads with these loads, no acquire).
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

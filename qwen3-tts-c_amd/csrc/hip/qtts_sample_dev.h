@@ -376,7 +376,7 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     for (int j = 0; j < EMAX; ++j) {
         const int i = i0 + j;
         const bool ok = j < E && i < n;
-        x[j] = ok ? lg[i] : -INFINITY;
+        x[j] = ok ? (FAST_ONLY ? ld_sc1(lg + i) : lg[i]) : -INFINITY;   // FAST_ONLY = GEMV tail: sc1 hand-off
         cnt[j] = (ok && pen) ? a.counts[(size_t)b * n + i] : 0;
     }
     if (tid == 0) { U.fast.misc[1] = stopped; U.fast.misc[2] = ng; }
