@@ -114,7 +114,7 @@ struct qtts_dev {
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
     bool profiling = false;
-    bool fuse_attn = true;   // QTTS_HIP_NO_FUSE=1: separate attention kernels (A/B diagnostics)
+    bool fuse_attn = false;  // QTTS_HIP_FUSE=1: GEMV-tail fusions (attention, sampler)
     bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
@@ -310,8 +310,11 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     }
     dv->tl.resize(dims->L);
     dv->sl.resize(dims->Ls);
-    const char *nf = getenv("QTTS_HIP_NO_FUSE");
-    dv->fuse_attn = !(nf && atoi(nf));
+    // GEMV-tail fusions (attention into QKV, sampler into the logit head) are
+    // correct but measured slower than separate kernels on MI355X (the per-kv-
+    // head ticket serialises 64 cross-XCD atomics; profiles/r01g): opt-in.
+    const char *nf = getenv("QTTS_HIP_FUSE");
+    dv->fuse_attn = nf && atoi(nf);
     const char *nm = getenv("QTTS_HIP_NO_MFMA");
     dv->use_mfma = !(nm && atoi(nm));
     codec_init(&dv->codec, dims, dv->st);
