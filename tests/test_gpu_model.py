@@ -251,3 +251,17 @@ def test_cli_stream_flag(tiny_dir):
                             "--fixed-codec-tokens", "8", "--stream", "2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert re.search(r"First packet: [\d.]+ ms", r.stderr)
+
+
+def test_e2e_fused_tails_opt_in(tiny_dir, monkeypatch):
+    """The GEMV-tail fusions (QTTS_HIP_FUSE=1: attention in the QKV GEMV,
+    sampler in the logit head, sc1 hand-off) stay bit-exact."""
+    monkeypatch.setenv("QTTS_HIP_FUSE", "1")
+    m = qtts.QwenTTS(tiny_dir)
+    try:
+        for name in ("greedy", "sampled"):
+            a = _gen(m, name)
+            np.testing.assert_array_equal(m.last_codes(), E[f"{name}_codes"])
+            audio_close(a, E[f"{name}_audio"])
+    finally:
+        m.close()

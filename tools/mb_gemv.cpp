@@ -1,0 +1,85 @@
+// mb_gemv.cpp - GEMV configuration sweep (development tool): times the batch-1
+// weight-streaming GEMV (qtts_gemv) on the 1.7B decode shapes for each KSPLIT,
+// NT on/off, back-to-back launches captured in a HIP graph.
+//
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iqwen3-tts-c_amd/csrc/hip tools/mb_gemv.cpp \
+//         -Lqwen3-tts-c_amd/lib -lqwen_tts_amd -Wl,-rpath,$PWD/qwen3-tts-c_amd/lib -o tools/mb_gemv
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#include "qtts_kernels.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+int main() {
+    struct Shape { const char *name; int R, C, epi; bool norm; };
+    const Shape shapes[] = {
+        {"talker qkv 4096x2048", 4096, 2048, EPI_STORE, true},
+        {"talker o 2048x2048", 2048, 2048, EPI_RESID, false},
+        {"talker gate|up 12288x2048", 12288, 2048, EPI_SWIGLU, true},
+        {"talker down 2048x6144", 2048, 6144, EPI_RESID, false},
+        {"codec head 3072x2048", 3072, 2048, EPI_STORE, true},
+        {"sub qkv 4096x1024", 4096, 1024, EPI_STORE, true},
+        {"sub o 1024x2048", 1024, 2048, EPI_RESID, false},
+        {"sub gate|up 6144x1024", 6144, 1024, EPI_SWIGLU, true},
+        {"sub down 1024x3072", 1024, 3072, EPI_RESID, false},
+    };
+    const int NW = 24;   // distinct weight copies so the sweep streams from HBM, not the Infinity Cache
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (const Shape &s : shapes) {
+        const size_t wn = (size_t)s.R * s.C;
+        std::vector<bf16_t *> W(NW);
+        for (auto &w : W) {
+            CK(hipMalloc(&w, wn * 2));
+            CK(hipMemset(w, 0x3c, wn * 2));
+        }
+        float *x, *y, *nw;
+        CK(hipMalloc(&x, s.C * 4 * 2));
+        CK(hipMalloc(&y, (size_t)s.R * 4 * 2));
+        CK(hipMalloc(&nw, s.C * 4));
+        CK(hipMemset(x, 0, s.C * 8));
+        CK(hipMemset(y, 0, s.R * 8));
+        CK(hipMemset(nw, 0, s.C * 4));
+        for (int nt = 0; nt < 2; ++nt)
+            for (int ks = 1; ks <= 32; ks *= 2) {
+                if ((s.C / 64) % ks) continue;
+                if (s.epi == EPI_SWIGLU && ks > 4) continue;
+                GemvArgs a;
+                a.R = s.R; a.C = s.C; a.ksplit = ks; a.nt = nt; a.nb = 1; a.x = x; a.ldx = s.C; a.y = y;
+                a.ldy = s.R; a.epi = s.epi; a.norm_w = s.norm ? nw : nullptr;
+                hipGraph_t g;
+                hipGraphExec_t ge;
+                CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+                for (int i = 0; i < 96; ++i) {
+                    a.W = W[i % NW];
+                    if (qtts_gemv(a, st)) { printf("launch failed\n"); exit(1); }
+                }
+                CK(hipStreamEndCapture(st, &g));
+                CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+                CK(hipGraphLaunch(ge, st));
+                CK(hipStreamSynchronize(st));
+                CK(hipEventRecord(e0, st));
+                for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(ge, st));
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double us = ms * 1e3 / (5 * 96);
+                printf("%-28s ks=%2d nt=%d grid=%5d  %7.2f us  %6.0f GB/s\n", s.name, ks, nt, (s.R + 32 / ks - 1) / (32 / ks),
+                       us, wn * 2 / (us * 1e-6) / 1e9);
+                CK(hipGraphExecDestroy(ge));
+                CK(hipGraphDestroy(g));
+            }
+        for (auto &w : W) CK(hipFree(w));
+        CK(hipFree(x));
+        CK(hipFree(y));
+        CK(hipFree(nw));
+    }
+    return 0;
+}
