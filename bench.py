@@ -226,7 +226,8 @@ def main():
     import qtts
     from synth_model import prompt_ids
 
-    md = args.model_dir or f"/tmp/qtts_bench_{args.preset}"
+    # the same synthetic dir the GPU tests generate (tests/conftest.py model_dir): one 3.4 GB write per box
+    md = args.model_dir or os.path.join(os.environ.get("QTTS_TEST_MODELS", "/tmp/qtts_test_models"), args.preset)
     ensure_model_shared(md, args.preset, ws, local)
     t = time.time()
     m = qtts.QwenTTS(md, device=dev)

@@ -8,6 +8,8 @@
 //          - optional RMSNorm (c/qwen_tts_kernels.c:27-39) with the full-row
 //            statistics computed per workgroup
 //          - optional copy-out (raw or normalised) by workgroup 0
+//          - or (k_gemv1_att) the short-context decode attention of the token,
+//            computed from its q|k|v row (qtts_attn_pro.h)
 //   epilogue: store / +bias / +bias then SiLU / residual add (x += acc) /
 //             SwiGLU over interleaved gate|up row quads.
 //
@@ -23,6 +25,7 @@
 // CUs.  Weight loads for the first block group are issued before the prologue
 // so HBM latency overlaps the norm.  Accumulation is fp32 (exact bf16->f32).
 #include "qtts_attn_dev.h"
+#include "qtts_attn_pro.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 #include "qtts_sample_dev.h"
@@ -30,7 +33,7 @@
 namespace {
 
 // Optional tail work of the batch-1 GEMV (TAIL = 1: decode attention of the
-// kv head whose q/k/v rows this grid just produced).
+// kv head whose q/k/v rows this grid just produced; TAIL = 2: the sampler).
 template <int TAIL> struct TailA { int unused; };
 template <> struct TailA<1> { AttnArgs at; };
 template <> struct TailA<2> { SampArgs sa; int *cnt; };
@@ -41,27 +44,26 @@ template <> struct TailA<2> { SampArgs sa; int *cnt; };
 // relaxed agent-scope ticket; the last arriver reads the rows with sc1 loads
 // (no release / acquire fences: a per-workgroup __threadfence() here cost
 // ~10x the kernel).  The last arriver resets the ticket (zeroed at alloc).
+// `flag` is an LDS word of the DYNAMIC region (see k_gemv1).
 
 // The last workgroup of the logit-head GEMV draws the token (qtts_sample_dev.h),
 // so sampling costs no kernel of its own.
-__device__ __forceinline__ void gemv_sample_tail(const SampArgs &sa, int *cnt, float *smem) {
-    __shared__ int tail_last;
+__device__ __forceinline__ void gemv_sample_tail(const SampArgs &sa, int *cnt, int *flag, float *pool) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tail_last = (old == (int)gridDim.x - 1);
+        *flag = (old == (int)gridDim.x - 1);
     }
     __syncthreads();
-    if (!tail_last) return;
+    if (!*flag) return;
     if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    qtts_samp::sample_row<true>(sa, 0, reinterpret_cast<unsigned char *>(smem));
+    qtts_samp::sample_row<true>(sa, 0, reinterpret_cast<unsigned char *>(pool));
 }
 
 // The last workgroup to finish the q/k/v rows of a kv head runs that head's
 // attention (one ticket per kv head).
-__device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int RPW, float *smem) {
-    __shared__ int tail_last;
+__device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int RPW, int *flag, float *pool) {
     const int HD = t.HD, NH = t.NH, KV = t.KV, gph = NH / KV;
     int kvg;
     if (row0 < NH * HD) kvg = (row0 / HD) / gph;
@@ -72,15 +74,15 @@ __device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int 
     __syncthreads();
     if (threadIdx.x == 0) {
         const int old = __hip_atomic_fetch_add(t.cnt + kvg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tail_last = (old == need - 1);
+        *flag = (old == need - 1);
     }
     __syncthreads();
-    if (!tail_last) return;
+    if (!*flag) return;
     switch (HD) {
-        case 128: attn_full_wg<128, 2, true>(t, kvg, 0, smem); break;
-        case 64: attn_full_wg<64, 2, true>(t, kvg, 0, smem); break;
-        case 32: attn_full_wg<32, 2, true>(t, kvg, 0, smem); break;
-        default: attn_full_wg<16, 2, true>(t, kvg, 0, smem); break;
+        case 128: attn_full_wg<128, 2, true>(t, kvg, 0, pool); break;
+        case 64: attn_full_wg<64, 2, true>(t, kvg, 0, pool); break;
+        case 32: attn_full_wg<32, 2, true>(t, kvg, 0, pool); break;
+        default: attn_full_wg<16, 2, true>(t, kvg, 0, pool); break;
     }
     if (threadIdx.x == 0) __hip_atomic_store(t.cnt + kvg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -244,12 +246,114 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 
 
 // ---------------------------------------------------------------------------
+// Batch-1 weight stream shared by k_gemv1 and k_gemv1_att: the 8-lane slot of
+// row `row` streams its KSPLIT share of the row's 64-column blocks in groups of
+// U1 x 16 B per lane, double-buffered in registers (the first group is issued
+// by the caller before its prologue).
+template <int U1, bool NT>
+struct G1Stream {
+    const v4u *Wr;
+    int nblk, ng, ks, ksn, sub;
+    v4u wv[U1];
+    __device__ __forceinline__ G1Stream(const GemvArgs &a, int row, int ks_, int ksn_, int sub_)
+        : ks(ks_), ksn(ksn_), sub(sub_) {
+        const int rowc = row < a.R ? row : a.R - 1;
+        Wr = reinterpret_cast<const v4u *>(a.W + (size_t)rowc * a.C) + sub;
+        nblk = a.C / 64 / ksn;
+        ng = (nblk + U1 - 1) / U1;
+    }
+    __device__ __forceinline__ void load(int g) {
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+            int j = g * U1 + u;
+            j = j < nblk ? j : nblk - 1;   // clamp: loads stay unconditional
+            const v4u *p = Wr + ((64 * (ks + j * ksn)) >> 3);
+            if constexpr (NT) wv[u] = __builtin_nontemporal_load(p);
+            else wv[u] = *p;
+        }
+    }
+    // dot of this lane's share with xs (LDS), reduced over the slot's 8 lanes
+    __device__ __forceinline__ float run(const float *xs) {
+        float acc = 0.f;
+        for (int g = 0; g < ng; ++g) {
+            v4u cur[U1];
+#pragma unroll
+            for (int u = 0; u < U1; ++u) cur[u] = wv[u];
+            if (g + 1 < ng) load(g + 1);
+#pragma unroll
+            for (int u = 0; u < U1; ++u) {
+                const int j = g * U1 + u;
+                if (j < nblk) {
+                    float f[8];
+                    unpack8(cur[u], f);
+                    const int cl = 64 * (ks + j * ksn) + 8 * sub;
+                    const float4 x0 = *reinterpret_cast<const float4 *>(xs + cl);
+                    const float4 x1 = *reinterpret_cast<const float4 *>(xs + cl + 4);
+                    acc = fmaf(f[0], x0.x, acc); acc = fmaf(f[1], x0.y, acc);
+                    acc = fmaf(f[2], x0.z, acc); acc = fmaf(f[3], x0.w, acc);
+                    acc = fmaf(f[4], x1.x, acc); acc = fmaf(f[5], x1.y, acc);
+                    acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
+                }
+            }
+        }
+        acc += __shfl_xor(acc, 1, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        acc += __shfl_xor(acc, 4, 64);
+        return acc;
+    }
+};
+
+// Batch-1 epilogue: KSPLIT partials through LDS `red` [32], one barrier, then
+// one thread per output row applies the epilogue.  SC1: plain stores become
+// write-through (the rows are handed to a tail of the same launch).
+template <bool SC1>
+__device__ __forceinline__ void g1_epilogue(const GemvArgs &a, float acc, float *red, int row0, int RPW, int ksn,
+                                            int ks, int rloc, int sub) {
+    const int tid = threadIdx.x;
+    if (sub == 0) red[ks * RPW + rloc] = acc;
+    __syncthreads();
+    if (tid < RPW) {
+        const int r = row0 + tid;
+        if (r < a.R) {
+            float v = red[tid];
+            for (int k = 1; k < ksn; ++k) v += red[k * RPW + tid];
+            switch (a.epi) {
+                case EPI_STORE:
+                    if constexpr (SC1) st_sc1(a.y + r, v);
+                    else a.y[r] = v;
+                    break;
+                case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
+                case EPI_BIAS_SILU: {
+                    const float z = v + a.bias[r];
+                    a.y[r] = z / (1.0f + expf(-z));
+                    break;
+                }
+                case EPI_RESID: a.y[r] += v; break;
+                case EPI_SWIGLU:
+                    if ((r & 7) < 4) {
+                        float u = red[tid + 4];
+                        for (int k = 1; k < ksn; ++k) u += red[k * RPW + tid + 4];
+                        a.y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * u;
+                    }
+                    break;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Batch-1 decode path.  Same slot mapping; the prologue loads x once as float4
 // (XV per thread), reduces the RMS statistic with one barrier, writes the
 // normalised row to LDS (second barrier); weights for the first U blocks are
 // already in flight.  One barrier in the epilogue: each output thread sums
 // the KSPLIT partials it needs (for SwiGLU also its up row's) straight from
 // LDS.
+// Dynamic LDS: [flag: 4 words][xs: C][red: 32][bred: 4].  The tails' ticket
+// flag lives in the dynamic region on purpose: a static __shared__ is placed
+// in front of it and shifts every float4 LDS access off its 16-B alignment
+// (replayed at 64 cycles each, cdna_hip_programming.md Guideline 17).
+constexpr int G1_HEAD = 4;   // floats in front of xs
+
 template <int U1, int XV, bool NT, int TAIL>
 __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -257,26 +361,12 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
     const int ksn = a.ksplit, RPW = 32 / ksn;
     const int rloc = slot % RPW, ks = slot / RPW;
     const int row0 = blockIdx.x * RPW, row = row0 + rloc;
-    const int rowc = row < a.R ? row : a.R - 1;
     const int C = a.C;
-    float *xs = smem;          // [C]
-    float *red = xs + C;       // [32]
-    float *bred = red + 32;    // [4]
-    const v4u *Wr = reinterpret_cast<const v4u *>(a.W + (size_t)rowc * C) + sub;
-    const int nblk = C / 64 / ksn;
-    const int ng = (nblk + U1 - 1) / U1;
-    v4u wv[U1];
-    auto load_group = [&](int g) {
-#pragma unroll
-        for (int u = 0; u < U1; ++u) {
-            int j = g * U1 + u;
-            j = j < nblk ? j : nblk - 1;
-            const v4u *p = Wr + ((64 * (ks + j * ksn)) >> 3);
-            if constexpr (NT) wv[u] = __builtin_nontemporal_load(p);
-            else wv[u] = *p;
-        }
-    };
-    load_group(0);
+    float *xs = smem + G1_HEAD;   // [C]
+    float *red = xs + C;          // [32]
+    float *bred = red + 32;       // [4]
+    G1Stream<U1, NT> ws(a, row, ks, ksn, sub);
+    ws.load(0);
 
     // ---- prologue: x (fp32 row or gathered bf16 row) -> optional RMSNorm -> LDS
     const bf16_t *trow = nullptr;
@@ -330,63 +420,35 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
     }
     __syncthreads();
 
-    // ---- stream the weights ----
-    float acc = 0.f;
-    for (int g = 0; g < ng; ++g) {
-        v4u cur[U1];
-#pragma unroll
-        for (int u = 0; u < U1; ++u) cur[u] = wv[u];
-        if (g + 1 < ng) load_group(g + 1);
-#pragma unroll
-        for (int u = 0; u < U1; ++u) {
-            const int j = g * U1 + u;
-            if (j < nblk) {
-                float f[8];
-                unpack8(cur[u], f);
-                const int cl = 64 * (ks + j * ksn) + 8 * sub;
-                const float4 x0 = *reinterpret_cast<const float4 *>(xs + cl);
-                const float4 x1 = *reinterpret_cast<const float4 *>(xs + cl + 4);
-                acc = fmaf(f[0], x0.x, acc); acc = fmaf(f[1], x0.y, acc);
-                acc = fmaf(f[2], x0.z, acc); acc = fmaf(f[3], x0.w, acc);
-                acc = fmaf(f[4], x1.x, acc); acc = fmaf(f[5], x1.y, acc);
-                acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
-            }
-        }
-    }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    if (sub == 0) red[ks * RPW + rloc] = acc;
-    __syncthreads();
-    if (tid < RPW) {
-        const int r = row0 + tid;
-        if (r < a.R) {
-            float v = red[tid];
-            for (int k = 1; k < ksn; ++k) v += red[k * RPW + tid];
-            switch (a.epi) {
-                case EPI_STORE:
-                    if constexpr (TAIL != 0) st_sc1(a.y + r, v);   // handed to this launch's tail
-                    else a.y[r] = v;
-                    break;
-                case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
-                case EPI_BIAS_SILU: {
-                    const float z = v + a.bias[r];
-                    a.y[r] = z / (1.0f + expf(-z));
-                    break;
-                }
-                case EPI_RESID: a.y[r] += v; break;
-                case EPI_SWIGLU:
-                    if ((r & 7) < 4) {
-                        float u = red[tid + 4];
-                        for (int k = 1; k < ksn; ++k) u += red[k * RPW + tid + 4];
-                        a.y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * u;
-                    }
-                    break;
-            }
-        }
-    }
-    if constexpr (TAIL == 1) gemv_attn_tail(ta.at, row0, RPW, smem);
-    if constexpr (TAIL == 2) gemv_sample_tail(ta.sa, ta.cnt, smem);
+    // ---- stream the weights, then the epilogue (and the tail) ----
+    const float acc = ws.run(xs);
+    g1_epilogue<TAIL != 0>(a, acc, red, row0, RPW, ksn, ks, rloc, sub);
+    int *flag = reinterpret_cast<int *>(smem);
+    if constexpr (TAIL == 1) gemv_attn_tail(ta.at, row0, RPW, flag, smem + G1_HEAD);
+    if constexpr (TAIL == 2) gemv_sample_tail(ta.sa, ta.cnt, flag, smem + G1_HEAD);
+}
+
+// ---------------------------------------------------------------------------
+// Batch-1 O projection with the decode attention as its prologue
+// (qtts_attn_pro.h): x = attention(q|k|v row, K/V cache) computed in every
+// workgroup into LDS, then the weight stream and the epilogue of k_gemv1.
+// Dynamic LDS: [xs: C][red: 32][lq: (NH+2KV)*HD][sc: NH*ATT_NMAX].
+template <int U1, bool NT, int HD>
+__global__ __launch_bounds__(256) void k_gemv1_att(GemvArgs a, AttnArgs t) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
+    const int ksn = a.ksplit, RPW = 32 / ksn;
+    const int rloc = slot % RPW, ks = slot / RPW;
+    const int row0 = blockIdx.x * RPW, row = row0 + rloc;
+    float *xs = smem;                        // [C] attention output = this GEMV's input
+    float *red = xs + a.C;                   // [32]
+    float *lq = red + 32;                    // [(NH+2KV)*HD] rotated q|k, raw v
+    float *sc = lq + (t.NH + 2 * t.KV) * HD; // [NH][ATT_NMAX] scores / probabilities
+    G1Stream<U1, NT> ws(a, row, ks, ksn, sub);
+    ws.load(0);
+    att_prologue<HD>(t, xs, lq, sc, blockIdx.x == 0);
+    const float acc = ws.run(xs);
+    g1_epilogue<false>(a, acc, red, row0, RPW, ksn, ks, rloc, sub);
 }
 
 }  // namespace
@@ -418,7 +480,7 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         const int grid = (a.R + rpw - 1) / rpw;
         const int nblk = a.C / 64 / a.ksplit;
         const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
-        const size_t smem = (size_t)(a.C + 40) * sizeof(float);
+        const size_t smem = (size_t)(G1_HEAD + a.C + 36) * sizeof(float);
         const TailA<0> t0{0};
 #define QTTS_G1(U, X)                                                                                 \
         if (a.nt) {                                                                                   \
@@ -488,7 +550,7 @@ int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st) {
         case 32: pool = AttnWG<32, 2>::POOL; break;
         default: pool = AttnWG<16, 2>::POOL; break;
     }
-    const size_t smem = (size_t)(a.C + 40 > pool ? a.C + 40 : pool) * sizeof(float);
+    const size_t smem = (size_t)(G1_HEAD + (a.C + 36 > pool ? a.C + 36 : pool)) * sizeof(float);
     const TailA<1> ta{t};
 #define QTTS_GT(U, X)                                                                                 \
     if (a.nt) {                                                                                       \
@@ -518,8 +580,9 @@ int qtts_gemv_sample(GemvArgs a, const SampArgs &sa, int *cnt, hipStream_t st) {
     const int grid = (a.R + rpw - 1) / rpw;
     const int nblk = a.C / 64 / a.ksplit;
     const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
-    size_t smem = (size_t)(a.C + 40) * sizeof(float);
+    size_t smem = (size_t)(a.C + 36) * sizeof(float);
     if (smem < sizeof(qtts_samp::FastSmem)) smem = sizeof(qtts_samp::FastSmem);
+    smem += G1_HEAD * sizeof(float);
     TailA<2> ta;
     ta.sa = sa;
     ta.cnt = cnt;
@@ -539,5 +602,34 @@ int qtts_gemv_sample(GemvArgs a, const SampArgs &sa, int *cnt, hipStream_t st) {
                       case 4: QTTS_GS(4, 4) break; default: QTTS_GS(4, 8) break; }
     }
 #undef QTTS_GS
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// O-projection GEMV with the decode attention as its prologue (batch 1,
+// short context: the sub-talker).  `target_wg` sizes the grid: every
+// workgroup recomputes the attention, so fewer, fuller workgroups trade
+// weight-stream parallelism for less redundant K/V traffic.  Returns 1 when
+// not covered (the caller launches attention + GEMV), 0 ok, -1 error.
+int qtts_gemv_att(GemvArgs a, const AttnArgs &t, int target_wg, hipStream_t st) {
+    if (!(a.nb == 1 && a.C <= 8192 && a.C % 64 == 0 && a.epi != EPI_SWIGLU && att_pro_ok(t, a.C))) return 1;
+    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, target_wg > 0 ? target_wg : 256);
+    const int rpw = 32 / a.ksplit;
+    const int grid = (a.R + rpw - 1) / rpw;
+    const int nblk = a.C / 64 / a.ksplit;
+    const size_t smem = (size_t)(a.C + 32 + att_pro_lds_floats(t.NH, t.KV, t.HD)) * sizeof(float);
+#define QTTS_GA(U, H)                                                                                 \
+    if (a.nt) {                                                                                       \
+        hipLaunchKernelGGL((k_gemv1_att<U, true, H>), dim3(grid), dim3(256), smem, st, a, t);         \
+        qtts_last_kernel = "k_gemv1_att<" #U ", true, " #H ">";                                       \
+    } else {                                                                                          \
+        hipLaunchKernelGGL((k_gemv1_att<U, false, H>), dim3(grid), dim3(256), smem, st, a, t);        \
+        qtts_last_kernel = "k_gemv1_att<" #U ", false, " #H ">";                                      \
+    }
+#define QTTS_GA_HD(U)                                                                                 \
+    switch (t.HD) { case 128: QTTS_GA(U, 128) break; case 64: QTTS_GA(U, 64) break;                   \
+                    case 32: QTTS_GA(U, 32) break; default: QTTS_GA(U, 16) break; }
+    if (nblk >= 8) { QTTS_GA_HD(8) } else { QTTS_GA_HD(4) }
+#undef QTTS_GA_HD
+#undef QTTS_GA
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

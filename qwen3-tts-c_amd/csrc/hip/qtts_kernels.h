@@ -66,6 +66,9 @@ struct AttnArgs {
 };
 int qtts_attn_keys_per_split(int HD);
 int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st);
+// O projection with the short-context decode attention as its prologue
+// (qtts_attn_pro.h); 1 = not covered
+int qtts_gemv_att(GemvArgs a, const AttnArgs &t, int target_wg, hipStream_t st);
 
 // Name of the kernel instantiation the last launcher on this thread chose
 // (diagnostics: per-kernel profile rows match rocprofv3's kernel names).

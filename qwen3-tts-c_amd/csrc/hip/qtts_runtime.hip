@@ -26,6 +26,7 @@
 #include <string>
 #include <vector>
 
+#include "qtts_attn_pro.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 #include "qtts_codec.h"
@@ -116,6 +117,8 @@ struct qtts_dev {
     bool profiling = false;
     bool fuse_attn = false;  // QTTS_HIP_FUSE=1: GEMV-tail fusions (attention, sampler)
     bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
+    bool att_pro = true;     // QTTS_HIP_ATT_PRO=0: sub-talker attention as a kernel of its own
+    int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
@@ -317,6 +320,10 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->fuse_attn = nf && atoi(nf);
     const char *nm = getenv("QTTS_HIP_NO_MFMA");
     dv->use_mfma = !(nm && atoi(nm));
+    const char *ap = getenv("QTTS_HIP_ATT_PRO");
+    dv->att_pro = !(ap && !atoi(ap));
+    const char *aw = getenv("QTTS_HIP_ATT_PRO_WG");
+    if (aw && atoi(aw) > 0) dv->att_pro_wg = atoi(aw);
     codec_init(&dv->codec, dims, dv->st);
     return dv;
 }
@@ -505,8 +512,10 @@ struct ProfScope {  // brackets one launch with events when profiling is on
     ProfScope(qtts_dev *d, int kind, double bytes) : dv(d), idx((size_t)-1) {
         if (!dv->profiling) return;
         qtts_dev::Prof p{kind, bytes, nullptr, nullptr, ""};
-        hipEventCreate(&p.a);
-        hipEventCreate(&p.b);
+        // no system-scope fence per event: a default event's cache write-back /
+        // invalidate would be timed as part of every short kernel
+        hipEventCreateWithFlags(&p.a, hipEventDisableSystemFence);
+        hipEventCreateWithFlags(&p.b, hipEventDisableSystemFence);
         hipEventRecord(p.a, dv->st);
         dv->prof.push_back(p);
         idx = dv->prof.size() - 1;
@@ -530,6 +539,12 @@ static double gemv_bytes(const GemvArgs &a) {
 static int pgemv(qtts_dev *dv, const GemvArgs &a, int kind) {
     ProfScope ps(dv, kind, gemv_bytes(a));
     return qtts_gemv(a, dv->st);
+}
+// O projection with the sub-talker attention as its prologue (k_gemv.hip):
+// algorithmic bytes add the K / V rows of the live positions once.
+static int pgemv_att(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
+    ProfScope ps(dv, kind, gemv_bytes(a) + 2.0 * (t.pos_const + 1) * t.KV * t.HD * 4);
+    return qtts_gemv_att(a, t, dv->att_pro_wg, dv->st) == 0 ? 0 : -1;
 }
 // Multi-row projection over `rows` activation rows (prefill, text
 // projection): the matrix-core kernel in chunks of 64 rows, else the GEMV in
@@ -685,10 +700,16 @@ static int subtalker(qtts_dev *dv) {
             t.pos = nullptr; t.pos_const = g; t.NH = d.NHs; t.KV = d.KVs; t.HD = d.HDs; t.out = dv->att_s;
             t.ld_out = AD; t.nrows = nb; t.skip = dv->stopped;
             t.cnt = dv->att_cnt;
-            CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
-            a = gv(ly.wo, d.Hs, AD, dv->att_s, AD, dv->x_st, d.Hs, nb, EPI_RESID);
-            a.nt = 0;
-            CKI(pgemv(dv, a, PK_GEMV_SUB));
+            GemvArgs o = gv(ly.wo, d.Hs, AD, dv->att_s, AD, dv->x_st, d.Hs, nb, EPI_RESID);
+            o.nt = 0;
+            if (dv->att_pro && nb == 1 && att_pro_ok(t, AD)) {
+                // q|k|v rows, then attention (as the prologue) + O projection + residual
+                CKI(pgemv(dv, a, PK_GEMV_SUB));
+                CKI(pgemv_att(dv, o, t, PK_GEMV_SUB));
+            } else {
+                CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
+                CKI(pgemv(dv, o, PK_GEMV_SUB));
+            }
             a = gv(ly.wgu, 2 * d.Is, d.Hs, dv->x_st, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
             CKI(pgemv(dv, a, PK_GEMV_SUB));

@@ -253,6 +253,23 @@ def test_cli_stream_flag(tiny_dir):
     assert re.search(r"First packet: [\d.]+ ms", r.stderr)
 
 
+@pytest.mark.parametrize("env", [{"QTTS_HIP_ATT_PRO": "0"}, {"QTTS_HIP_ATT_PRO_WG": "16"}])
+def test_e2e_subtalker_attention_variants(tiny_dir, monkeypatch, env):
+    """The sub-talker attention as its own kernel (QTTS_HIP_ATT_PRO=0) and the
+    attention-prologue O GEMV on a different grid both stay bit-exact (the
+    default path is covered by test_e2e_codes_bit_exact_and_audio)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m = qtts.QwenTTS(tiny_dir)
+    try:
+        for name in ("greedy", "sampled"):
+            a = _gen(m, name)
+            np.testing.assert_array_equal(m.last_codes(), E[f"{name}_codes"])
+            audio_close(a, E[f"{name}_audio"])
+    finally:
+        m.close()
+
+
 def test_e2e_fused_tails_opt_in(tiny_dir, monkeypatch):
     """The GEMV-tail fusions (QTTS_HIP_FUSE=1: attention in the QKV GEMV,
     sampler in the logit head, sc1 hand-off) stay bit-exact."""

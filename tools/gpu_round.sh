@@ -16,9 +16,17 @@ if [ "$MODE" = dist ]; then
     --no-profile > $O/dist2.json 2> $O/dist2.err
   echo done; exit 0
 fi
+if [ "$MODE" = mb ] || [ "$MODE" = all+mb ]; then
+  # micro-benchmarks built in-tree on the CPU side (tools/mb_*)
+  timeout -k 10 120 tools/mb_l2 > $O/mb_l2.txt 2>&1
+  timeout -k 10 120 tools/mb_barrier > $O/mb_barrier.txt 2>&1
+  timeout -k 10 300 tools/mb_gemv > $O/mb_gemv.txt 2>&1
+  [ "$MODE" = mb ] && { echo done; exit 0; }
+  MODE=all
+fi
 if [ "$MODE" = all ]; then
 rc=0
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/gpu_tests.log 2>&1 || rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || rc=$?
 # 1 = some test failed (keep measuring); anything else (timeout, abort, crash) ends the call
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc"; exit $rc; fi
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
