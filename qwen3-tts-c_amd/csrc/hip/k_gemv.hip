@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                     const bf16_t *t = a.table + (size_t)src_row_id(b) * C;
                     for (int c = tid; c < C; c += 256) { float v = bf2f(t[c]); ss += v * v; }
                 } else {
-                    const float *xr = a.x + (size_t)b * a.ldx;
+                    const float *xr = a.table_f32 ? a.table_f32 + (size_t)src_row_id(b) * C : a.x + (size_t)b * a.ldx;
                     for (int c = tid; c < C; c += 256) { float v = xr[c]; ss += v * v; }
                 }
             }
@@ -159,6 +159,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             float v = 0.0f;
             if (b < nb) {
                 if (a.table) v = bf2f(a.table[(size_t)src_row_id(b) * C + cg]);
+                else if (a.table_f32) v = a.table_f32[(size_t)src_row_id(b) * C + cg];
                 else v = a.x[(size_t)b * a.ldx + cg];
                 if (a.xcopy && blockIdx.x == 0 && !a.xcopy_normed) a.xcopy[(size_t)b * a.ldxc + cg] = v;
                 if (a.norm_w) v = v * inv[b] * a.norm_w[cg];
@@ -370,10 +371,13 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
 
     // ---- prologue: x (fp32 row or gathered bf16 row) -> optional RMSNorm -> LDS
     const bf16_t *trow = nullptr;
-    if (a.table) {
+    const float *xrow = a.x;
+    if (a.table || a.table_f32) {
         const int *p = a.ids + a.ids_off;
         if (a.row_sel) p += (size_t)a.row_sel[0] * a.ids_rstride;
-        trow = a.table + (size_t)(*p) * C;
+        const size_t off = (size_t)(*p) * C;
+        if (a.table) trow = a.table + off;
+        else xrow = a.table_f32 + off;
     }
     float4 xv[XV], wn[XV];
     float ss = 0.f;
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
             v = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
                             __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
         } else {
-            v = *reinterpret_cast<const float4 *>(a.x + cc);
+            v = *reinterpret_cast<const float4 *>(xrow + cc);
         }
         if (c >= C) v = make_float4(0.f, 0.f, 0.f, 0.f);
         xv[i] = v;

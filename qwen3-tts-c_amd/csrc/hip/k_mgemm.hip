@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
 // receives the per-row 1/rms when a.norm_w is set.  Returns 1 when the shape
 // is not covered (caller uses qtts_gemv), 0 ok, -1 error.
 int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st) {
-    if (a.nb < 2 || a.nb > 64 || a.C % 32 || a.R % 16 || a.xcopy || (a.norm_w && !inv_scratch) ||
+    if (a.nb < 2 || a.nb > 64 || a.C % 32 || a.R % 16 || a.xcopy || a.table_f32 || (a.norm_w && !inv_scratch) ||
         (a.table && a.norm_w) || (!a.table && (a.ldx % 4 || ((uintptr_t)a.x & 15))) || (a.C % 8))
         return 1;
     if (a.norm_w) hipLaunchKernelGGL(k_row_rms, dim3(a.nb), dim3(256), 0, st, a.x, a.ldx, a.C, a.eps, inv_scratch);

@@ -14,10 +14,11 @@ struct GemvArgs {
     int cch = 0;                // set by launcher
     int nt = 1;                 // non-temporal weight loads
     int nb = 1;                 // batch rows
-    // x source: fp32 rows, or bf16 table rows gathered by id
+    // x source: fp32 rows, or bf16 / fp32 table rows gathered by id
     const float *x = nullptr;
     int ldx = 0;
-    const bf16_t *table = nullptr;  // [*, C]
+    const bf16_t *table = nullptr;      // [*, C]
+    const float *table_f32 = nullptr;   // [*, C] (precomputed projected embeddings)
     const int *ids = nullptr;       // id(b) = ids[b*ids_bstride + row_sel[b]*ids_rstride + ids_off]
     int ids_bstride = 1, ids_rstride = 0, ids_off = 0;
     const int *row_sel = nullptr;
@@ -34,7 +35,10 @@ struct GemvArgs {
     int epi = EPI_STORE;
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {
-        return table ? (C % 4 == 0) : (((uintptr_t)x & 15) == 0 && (!norm_w || ((uintptr_t)norm_w & 15) == 0));
+        if (table) return C % 4 == 0;
+        const bool nw_ok = !norm_w || ((uintptr_t)norm_w & 15) == 0;
+        if (table_f32) return C % 4 == 0 && ((uintptr_t)table_f32 & 15) == 0 && nw_ok;
+        return ((uintptr_t)x & 15) == 0 && nw_ok;
     }
 };
 int qtts_gemv(const GemvArgs &a, hipStream_t st);

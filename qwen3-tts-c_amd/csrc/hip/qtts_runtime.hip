@@ -84,6 +84,10 @@ struct qtts_dev {
     // sub-talker
     bf16_t *st_emb = nullptr, *lm = nullptr, *st_proj = nullptr;
     float *st_projb = nullptr, *st_norm = nullptr;
+    // small_to_mtp_projection applied once at load to every embedding row a
+    // sub-talker pass g >= 1 can consume (fp32): [V][Hs] of the talker codec
+    // embedding (pass 1) and [G-1][Vs][Hs] of the sub-talker ones (passes 2..)
+    float *codec_ptab = nullptr, *st_ptab = nullptr;
     // codec
     CodecModel codec;
     // rope
@@ -363,6 +367,8 @@ static int build_rope(qtts_dev *dv, int npos, int hd, float theta, float **cs, f
     return 0;
 }
 
+static int build_proj_tables(qtts_dev *dv);
+
 extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
     const qtts_dims_t &d = dv->d;
     hipSetDevice(dv->device);
@@ -396,6 +402,8 @@ extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
         fprintf(stderr, "Error: vocab > 4096 unsupported by the device sampler\n");
         return -1;
     }
+    const char *pt = getenv("QTTS_HIP_PTAB");
+    if (dv->st_proj && !(pt && !atoi(pt))) CKI(build_proj_tables(dv));
     return codec_finalize(&dv->codec);
 }
 
@@ -571,6 +579,35 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
     return 0;
 }
 
+// ST_PROJECT_INPUT (T.c:693-702) of every embedding row a pass g >= 1 can
+// read, once at load: the per-frame input projection GEMV of those passes
+// becomes a row gather (the row a pass needs is fixed by the code id alone).
+static int build_proj_tables(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    const int nid = d.V > d.Vs ? d.V : d.Vs;
+    std::vector<int> io(nid);
+    for (int i = 0; i < nid; ++i) io[i] = i;
+    int *ids = (int *)dalloc(dv, (size_t)nid * 4, false);
+    dv->codec_ptab = (float *)dalloc(dv, (size_t)d.V * d.Hs * 4, true);
+    dv->st_ptab = (float *)dalloc(dv, (size_t)(d.G - 1) * d.Vs * d.Hs * 4, true);
+    if (!ids || !dv->codec_ptab || !dv->st_ptab) return -1;
+    CK(hipMemcpy(ids, io.data(), (size_t)nid * 4, hipMemcpyHostToDevice));
+    GemvArgs a;
+    a.W = dv->st_proj; a.R = d.Hs; a.C = d.H; a.y = dv->codec_ptab; a.ldy = d.Hs;
+    a.epi = dv->st_projb ? EPI_BIAS : EPI_STORE;
+    a.bias = dv->st_projb;
+    a.nt = 0;
+    a.table = dv->codec_emb; a.ids = ids; a.ids_bstride = 1;
+    CKI(rows_proj(dv, a, d.V));
+    for (int g = 0; g < d.G - 1; ++g) {
+        a.table = dv->st_emb + (size_t)g * d.Vs * d.H;
+        a.y = dv->st_ptab + (size_t)g * d.Vs * d.Hs;
+        CKI(rows_proj(dv, a, d.Vs));
+    }
+    CK(hipStreamSynchronize(dv->st));
+    return 0;
+}
+
 // QKV projection + decode attention: one fused kernel at batch 1 (the
 // attention runs as the GEMV's tail, k_gemv.hip), else two launches.
 static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
@@ -671,17 +708,21 @@ static int subtalker(qtts_dev *dv) {
         // input source for this pass
         GemvArgs src;  // x / table description only
         src.nb = nb;
+        // passes >= 1 of a projecting model gather their already-projected row
+        const bool ptab = proj && g >= 1 && dv->st_ptab;
         if (g == 0) { src.x = dv->tk_hid; src.ldx = d.H; }
         else {
-            src.table = g == 1 ? dv->codec_emb : dv->st_emb + (size_t)(g - 2) * d.Vs * d.H;
+            if (ptab) src.table_f32 = g == 1 ? dv->codec_ptab : dv->st_ptab + (size_t)(g - 2) * d.Vs * d.Hs;
+            else src.table = g == 1 ? dv->codec_emb : dv->st_emb + (size_t)(g - 2) * d.Vs * d.H;
             src.ids = dv->codes; src.ids_bstride = cstride; src.row_sel = dv->cur_row; src.ids_rstride = d.G;
             src.ids_off = g - 1;
         }
         auto set_src = [&](GemvArgs &a) {
-            a.x = src.x; a.ldx = src.ldx; a.table = src.table; a.ids = src.ids; a.ids_bstride = src.ids_bstride;
-            a.row_sel = src.row_sel; a.ids_rstride = src.ids_rstride; a.ids_off = src.ids_off;
+            a.x = src.x; a.ldx = src.ldx; a.table = src.table; a.table_f32 = src.table_f32; a.ids = src.ids;
+            a.ids_bstride = src.ids_bstride; a.row_sel = src.row_sel; a.ids_rstride = src.ids_rstride;
+            a.ids_off = src.ids_off;
         };
-        if (proj) {  // ST_PROJECT_INPUT (T.c:693-702)
+        if (proj && !ptab) {  // ST_PROJECT_INPUT (T.c:693-702)
             GemvArgs a = gv(dv->st_proj, d.Hs, d.H, nullptr, 0, dv->x_st, d.Hs, nb, dv->st_projb ? EPI_BIAS : EPI_STORE);
             set_src(a);
             a.bias = dv->st_projb;
@@ -692,7 +733,7 @@ static int subtalker(qtts_dev *dv) {
             Layer &ly = dv->sl[l];
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, dv->x_st, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
-            if (l == 0 && !proj) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
+            if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             AttnArgs t;
             t.mode = 0; t.qkv = dv->qkv_s; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
             t.rope_cos = dv->rope_cos_s; t.rope_sin = dv->rope_sin_s;

@@ -253,7 +253,7 @@ def test_cli_stream_flag(tiny_dir):
     assert re.search(r"First packet: [\d.]+ ms", r.stderr)
 
 
-@pytest.mark.parametrize("env", [{"QTTS_HIP_ATT_PRO": "0"}, {"QTTS_HIP_ATT_PRO_WG": "16"}])
+@pytest.mark.parametrize("env", [{"QTTS_HIP_ATT_PRO": "0"}, {"QTTS_HIP_ATT_PRO_WG": "16"}, {"QTTS_HIP_PTAB": "0"}])
 def test_e2e_subtalker_attention_variants(tiny_dir, monkeypatch, env):
     """The sub-talker attention as its own kernel (QTTS_HIP_ATT_PRO=0) and the
     attention-prologue O GEMV on a different grid both stay bit-exact (the
