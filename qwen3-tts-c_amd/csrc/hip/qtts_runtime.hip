@@ -121,7 +121,8 @@ struct qtts_dev {
     bool profiling = false;
     bool fuse_attn = false;  // QTTS_HIP_FUSE=1: GEMV-tail fusions (attention, sampler)
     bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
-    bool att_pro = true;     // QTTS_HIP_ATT_PRO=0: sub-talker attention as a kernel of its own
+    bool att_pro = false;    // QTTS_HIP_ATT_PRO=1: sub-talker attention as the O GEMV's prologue
+                             // (measured slower: profiles/r01d_envsweep.txt)
     int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
@@ -325,7 +326,7 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     const char *nm = getenv("QTTS_HIP_NO_MFMA");
     dv->use_mfma = !(nm && atoi(nm));
     const char *ap = getenv("QTTS_HIP_ATT_PRO");
-    dv->att_pro = !(ap && !atoi(ap));
+    dv->att_pro = ap && atoi(ap);
     const char *aw = getenv("QTTS_HIP_ATT_PRO_WG");
     if (aw && atoi(aw) > 0) dv->att_pro_wg = atoi(aw);
     codec_init(&dv->codec, dims, dv->st);

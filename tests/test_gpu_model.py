@@ -253,11 +253,13 @@ def test_cli_stream_flag(tiny_dir):
     assert re.search(r"First packet: [\d.]+ ms", r.stderr)
 
 
-@pytest.mark.parametrize("env", [{"QTTS_HIP_ATT_PRO": "0"}, {"QTTS_HIP_ATT_PRO_WG": "16"}, {"QTTS_HIP_PTAB": "0"}])
+@pytest.mark.parametrize("env", [{"QTTS_HIP_ATT_PRO": "1"}, {"QTTS_HIP_ATT_PRO": "1", "QTTS_HIP_ATT_PRO_WG": "16"},
+                                 {"QTTS_HIP_PTAB": "0"}, {"QTTS_HIP_NO_SHORT_ATTN": "1"}])
 def test_e2e_subtalker_attention_variants(tiny_dir, monkeypatch, env):
-    """The sub-talker attention as its own kernel (QTTS_HIP_ATT_PRO=0) and the
-    attention-prologue O GEMV on a different grid both stay bit-exact (the
-    default path is covered by test_e2e_codes_bit_exact_and_audio)."""
+    """Alternative sub-talker paths stay bit-exact: attention as the O GEMV's
+    prologue (opt-in, two grids), the per-pass input projection instead of the
+    projected tables, the split-K decode attention instead of k_attn_short
+    (the default path is covered by test_e2e_codes_bit_exact_and_audio)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     m = qtts.QwenTTS(tiny_dir)
