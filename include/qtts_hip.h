@@ -112,6 +112,16 @@ int qtts_dev_codec_stream_begin(qtts_dev_t *dev, int max_frames);
 int qtts_dev_codec_stream_push_slot(qtts_dev_t *dev, int b, int frame0, int T, float *host_out);
 int qtts_dev_codec_stream_push_host(qtts_dev_t *dev, const int *codes, int T, float *host_out);
 
+/* The same exact streaming decode overlapped with the decode loop: it runs on
+ * a second (low-priority) HIP stream; push orders itself after the frames
+ * already enqueued on the context stream (an event), decodes slot b's frames
+ * [frame0, frame0 + T) into a device waveform and returns at once; end copies
+ * `frames` * 1920 samples to host_out and waits.  Replaces the codec call
+ * after the loop in qwen_tts_generate (Q.c:1376-1383) for one utterance. */
+int qtts_dev_codec_async_begin(qtts_dev_t *dev, int max_frames);
+int qtts_dev_codec_async_push(qtts_dev_t *dev, int b, int frame0, int T);
+int qtts_dev_codec_async_end(qtts_dev_t *dev, float *host_out, int frames);
+
 /* ---- host-pointer stage wrappers (oracle-level tests, c/qwen_tts.h:483-502) ---- */
 int qtts_dev_talker_prefill_host(qtts_dev_t *dev, const float *embeds, int n, float *hidden_out);
 int qtts_dev_talker_forward_host(qtts_dev_t *dev, const float *embed, float *logits, float *hidden_out);

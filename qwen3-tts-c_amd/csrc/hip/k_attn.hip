@@ -15,6 +15,7 @@
 // Scores: HD/8 lanes per key (two float4 loads each) -> 256/(HD/8) keys per
 // pass; P.V: HD/4 lanes per row -> 256/(HD/4) rows per pass, partial sums
 // combined through LDS in a fixed order.
+#include "qtts_attn_dev.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 
@@ -411,126 +412,11 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     if (tid == 0) __hip_atomic_store(a.cnt + r * a.KV + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---------------------------------------------------------------------------
-// Short-context decode attention: n = pos + 1 <= 16 keys (the sub-talker,
-// whose KV restarts every frame, T.c:562-569; ST_FORWARD T.c:646-671), one
-// workgroup per (kv head, row) serving its GQA pair of query heads.  At this
-// size the kernel is bound by its own instruction stream and memory round
-// trips, so every load is issued up front and each thread does one piece:
-//   threads < 4*HD/4  one float4 of q0 | q1 | k | v: per-head RMSNorm over
-//                     HD/4-lane shuffles, rotate-half RoPE (partner HD/8
-//                     lanes away) -> LDS; k / v of the token -> cache
-//   all               scores: HD/16 lanes per (query head, key)
-//   wave 0            softmax over the keys of each head (16-lane shuffles),
-//                     x * (1/sum) as kernel_softmax (K.c:371-378)
-//   threads < 2*HD    P.V: one output each, keys in order (st_axpy order)
 template <int HD>
 __global__ __launch_bounds__(256) void k_attn_short(AttnArgs a) {
-    constexpr int D4 = HD / 4, LPK = HD / 16, NK = 16;
     __shared__ __attribute__((aligned(16))) float lq[4 * HD];   // rotated q0 | q1 | k, raw v
-    __shared__ float sc[2][NK];
-    const int tid = threadIdx.x;
-    const int kvh = blockIdx.x, r = blockIdx.y;
-    const int KVD = a.KV * HD;
-    const int p = a.pos ? a.pos[r] : a.pos_const, n = p + 1;
-    const float *row = a.qkv + (size_t)r * a.ld_qkv;
-    const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
-    const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
-    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    // ---- every load first: the token's q0|q1|k|v, K rows for the scores, V columns for P.V
-    const int seg = tid / D4, l = tid - seg * D4;     // seg 0, 1: query heads, 2: k, 3: v
-    float4 x = zero4;
-    if (seg < 4) {
-        const float *src = seg < 2 ? row + (2 * kvh + seg) * HD
-                                   : row + (seg == 2 ? a.NH * HD : (a.NH + a.KV) * HD) + kvh * HD;
-        x = reinterpret_cast<const float4 *>(src)[l];
-    }
-    const int dI = tid / LPK, sub = tid - dI * LPK, gs = dI / NK, ts = dI - gs * NK;
-    const bool kld = gs < 2 && ts < p;
-    float4 kr[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        kr[c] = kld ? reinterpret_cast<const float4 *>(Kc + (size_t)ts * KVD + 16 * sub)[c] : zero4;
-    const int go = tid / HD, dd = tid - go * HD;
-    float vr[NK];
-#pragma unroll
-    for (int t = 0; t < NK; ++t) vr[t] = (go < 2 && t < p) ? Vc[(size_t)t * KVD + dd] : 0.f;
-
-    // ---- per-head RMSNorm (T.c:646-649) + RoPE (T.c:650-653) -> LDS; k, v -> cache (T.c:654-655)
-    float ss = x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
-#pragma unroll
-    for (int o = D4 / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
-    if (seg < 3) {
-        const float iv = rms_inv(ss, HD, a.eps);
-        const float4 w = reinterpret_cast<const float4 *>(seg < 2 ? a.qn_w : a.kn_w)[l];
-        x.x = x.x * iv * w.x; x.y = x.y * iv * w.y; x.z = x.z * iv * w.z; x.w = x.w * iv * w.w;
-    }
-    float4 o4;
-    o4.x = __shfl_xor(x.x, D4 / 2, 64); o4.y = __shfl_xor(x.y, D4 / 2, 64);
-    o4.z = __shfl_xor(x.z, D4 / 2, 64); o4.w = __shfl_xor(x.w, D4 / 2, 64);
-    if (seg < 4) {
-        float4 y = x;
-        if (seg < 3) {
-            const float4 c4 = reinterpret_cast<const float4 *>(a.rope_cos + (size_t)p * HD)[l];
-            const float4 s4 = reinterpret_cast<const float4 *>(a.rope_sin + (size_t)p * HD)[l];
-            if (l < D4 / 2) {   // x[i] c[i] - x[i+half] s[i]
-                y.x = x.x * c4.x - o4.x * s4.x; y.y = x.y * c4.y - o4.y * s4.y;
-                y.z = x.z * c4.z - o4.z * s4.z; y.w = x.w * c4.w - o4.w * s4.w;
-            } else {            // x[i+half] c[i] + x[i] s[i]
-                y.x = x.x * c4.x + o4.x * s4.x; y.y = x.y * c4.y + o4.y * s4.y;
-                y.z = x.z * c4.z + o4.z * s4.z; y.w = x.w * c4.w + o4.w * s4.w;
-            }
-        }
-        reinterpret_cast<float4 *>(lq)[tid] = y;
-        if (seg >= 2 && !(a.skip && a.skip[r])) {
-            float *dst = (seg == 2 ? a.kc : a.vc) + ((size_t)r * a.S + p) * KVD + kvh * HD;
-            reinterpret_cast<float4 *>(dst)[l] = y;
-        }
-    }
-    __syncthreads();
-
-    // ---- scores q.k_t / sqrt(HD) (T.c:662-665)
-    {
-        float d = 0.f;
-        if (gs < 2 && ts < n) {
-            const float4 *q4 = reinterpret_cast<const float4 *>(lq + gs * HD + 16 * sub);
-            const float4 *k4 = reinterpret_cast<const float4 *>(lq + 2 * HD + 16 * sub);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 k = ts == p ? k4[c] : kr[c], q = q4[c];
-                d += q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
-            }
-        }
-#pragma unroll
-        for (int o = LPK / 2; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (sub == 0 && gs < 2) sc[gs][ts] = ts < n ? d * div_rn(1.0f, sqrt_rn((float)HD)) : -INFINITY;
-    }
-    __syncthreads();
-
-    // ---- softmax per head over its <= 16 keys
-    if (tid < 2 * NK) {
-        const int g = tid / NK, t = tid - g * NK;
-        const float s = sc[g][t];
-        float m = s;
-#pragma unroll
-        for (int o = NK / 2; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        const float e = t < n ? expf(s - m) : 0.f;
-        float sum = e;
-#pragma unroll
-        for (int o = NK / 2; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
-        sc[g][t] = e * div_rn(1.0f, sum);
-    }
-    __syncthreads();
-
-    // ---- P.V, keys in order (T.c:667-671)
-    if (go < 2) {
-        float acc = 0.f;
-#pragma unroll
-        for (int t = 0; t < NK; ++t)
-            if (t < n) acc += sc[go][t] * (t == p ? lq[3 * HD + dd] : vr[t]);
-        a.out[(size_t)r * a.ld_out + (2 * kvh + go) * HD + dd] = acc;
-    }
+    __shared__ float sc[2 * 16];
+    attn_short_wg<HD, false>(a, blockIdx.x, blockIdx.y, lq, sc);
 }
 
 }  // namespace

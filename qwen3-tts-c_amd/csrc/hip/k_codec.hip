@@ -917,6 +917,18 @@ void codec_stream_free(CodecModel *m) {
 
 int codec_stream_begin(CodecModel *m, int max_frames) {
     const qtts_dims_t &d = m->d;
+    CodecStream &S0 = m->cs;
+    if (S0.active && max_frames + S0.tc <= S0.rope_cap) {
+        // reuse the buffers: only the carried state restarts (zero histories =
+        // the causal left padding, no K/V rows, position 0), on the codec stream
+        for (size_t i = 0; i < S0.hist.size(); ++i)
+            if (hipMemsetAsync(S0.hist[i], 0, (size_t)S0.hist_c[i] * (S0.hist_h[i] > 0 ? S0.hist_h[i] : 1) * 4,
+                               m->st) != hipSuccess)
+                return -1;
+        S0.pos0 = 0;
+        S0.hl = 0;
+        return 0;
+    }
     codec_stream_free(m);
     if (ensure_codec_state(m, 1)) return -1;   // split-K workspace
     CodecStream &S = m->cs;
@@ -997,6 +1009,10 @@ int codec_stream_begin(CodecModel *m, int max_frames) {
 }
 
 int codec_stream_push(CodecModel *m, const int *codes, int ldc_codes, int Ttot, float *host_out) {
+    return codec_stream_push_to(m, codes, ldc_codes, Ttot, host_out, true);
+}
+
+int codec_stream_push_to(CodecModel *m, const int *codes, int ldc_codes, int Ttot, float *out, bool host) {
     CodecStream &S = m->cs;
     const qtts_dims_t &d = m->d;
     if (!S.active || ldc_codes != d.cq) return -1;
@@ -1079,10 +1095,12 @@ int codec_stream_push(CodecModel *m, const int *codes, int ldc_codes, int Ttot, 
         KCK(sconv(m, slot, voc, ld, C, L, "decoder.decoder.6.conv.weight", "decoder.decoder.6.conv.bias", 1, 7, 1, wav,
                   ld, XE_BIAS_M, cw(m, "decoder.decoder.5.alpha"), cw(m, "decoder.decoder.5.beta"), nullptr));
         hipLaunchKernelGGL(k_clamp, dim3((L + 255) / 256), dim3(256), 0, st, wav, L);
-        if (hipMemcpyAsync(host_out + written, wav, (size_t)L * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+        if (hipMemcpyAsync(out + written, wav, (size_t)L * 4, host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice,
+                           st) != hipSuccess)
+            return -1;
         written += L;
         S.pos0 += T;
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return -1;
+    if (host && hipStreamSynchronize(st) != hipSuccess) return -1;
     return written;
 }

@@ -78,6 +78,16 @@ __device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int 
     }
     __syncthreads();
     if (!*flag) return;
+    if (t.S <= 16) {   // short context (the sub-talker): the lean single-workgroup body
+        switch (HD) {
+            case 128: attn_short_wg<128, true>(t, kvg, 0, pool, pool + 4 * 128); break;
+            case 64: attn_short_wg<64, true>(t, kvg, 0, pool, pool + 4 * 64); break;
+            case 32: attn_short_wg<32, true>(t, kvg, 0, pool, pool + 4 * 32); break;
+            default: attn_short_wg<16, true>(t, kvg, 0, pool, pool + 4 * 16); break;
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(t.cnt + kvg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     switch (HD) {
         case 128: attn_full_wg<128, 2, true>(t, kvg, 0, pool); break;
         case 64: attn_full_wg<64, 2, true>(t, kvg, 0, pool); break;

@@ -72,6 +72,9 @@ float *codec_decode(CodecModel *m, const int *codes_dev, int T, int *out_samples
 // ints) and writes T * 1920 samples to host_out.  Returns samples or -1.
 int codec_stream_begin(CodecModel *m, int max_frames);
 int codec_stream_push(CodecModel *m, const int *codes_dev, int ldc, int T, float *host_out);
+// the same into `out` (host memory, synchronous; or device memory: enqueued on
+// m->st only, nothing waited for)
+int codec_stream_push_to(CodecModel *m, const int *codes_dev, int ldc, int T, float *out, bool host);
 void codec_stream_free(CodecModel *m);
 
 // ---- generic fp32 implicit GEMM (exported for the kernel-level C-ABI) ----

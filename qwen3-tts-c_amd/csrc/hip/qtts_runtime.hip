@@ -115,11 +115,18 @@ struct qtts_dev {
     bool have_par = false;
     hipGraphExec_t g0 = nullptr, gN = nullptr;
     int graph_key = -1;
+    // codec overlapped with the decode (qtts_dev_codec_async_*): its own stream,
+    // ordered after the frames it decodes by an event; output stays on device
+    hipStream_t cst = nullptr;
+    hipEvent_t cev = nullptr;
+    float *cwav = nullptr;
+    size_t cwav_cap = 0;
     // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
     bool profiling = false;
-    bool fuse_attn = false;  // QTTS_HIP_FUSE=1: GEMV-tail fusions (attention, sampler)
+    bool fuse_attn = false;  // QTTS_HIP_FUSE=1: GEMV-tail fusions (talker attention, samplers)
+    bool fuse_st = false;    // QTTS_HIP_FUSE_ST=1: sub-talker attention as the QKV GEMV's tail
     bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
     bool att_pro = false;    // QTTS_HIP_ATT_PRO=1: sub-talker attention as the O GEMV's prologue
                              // (measured slower: profiles/r01d_envsweep.txt)
@@ -323,6 +330,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     // head ticket serialises 64 cross-XCD atomics; profiles/r01g): opt-in.
     const char *nf = getenv("QTTS_HIP_FUSE");
     dv->fuse_attn = nf && atoi(nf);
+    const char *ns = getenv("QTTS_HIP_FUSE_ST");
+    dv->fuse_st = ns && atoi(ns);
     const char *nm = getenv("QTTS_HIP_NO_MFMA");
     dv->use_mfma = !(nm && atoi(nm));
     const char *ap = getenv("QTTS_HIP_ATT_PRO");
@@ -339,6 +348,10 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
     hipStreamSynchronize(dv->st);
     free_state(dv);
     codec_destroy(&dv->codec);
+    if (dv->cst) hipStreamSynchronize(dv->cst);
+    if (dv->cwav) hipFree(dv->cwav);
+    if (dv->cev) hipEventDestroy(dv->cev);
+    if (dv->cst) hipStreamDestroy(dv->cst);
     for (void *p : dv->wallocs) hipFree(p);
     hipStreamDestroy(dv->st);
     delete dv;
@@ -612,7 +625,7 @@ static int build_proj_tables(qtts_dev *dv) {
 // QKV projection + decode attention: one fused kernel at batch 1 (the
 // attention runs as the GEMV's tail, k_gemv.hip), else two launches.
 static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
-    if (dv->nrun == 1 && dv->fuse_attn) {
+    if (dv->nrun == 1 && (t.S <= 16 ? dv->fuse_st : dv->fuse_attn)) {
         int rc;
         {
             ProfScope ps(dv, kind, gemv_bytes(a));
@@ -1020,6 +1033,58 @@ extern "C" int qtts_dev_codec_stream_push_host(qtts_dev_t *dv, const int *codes,
         r = codec_stream_push(&dv->codec, dc, dv->d.cq, T, host_out);
     hipFree(dc);
     return r;
+}
+
+// ----------------------------------------------------------------- codec overlapped with the decode
+// The exact streaming decode (codec_stream_*), run on a second stream while
+// the frame graphs continue on the context stream: each push waits (event)
+// for the frames already enqueued, decodes them into a device waveform, and
+// nothing is waited for on the host until qtts_dev_codec_async_end.
+extern "C" int qtts_dev_codec_async_begin(qtts_dev_t *dv, int max_frames) {
+    if (!dv || max_frames < 1) return -1;
+    hipSetDevice(dv->device);
+    if (!dv->cst) {
+        int lo = 0, hi = 0;
+        CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
+        CK(hipEventCreateWithFlags(&dv->cev, hipEventDisableTiming));
+    }
+    const size_t need = (size_t)max_frames * 1920;
+    if (need > dv->cwav_cap) {
+        CK(hipStreamSynchronize(dv->cst));
+        if (dv->cwav) CK(hipFree(dv->cwav));
+        dv->cwav = nullptr;
+        CK(hipMalloc(&dv->cwav, need * 4));
+        dv->cwav_cap = need;
+    }
+    CK(hipStreamSynchronize(dv->st));   // the stream state is shared with the synchronous paths
+    dv->codec.st = dv->cst;
+    const int rc = codec_stream_begin(&dv->codec, max_frames);
+    dv->codec.st = dv->st;
+    return rc;
+}
+
+extern "C" int qtts_dev_codec_async_push(qtts_dev_t *dv, int b, int frame0, int T) {
+    if (!dv || !dv->cst || b < 0 || b >= dv->nb || T < 1 || frame0 < 0 || frame0 + T > dv->max_frames + 1 ||
+        (size_t)(frame0 + T) * 1920 > dv->cwav_cap)
+        return -1;
+    hipSetDevice(dv->device);
+    CK(hipEventRecord(dv->cev, dv->st));
+    CK(hipStreamWaitEvent(dv->cst, dv->cev, 0));
+    const int *codes = dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G + (size_t)frame0 * dv->d.G;
+    dv->codec.st = dv->cst;
+    const int n = codec_stream_push_to(&dv->codec, codes, dv->d.G, T, dv->cwav + (size_t)frame0 * 1920, false);
+    dv->codec.st = dv->st;
+    return n;
+}
+
+extern "C" int qtts_dev_codec_async_end(qtts_dev_t *dv, float *host_out, int frames) {
+    if (!dv || !dv->cst || frames < 0 || (size_t)frames * 1920 > dv->cwav_cap) return -1;
+    hipSetDevice(dv->device);
+    if (frames > 0)
+        CK(hipMemcpyAsync(host_out, dv->cwav, (size_t)frames * 1920 * 4, hipMemcpyDeviceToHost, dv->cst));
+    CK(hipStreamSynchronize(dv->cst));
+    return frames * 1920;
 }
 
 // ----------------------------------------------------------------- host-pointer stage wrappers
