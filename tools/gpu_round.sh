@@ -1,10 +1,12 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, the bench line, rocprofv3 kernel stats of the
-# same bench command, and a separate FETCH_SIZE / WRITE_SIZE PMC pass.
-# Usage (via gpurun): bash tools/gpu_round.sh <tag>
+# One GPU-box pass: parity tests, rocprofv3 kernel stats of the bench command,
+# separate FETCH_SIZE / WRITE_SIZE PMC passes, then the bench line itself --
+# after the summaries are in the box's profiles/ so the line's
+# roofline.rocprof_avg_us / traffic come from the same code.
+# Usage (via gpurun): bash tools/gpu_round.sh <tag> [all|all+mb|mb|prof|dist]
 set -eo pipefail
 TAG=${1:-r01}
-MODE=${2:-all}   # all | prof (skip tests and the plain bench run) | dist (2-rank gloo rehearsal only)
+MODE=${2:-all}   # all | all+mb (micro-benchmarks first) | mb | prof (no tests) | dist (2-rank gloo rehearsal)
 R=$GRAFT_REPO_ROOT
 [ -z "$R" ] && R=$(pwd)
 O=$R/gpurun_out/$TAG
@@ -25,15 +27,19 @@ if [ "$MODE" = mb ] || [ "$MODE" = all+mb ]; then
   MODE=all
 fi
 if [ "$MODE" = all ]; then
-rc=0
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || rc=$?
-# 1 = some test failed (keep measuring); anything else (timeout, abort, crash) ends the call
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc"; exit $rc; fi
-timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+  rc=0
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || rc=$?
+  # 1 = some test failed (keep measuring); anything else (timeout, abort, crash) ends the call
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc"; exit $rc; fi
 fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch.log 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $O/pmc_write -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_write.log 2>&1
 python3 $R/tools/prof_summary.py $O
+# the bench reads the newest profiles/*kernel_stats.csv / *pmc.json
+cp $O/kernel_stats.csv $R/profiles/${TAG}_kernel_stats.csv
+cp $O/pmc.json $R/profiles/${TAG}_pmc.json
+cd $R
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
 echo done
