@@ -26,13 +26,17 @@ int main() {
         {"sub gate|up 6144x1024", 6144, 1024, EPI_SWIGLU, true},
         {"sub down 1024x3072", 1024, 3072, EPI_RESID, false},
     };
-    const int NW = 24;   // distinct weight copies so the sweep streams from HBM, not the Infinity Cache
+    // distinct weight copies: 24 = the sweep streams from HBM; MB_NW=1 = the
+    // weights stay resident in the Infinity Cache across replays
+    const int NW = getenv("MB_NW") ? atoi(getenv("MB_NW")) : 24;
+    const bool talker_only = getenv("MB_TALKER") != nullptr;
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (const Shape &s : shapes) {
+        if (talker_only && s.name[0] != 't') continue;
         const size_t wn = (size_t)s.R * s.C;
         std::vector<bf16_t *> W(NW);
         for (auto &w : W) {
