@@ -1,12 +1,16 @@
 // k_sample.hip - the sampler as a kernel of its own: one workgroup per batch
-// row (the device code and its derivation are in qtts_sample_dev.h).
+// row (the device code and its derivation are in qtts_sample_dev.h).  The
+// register fast path (top_p >= 1, 0 < top_k < n) gets instantiations of its
+// own, sized by the ids per thread (EM = ceil(n / 256) rounded up to 8 or 16),
+// so a draw neither carries the full path's code nor iterates unused slots.
 #include "qtts_sample_dev.h"
 
 namespace {
 
+template <bool FAST, int EM>
 __global__ __launch_bounds__(256) void k_sample(SampArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    qtts_samp::sample_row<false>(a, blockIdx.x, smraw);
+    qtts_samp::sample_row<FAST, EM>(a, blockIdx.x, smraw);
 }
 
 }  // namespace
@@ -16,7 +20,18 @@ int qtts_sample(const SampArgs &a, hipStream_t st) {
         fprintf(stderr, "qtts_sample: vocab %d unsupported (max %d)\n", a.n, qtts_samp::NMAX);
         return -1;
     }
-    hipLaunchKernelGGL(k_sample, dim3(a.nb), dim3(256), sizeof(qtts_samp::KSmem), st, a);
-    qtts_last_kernel = "k_sample";
+    if (qtts_samp::fast_path(a)) {
+        const size_t sm = sizeof(qtts_samp::FastSmem);
+        if (a.n <= 8 * 256) {
+            hipLaunchKernelGGL((k_sample<true, 8>), dim3(a.nb), dim3(256), sm, st, a);
+            qtts_last_kernel = "k_sample<true, 8>";
+        } else {
+            hipLaunchKernelGGL((k_sample<true, 16>), dim3(a.nb), dim3(256), sm, st, a);
+            qtts_last_kernel = "k_sample<true, 16>";
+        }
+    } else {
+        hipLaunchKernelGGL((k_sample<false, qtts_samp::EMAX>), dim3(a.nb), dim3(256), sizeof(qtts_samp::KSmem), st, a);
+        qtts_last_kernel = "k_sample<false, 16>";
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

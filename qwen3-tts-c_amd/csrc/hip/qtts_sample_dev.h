@@ -185,7 +185,8 @@ struct FastSmem {
 // holds the k-th key fits entirely.  Returns T (threshold key prefix, low
 // bits 0 after an early exit), take_eq = how many keys == T to take in index
 // order when the select ran to the last digit; ne = number of eligible keys.
-__device__ __forceinline__ void radix_select_regs(FastSmem &fs, const uint32_t (&kk)[EMAX], int E, int k, uint32_t &T,
+template <int EM>
+__device__ __forceinline__ void radix_select_regs(FastSmem &fs, const uint32_t (&kk)[EM], int E, int k, uint32_t &T,
                                   uint32_t &Tmask, int &take_eq, int &ne) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #pragma unroll
@@ -197,7 +198,7 @@ __device__ __forceinline__ void radix_select_regs(FastSmem &fs, const uint32_t (
     for (int shift = 24; shift >= 0; shift -= 8, par ^= 1) {
         int *h = fs.hist[par][w];
 #pragma unroll
-        for (int j = 0; j < EMAX; ++j)
+        for (int j = 0; j < EM; ++j)
             if (j < E && kk[j] != 0u && (kk[j] & mask) == prefix) atomicAdd(&h[(kk[j] >> shift) & 255u], 1);
         __syncthreads();
         // every wave scans the merged histogram from the top (same result in all waves)
@@ -267,22 +268,93 @@ __device__ __forceinline__ void block_scan2(FastSmem &fs, int x, int y, int &ex,
     ey = e >> 16;
 }
 
+// Wave 0, ke <= 64 selected (sel_v / sel_i in index order).  Lane j ranks its
+// (value desc, index asc) key -- the order the reference's strict '>'
+// insertion list leaves (K.c:436-449) -- against all ke keys read back from
+// LDS by broadcast (8 loads in flight per step), scatters itself to
+// top_*[rank]; then p_j = expf(v_j - v_0), the sum in j order, r = u * sum
+// and the first j whose running sum reaches r (K.c:451-477), every lane
+// walking the same broadcast values.  Lane 0 owns the RNG.  Returns the id
+// (all lanes).  (v_readlane per step measured 2-3x slower than the LDS reads.)
+__device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rng) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    unsigned long long *keys = reinterpret_cast<unsigned long long *>(fs.top_v);   // 64 x 8 B scratch
+    float vj = 0.f;
+    int ij = 0;
+    unsigned long long key = 0ull;
+    if (lane < ke) {
+        vj = fs.sel_v[lane];
+        ij = fs.sel_i[lane];
+        key = ((unsigned long long)okey(vj) << 32) | (0xFFFFFFFFu - (uint32_t)ij);
+    }
+    keys[lane] = key;   // lanes >= ke: 0, below every real key
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: LDS is in order once the writes landed
+    int rank = 0;
+    for (int t0 = 0; t0 < ke; t0 += 8) {
+        unsigned long long kt[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kt[u] = keys[t0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += kt[u] > key;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float *pv = fs.sel_v;   // reused: [rank] -> p_rank, indices in top_i
+    if (lane < ke) fs.top_i[rank] = ij;
+    float e = 0.f;
+    if (lane < ke) pv[rank] = vj;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float v0 = pv[0];
+    if (lane < ke) e = expf_glibc(pv[lane] - v0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < ke) pv[lane] = e;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float sum = 0.f;
+    for (int j0 = 0; j0 < ke; j0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = pv[j0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (j0 + u < ke) sum += p[u];
+    }
+    if (!(sum > 0.0f)) return fs.top_i[0];
+    float r = 0.f;
+    if (lane == 0) r = rand_uniform(rng) * sum;
+    r = __shfl(r, 0, 64);
+    float c = 0.f;
+    for (int j0 = 0; j0 < ke; j0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = pv[j0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (j0 + u < ke) {
+                c += p[u];
+                if (c >= r) return fs.top_i[j0 + u];
+            }
+        }
+    }
+    return 0;
+}
+
 // Returns the sampled id (all threads).  v[]: logits / temperature.
-__device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[EMAX], int E, int n, int k, uint32_t &rng) {
+template <int EM>
+__device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[EM], int E, int n, int k, uint32_t &rng) {
 #pragma clang fp contract(off)
     const int tid = threadIdx.x;
-    uint32_t kk[EMAX];
+    uint32_t kk[EM];
 #pragma unroll
-    for (int j = 0; j < EMAX; ++j) kk[j] = (j < E && tid * E + j < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
+    for (int j = 0; j < EM; ++j) kk[j] = (j < E && tid * E + j < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
     uint32_t T, Tm;
     int take_eq, ne;
-    radix_select_regs(fs, kk, E, k, T, Tm, take_eq, ne);
+    radix_select_regs<EM>(fs, kk, E, k, T, Tm, take_eq, ne);
     const int ke = k < ne ? k : ne;
     if (ke == 0) return 0;                       // nothing eligible: the reference returns 0
     // taken: (key & Tm) > T, or == T for the first take_eq of those in index order
     int ngt = 0, neq = 0;
 #pragma unroll
-    for (int j = 0; j < EMAX; ++j) {
+    for (int j = 0; j < EM; ++j) {
         if (j < E && kk[j] != 0u) {
             const uint32_t m = kk[j] & Tm;
             ngt += m > T;
@@ -294,7 +366,7 @@ __device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[E
     int pos = gt0 + min(eq0, take_eq);
     int eqc = eq0;
 #pragma unroll
-    for (int j = 0; j < EMAX; ++j) {
+    for (int j = 0; j < EM; ++j) {
         if (j < E && kk[j] != 0u) {
             const uint32_t m = kk[j] & Tm;
             bool take = m > T;
@@ -303,6 +375,16 @@ __device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[E
         }
     }
     __syncthreads();
+    if (ke <= 64) {   // the common case (top-k 50): one wave sorts and draws
+        if (tid < 64) {
+            const int t = wave_sort_draw(fs, ke, rng);
+            if (tid == 0) fs.misc[0] = t;
+        }
+        __syncthreads();
+        const int out = fs.misc[0];
+        __syncthreads();   // fs is reused by a second draw (fixed-mode EOS re-sample)
+        return out;
+    }
     // exact rank among the ke selected (value desc, index asc); sel_* is in index order
     for (int s2 = tid; s2 < ke; s2 += 256) {
         const float vs = fs.sel_v[s2];
@@ -353,7 +435,7 @@ __host__ __device__ inline bool fast_path(const SampArgs &a) {
 // One row's draw (all 256 threads of the workgroup).  `smraw` >= sizeof(KSmem),
 // or sizeof(FastSmem) with FAST_ONLY (the caller guarantees fast_path(a)).
 // Used by k_sample and, FAST_ONLY, as the tail of the logit-head GEMV.
-template <bool FAST_ONLY>
+template <bool FAST_ONLY, int EM = EMAX>
 __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned char *smraw) {
 #pragma clang fp contract(off)
     KSmem &U = *reinterpret_cast<KSmem *>(smraw);
@@ -369,11 +451,11 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     const int E = (n + 255) / 256;
     const float *lg = a.logits + (size_t)b * a.ld;
     const int i0 = tid * E;
-    float x[EMAX];
-    int cnt[EMAX];
+    float x[EM];
+    int cnt[EM];
     const bool pen = a.mode == 1 && a.rep != 1.0f && a.counts;
 #pragma unroll
-    for (int j = 0; j < EMAX; ++j) {
+    for (int j = 0; j < EM; ++j) {
         const int i = i0 + j;
         const bool ok = j < E && i < n;
         x[j] = ok ? (FAST_ONLY ? ld_sc1(lg + i) : lg[i]) : -INFINITY;   // FAST_ONLY = GEMV tail: sc1 hand-off
@@ -386,7 +468,7 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     __syncthreads();
     if (a.mode == 1) {
 #pragma unroll
-        for (int j = 0; j < EMAX; ++j) {
+        for (int j = 0; j < EM; ++j) {
             const int i = i0 + j;
             float v = x[j];
             if (i >= a.suppress_lo && i != a.eos) v = -1e9f;
@@ -399,20 +481,20 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     const bool fast = FAST_ONLY || fast_path(a);
     int tok = 0;
     if (fast) {
-        float v[EMAX];
+        float v[EM];
 #pragma unroll
-        for (int j = 0; j < EMAX; ++j) v[j] = div_rn(x[j], temp);
-        tok = sample_fast_regs(U.fast, v, E, n, a.top_k, rng);
+        for (int j = 0; j < EM; ++j) v[j] = div_rn(x[j], temp);
+        tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng);
         if (a.mode == 1 && a.fixed > 0 && tok == a.eos && ng < a.fixed) {   // Q.c:1315-1321
 #pragma unroll
-            for (int j = 0; j < EMAX; ++j)
+            for (int j = 0; j < EM; ++j)
                 if (i0 + j == a.eos) v[j] = div_rn(-1e9f, temp);
-            tok = sample_fast_regs(U.fast, v, E, n, a.top_k, rng);
+            tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng);
         }
     } else if constexpr (!FAST_ONLY) {
         SampSmem &sm = U.full;
 #pragma unroll
-        for (int j = 0; j < EMAX; ++j)
+        for (int j = 0; j < EM; ++j)
             if (j < E && i0 + j < n) sm.lg[i0 + j] = x[j];
         __syncthreads();
         tok = sample_any(sm, n, a.top_k, a.top_p, a.temp, rng);

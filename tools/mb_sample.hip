@@ -1,0 +1,98 @@
+// mb_sample.hip - micro-benchmark (development tool): where the on-device
+// sampler's time goes.  Times 200 back-to-back launches (one HIP graph) of
+// kernels that stop after successive phases of the fast path on the same
+// 2048-logit row (sub-talker shape, top-k 50, T 0.9):
+//   0 empty kernel            (launch floor)
+//   1 logits loaded            (+ a store of their sum)
+//   2 + radix select           (k-th largest key)
+//   3 + selection, rank, draw  (= the full fast path, qtts_sample_dev.h)
+//
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iqwen3-tts-c_amd/csrc/hip tools/mb_sample.hip -o tools/mb_sample
+#include "qtts_sample_dev.h"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+using namespace qtts_samp;
+
+template <int PHASE>
+__global__ __launch_bounds__(256) void k_phase(SampArgs a, float *sink) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    FastSmem &fs = *reinterpret_cast<FastSmem *>(smraw);
+    const int tid = threadIdx.x;
+    if constexpr (PHASE == 0) {
+        if (tid == 0) sink[0] = 1.f;
+        return;
+    }
+    constexpr int EM = 8;
+    const int n = a.n, E = (n + 255) / 256;
+    float v[EM];
+#pragma unroll
+    for (int j = 0; j < EM; ++j) v[j] = (j < E && tid * E + j < n) ? div_rn(ld_sc1(a.logits + tid * E + j), a.temp) : -INFINITY;
+    if constexpr (PHASE == 1) {
+        float s = 0.f;
+        for (int j = 0; j < EM; ++j) s += v[j];
+        if (s == 12345.f) sink[0] = s;
+        return;
+    }
+    if constexpr (PHASE == 2) {
+        uint32_t kk[EM];
+#pragma unroll
+        for (int j = 0; j < EM; ++j) kk[j] = (j < E && tid * E + j < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
+        uint32_t T, Tm;
+        int take_eq, ne;
+        radix_select_regs<EM>(fs, kk, E, a.top_k, T, Tm, take_eq, ne);
+        if (tid == 0) sink[0] = (float)T + take_eq + ne;
+        return;
+    }
+    uint32_t rng = 0x42280000u;
+    const int t = sample_fast_regs<EM>(fs, v, E, n, a.top_k, rng);
+    if (tid == 0) sink[0] = (float)t;
+}
+
+template <int PHASE>
+static float time_phase(const SampArgs &a, float *sink, hipStream_t st) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+    for (int i = 0; i < 200; ++i)
+        hipLaunchKernelGGL((k_phase<PHASE>), dim3(1), dim3(256), sizeof(FastSmem), st, a, sink);
+    CK(hipStreamEndCapture(st, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipStreamSynchronize(st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, st));
+    for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(ge, st));
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    return ms * 1e3f / 1000.f;
+}
+
+int main() {
+    const int n = 2048;
+    float *lg, *sink;
+    CK(hipMalloc(&lg, n * 4));
+    CK(hipMalloc(&sink, 64));
+    float h[n];
+    unsigned s = 12345;
+    for (int i = 0; i < n; ++i) {   // logits ~ a few units wide, like a sampled head
+        s = s * 1664525u + 1013904223u;
+        h[i] = ((s >> 8) / 16777216.0f - 0.5f) * 8.0f;
+    }
+    CK(hipMemcpy(lg, h, n * 4, hipMemcpyHostToDevice));
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    SampArgs a;
+    a.logits = lg; a.ld = n; a.n = n; a.nb = 1; a.top_k = 50; a.top_p = 1.f; a.temp = 0.9f;
+    printf("phase 0 empty kernel        %6.2f us\n", time_phase<0>(a, sink, st));
+    printf("phase 1 + logits loaded     %6.2f us\n", time_phase<1>(a, sink, st));
+    printf("phase 2 + radix select      %6.2f us\n", time_phase<2>(a, sink, st));
+    printf("phase 3 + select/rank/draw  %6.2f us\n", time_phase<3>(a, sink, st));
+    return 0;
+}
