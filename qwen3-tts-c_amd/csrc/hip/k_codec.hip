@@ -166,6 +166,108 @@ __global__ __launch_bounds__(256) void k_xgemm(XGemm g) {
     }
 }
 
+// Causal conv, stride 1 (Cd.c conv stacks, K.c:659-871), as Kw accumulated
+// per-tap GEMMs: out[co][t] = b[co] + sum_tap sum_ci Wt[tap][co][ci] * x'[ci][t + tap*dil - pad],
+// x' = SnakeBeta(x) when g.sa is set (K.c:251-311).  64 (co) x 128 (t) tile
+// per workgroup, 4 waves of 32 x 64 (two v_mfma_f32_32x32x2f32 blocks: exact
+// fp32 products).  Per stage of 16 input channels the B window
+// x'[16][t0 - pad, t0 + 128) is staged ONCE in LDS -- SnakeBeta applied once
+// per element -- and every tap reads it shifted by tap*dil; the stage's
+// Kw x 64 x 16 weights come from the re-laid [Kw][co][ci] copy as float4.
+// The next stage's loads are in registers while the MFMAs consume this one.
+constexpr int CV_BM = 64, CV_BN = 128, CV_BC = 16, CV_HALO = 64;   // halo >= (Kw-1)*dil (host-checked)
+
+template <int KW>
+__global__ __launch_bounds__(256) void k_conv(XGemm g) {
+    constexpr int NBW = CV_BN + CV_HALO;                     // staged window columns
+    constexpr int NA4 = KW * CV_BM * CV_BC / 4 / 256;       // float4 weight loads per thread (ceil below)
+    constexpr int NA4C = (KW * CV_BM * CV_BC / 4 + 255) / 256;
+    constexpr int NB = (CV_BC * NBW + 255) / 256;            // window loads per thread
+    __shared__ __attribute__((aligned(16))) float As[KW][CV_BM][CV_BC + 1];
+    __shared__ float Bs[CV_BC][NBW + 1];
+    (void)NA4;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int m0 = blockIdx.y * CV_BM, n0 = blockIdx.x * CV_BN;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 64;
+    const int ci = g.K / KW, dil = g.dil, t0 = n0 - g.pad;
+    const int win = CV_BN + (KW - 1) * dil;                  // columns actually needed
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
+    float4 ra[NA4C];
+    float rb[NB];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int j = 0; j < NA4C; ++j) {
+            const int e = tid + 256 * j;                     // float4 index in [KW][BM][BC/4]
+            const int c4 = e % (CV_BC / 4), m = (e / (CV_BC / 4)) % CV_BM, tap = e / (CV_BC / 4 * CV_BM);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (tap < KW && m0 + m < g.M)
+                v = *reinterpret_cast<const float4 *>(g.wt + ((size_t)tap * g.M + m0 + m) * ci + c0 + 4 * c4);
+            ra[j] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int e = tid + 256 * j, c = e / NBW, x = e - c * NBW, t = t0 + x;
+            float v = 0.f;
+            if (c < CV_BC && x < win && t >= g.tmin && t < g.L) {
+                v = g.B[(size_t)(c0 + c) * g.ldb + t];
+                if (g.sa) v = snake1(v, g.sa[c0 + c], g.sb[c0 + c]);
+            }
+            rb[j] = v;
+        }
+    };
+    load(0);
+    for (int c0 = 0; c0 < ci; c0 += CV_BC) {
+#pragma unroll
+        for (int j = 0; j < NA4C; ++j) {
+            const int e = tid + 256 * j;
+            const int c4 = e % (CV_BC / 4), m = (e / (CV_BC / 4)) % CV_BM, tap = e / (CV_BC / 4 * CV_BM);
+            if (tap < KW) {
+                As[tap][m][4 * c4 + 0] = ra[j].x; As[tap][m][4 * c4 + 1] = ra[j].y;
+                As[tap][m][4 * c4 + 2] = ra[j].z; As[tap][m][4 * c4 + 3] = ra[j].w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int e = tid + 256 * j, c = e / NBW, x = e - c * NBW;
+            if (c < CV_BC) Bs[c][x] = rb[j];
+        }
+        __syncthreads();
+        if (c0 + CV_BC < ci) load(c0 + CV_BC);
+#pragma unroll
+        for (int tap = 0; tap < KW; ++tap) {
+            const int sh = tap * dil;
+#pragma unroll
+            for (int kk = 0; kk < CV_BC; kk += 2) {
+                const int kr = kk + (lane >> 5);
+                const float a = As[tap][wm + (lane & 31)][kr];
+                const float b0 = Bs[kr][wn + (lane & 31) + sh];
+                const float b1 = Bs[kr][wn + 32 + (lane & 31) + sh];
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + (lane & 31);
+        if (m >= g.M) continue;
+        if (n < g.N) xg_epi(g, m, n, acc0[r]);
+        if (n + 32 < g.N) xg_epi(g, m, n + 32, acc1[r]);
+    }
+}
+
+// w [co][ci][Kw] -> wt [Kw][co][ci]
+__global__ void k_wt_relayout(const float *w, int co, int ci, int Kw, float *wt) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x, n = (size_t)co * ci * Kw;
+    if (i >= n) return;
+    const int tap = (int)(i % Kw), c = (int)((i / Kw) % ci), o = (int)(i / ((size_t)Kw * ci));
+    wt[((size_t)tap * co + o) * ci + c] = w[i];
+}
+
 __global__ void k_xg_reduce(XGemm g, int nz) {
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (size_t)g.M * g.N) return;
@@ -293,8 +395,31 @@ __global__ void k_iota(int *p, int n, int zero) {
 
 }  // namespace
 
+// k_conv covers the conv when its re-laid weights are given, the channels
+// come in whole stages, the window halo fits and the output fills the chip
+// (small first-packet decodes keep the split-K GEMM).  QTTS_HIP_CONV=0 / 1
+// disables / forces it (tests).
+static bool conv_ok(const XGemm &g) {
+    static const char *f = getenv("QTTS_HIP_CONV");
+    if (f && !atoi(f)) return false;
+    if (!g.wt || g.bmode != XB_CONV || g.amode != XA_ROWS || !(g.Kw == 1 || g.Kw == 3 || g.Kw == 7) ||
+        (g.K / g.Kw) % CV_BC || (g.Kw - 1) * g.dil > CV_HALO || ((uintptr_t)g.wt & 15))
+        return false;
+    const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM);
+    return (f && atoi(f)) || tiles >= 96;
+}
+
 int qtts_xgemm(const XGemm &g, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
+    if (conv_ok(g)) {
+        const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM);
+        switch (g.Kw) {
+            case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
+            case 3: hipLaunchKernelGGL(k_conv<3>, cg, dim3(256), 0, st, g); break;
+            default: hipLaunchKernelGGL(k_conv<1>, cg, dim3(256), 0, st, g); break;
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, 1);
     // split-K when the output has too few tiles to fill the chip (first-packet
     // sized decodes): z ranges of >= 8 K-steps, partials in g.part
@@ -321,6 +446,20 @@ static float *cw(CodecModel *m, const std::string &n) {
     return it == m->w.end() ? nullptr : it->second;
 }
 
+// conv weight `n` ([co][ci][Kw]) re-laid as [Kw][co][ci] for k_conv, made on first use
+static const float *cwt(CodecModel *m, const std::string &n, int co, int ci, int Kw) {
+    auto it = m->wt.find(n);
+    if (it != m->wt.end()) return it->second;
+    const float *w = cw(m, n);
+    float *t = nullptr;
+    const size_t cnt = (size_t)co * ci * Kw;
+    if (!w || hipMalloc(&t, cnt * 4) != hipSuccess) return nullptr;
+    hipLaunchKernelGGL(k_wt_relayout, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, m->st, w, co, ci, Kw, t);
+    m->wt[n] = t;
+    m->wbytes += cnt * 4;
+    return t;
+}
+
 void codec_init(CodecModel *m, const qtts_dims_t *d, hipStream_t st) {
     m->d = *d;
     m->st = st;
@@ -341,6 +480,8 @@ void codec_destroy(CodecModel *m) {
     codec_free_state(m);
     for (auto &kv : m->w) hipFree(kv.second);
     m->w.clear();
+    for (auto &kv : m->wt) hipFree(kv.second);
+    m->wt.clear();
     if (m->cb) hipFree(m->cb);
     m->cb = nullptr;
 }
@@ -555,7 +696,7 @@ static int conv(CodecModel *m, const float *x, int ci, int L, const std::string 
                 const float *ea = nullptr, const float *eb = nullptr) {
     XGemm g;
     g.M = co; g.N = L; g.K = ci * K;
-    g.amode = XA_ROWS; g.A = cw(m, wn); g.lda = ci * K;
+    g.amode = XA_ROWS; g.A = cw(m, wn); g.lda = ci * K; g.wt = cwt(m, wn, co, ci, K);
     g.bmode = XB_CONV; g.B = x; g.ldb = L; g.Kw = K; g.dil = dil; g.pad = (K - 1) * dil; g.L = L;
     g.sa = sa; g.sb = sb;
     g.C = out; g.ldc = L; g.emode = emode; g.bias = bn.empty() ? nullptr : cw(m, bn); g.res = res; g.ldres = L;
@@ -737,7 +878,15 @@ extern "C" int qtts_hip_causal_conv1d(float *out, const float *in, const float *
     g.amode = XA_ROWS; g.A = w; g.lda = ci * k;
     g.bmode = XB_CONV; g.B = in; g.ldb = L; g.Kw = k; g.dil = dilation; g.pad = (k - 1) * dilation; g.L = L;
     g.C = out; g.ldc = L; g.emode = XE_BIAS_M; g.bias = b;
-    return qtts_xgemm(g, st);
+    float *t = nullptr;
+    const size_t cnt = (size_t)co * ci * k;
+    if (hipMalloc(&t, cnt * 4) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_wt_relayout, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, w, co, ci, k, t);
+    g.wt = t;
+    const int rc = qtts_xgemm(g, st);
+    if (hipStreamSynchronize(st) != hipSuccess) { hipFree(t); return -1; }
+    hipFree(t);
+    return rc;
 }
 
 extern "C" int qtts_hip_transposed_conv1d(float *out, const float *in, const float *w, const float *b, int ci, int co,
@@ -802,7 +951,7 @@ int sconv(CodecModel *m, int slot, float *x, int ldx, int ci, int L, const std::
     if (H > 0) hist_in(m, slot, x, ldx);
     XGemm g;
     g.M = co; g.N = L; g.K = ci * K;
-    g.amode = XA_ROWS; g.A = cw(m, wn); g.lda = ci * K;
+    g.amode = XA_ROWS; g.A = cw(m, wn); g.lda = ci * K; g.wt = cwt(m, wn, co, ci, K);
     g.bmode = XB_CONV; g.B = x; g.ldb = ldx; g.Kw = K; g.dil = dil; g.pad = H; g.L = L; g.tmin = -H;
     g.sa = sa; g.sb = sb;
     g.C = out; g.ldc = ldo; g.emode = emode; g.bias = bn.empty() ? nullptr : cw(m, bn); g.res = res; g.ldres = ldo;

@@ -53,6 +53,7 @@ struct CodecModel {
     int t_cap = 0, rope_cap = 0;
     int *codes_tmp = nullptr;
     float *wav = nullptr;
+    std::map<std::string, float *> wt;         // conv weights re-laid [Kw][co][ci] for k_conv, by name
     float *xg_part = nullptr;                  // split-K workspace of the codec GEMMs
     size_t xg_part_elems = 0;
     CodecStream cs;
@@ -109,5 +110,6 @@ struct XGemm {
     size_t part_elems = 0;
     int tmin = 0;                              // conv/tconv input columns t >= tmin are read (t < 0: the
                                                // streaming history kept in the buffer's left margin)
+    const float *wt = nullptr;                 // XB_CONV: the weights as [Kw][M][K/Kw] (k_conv's layout)
 };
 int qtts_xgemm(const XGemm &g, hipStream_t st);

@@ -142,6 +142,28 @@ def test_causal_conv1d_golden(gpu, i):
     np.testing.assert_allclose(out.cpu().numpy().reshape(co, L), K[f"conv{i}_y"], atol=2e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("ci,co,k,L,d", [(96, 96, 7, 8192, 9), (64, 192, 3, 4096, 1), (32, 128, 1, 6144, 1),
+                                         (768, 768, 7, 1024, 3)])
+def test_causal_conv1d_vocoder_shapes(gpu, ci, co, k, L, d):
+    """Vocoder-sized convs (the tap-staged k_conv path: channels in stages of
+    16, dilation up to 9) against a float64 restatement of kernel_causal_conv1d
+    (K.c:659-871): zero left pad (k-1)*d, bias, stride 1."""
+    import torch
+    rng = np.random.default_rng(ci + co + k + d)
+    x = rng.standard_normal((ci, L)).astype(np.float32)
+    w = (rng.standard_normal((co, ci, k)) / np.sqrt(ci * k)).astype(np.float32)
+    b = rng.standard_normal(co).astype(np.float32)
+    out = torch.zeros(co * L, device=gpu)
+    qtts.Kernels.causal_conv1d(out, T(x, gpu), T(w, gpu), T(b, gpu), ci, co, k, L, d, 1)
+    torch.cuda.synchronize()
+    pad = (k - 1) * d
+    xp = np.concatenate([np.zeros((ci, pad)), x.astype(np.float64)], axis=1)
+    ref = np.tile(b.astype(np.float64)[:, None], (1, L))
+    for tap in range(k):
+        ref += w[:, :, tap].astype(np.float64) @ xp[:, tap * d: tap * d + L]
+    np.testing.assert_allclose(out.cpu().numpy().reshape(co, L), ref, atol=2e-5, rtol=1e-4)
+
+
 @pytest.mark.parametrize("i", range(5))
 def test_transposed_conv1d_golden(gpu, i):
     import torch
