@@ -177,8 +177,14 @@ __global__ __launch_bounds__(256) void k_xgemm(XGemm g) {
 // The next stage's loads are in registers while the MFMAs consume this one.
 constexpr int CV_BM = 64, CV_BN = 128, CV_BC = 16, CV_HALO = 64;   // halo >= (Kw-1)*dil (host-checked)
 
+// blockIdx.z: transposed-conv output phase (tconv_run): weights g.wt + z*KW*M*ci,
+// outputs at column n*stride + phase + z
 template <int KW>
 __global__ __launch_bounds__(256) void k_conv(XGemm g) {
+    if (blockIdx.z) {
+        g.wt += (size_t)blockIdx.z * KW * g.M * (g.K / KW);
+        g.phase += blockIdx.z;
+    }
     constexpr int NBW = CV_BN + CV_HALO;                     // staged window columns
     constexpr int NA4 = KW * CV_BM * CV_BC / 4 / 256;       // float4 weight loads per thread (ceil below)
     constexpr int NA4C = (KW * CV_BM * CV_BC / 4 + 255) / 256;
@@ -266,6 +272,17 @@ __global__ void k_wt_relayout(const float *w, int co, int ci, int Kw, float *wt)
     if (i >= n) return;
     const int tap = (int)(i % Kw), c = (int)((i / Kw) % ci), o = (int)(i / ((size_t)Kw * ci));
     wt[((size_t)tap * co + o) * ci + c] = w[i];
+}
+
+// transposed conv w [ci][co][Kw] (Kw = ntap*s) -> per phase causal-conv weights
+// wt [s][ntap][co][ci]: phase ph, conv tap j' (input t - (ntap-1-j')) uses w[..][ph + (ntap-1-j')*s]
+__global__ void k_wt_tconv(const float *w, int ci, int co, int Kw, int s, float *wt) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x, n = (size_t)co * ci * Kw;
+    if (i >= n) return;
+    const int nt = Kw / s;
+    const int c = (int)(i % ci), o = (int)((i / ci) % co), tap = (int)((i / ((size_t)ci * co)) % nt),
+              ph = (int)(i / ((size_t)ci * co * nt));
+    wt[i] = w[((size_t)c * co + o) * Kw + ph + (nt - 1 - tap) * s];
 }
 
 __global__ void k_xg_reduce(XGemm g, int nz) {
@@ -402,24 +419,30 @@ __global__ void k_iota(int *p, int n, int zero) {
 static bool conv_ok(const XGemm &g) {
     static const char *f = getenv("QTTS_HIP_CONV");
     if (f && !atoi(f)) return false;
-    if (!g.wt || g.bmode != XB_CONV || g.amode != XA_ROWS || !(g.Kw == 1 || g.Kw == 3 || g.Kw == 7) ||
-        (g.K / g.Kw) % CV_BC || (g.Kw - 1) * g.dil > CV_HALO || ((uintptr_t)g.wt & 15))
+    static const char *ft = getenv("QTTS_HIP_CONV_TILES");
+    static const int min_tiles = ft ? atoi(ft) : 96;
+    if (!g.wt || g.bmode != XB_CONV || g.amode != XA_ROWS ||
+        !(g.Kw == 1 || g.Kw == 2 || g.Kw == 3 || g.Kw == 7) || (g.K / g.Kw) % CV_BC ||
+        (g.Kw - 1) * g.dil > CV_HALO || ((uintptr_t)g.wt & 15))
         return false;
-    const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM);
-    return (f && atoi(f)) || tiles >= 96;
+    const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM) * (g.stride > 1 ? g.stride : 1);
+    return (f && atoi(f)) || tiles >= min_tiles;
+}
+
+static int conv_launch(const XGemm &g, int nz, hipStream_t st) {
+    const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM, nz);
+    switch (g.Kw) {
+        case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
+        case 3: hipLaunchKernelGGL(k_conv<3>, cg, dim3(256), 0, st, g); break;
+        case 2: hipLaunchKernelGGL(k_conv<2>, cg, dim3(256), 0, st, g); break;
+        default: hipLaunchKernelGGL(k_conv<1>, cg, dim3(256), 0, st, g); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int qtts_xgemm(const XGemm &g, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
-    if (conv_ok(g)) {
-        const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM);
-        switch (g.Kw) {
-            case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
-            case 3: hipLaunchKernelGGL(k_conv<3>, cg, dim3(256), 0, st, g); break;
-            default: hipLaunchKernelGGL(k_conv<1>, cg, dim3(256), 0, st, g); break;
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
+    if (conv_ok(g)) return conv_launch(g, g.stride > 1 ? g.stride : 1, st);
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, 1);
     // split-K when the output has too few tiles to fill the chip (first-packet
     // sized decodes): z ranges of >= 8 K-steps, partials in g.part
@@ -706,17 +729,48 @@ static int conv(CodecModel *m, const float *x, int ci, int L, const std::string 
 }
 
 // transposed conv (stride s, kernel Kw = s * ntap) as s phase GEMMs
-static int tconv(CodecModel *m, const float *x, int ci, int L, const float *w, const float *bias, int co, int Kw,
-                 int s, float *out, const float *sa, const float *sb, hipStream_t st) {
+// transposed-conv weights re-laid per phase for k_conv (k_wt_tconv), made on first use
+static const float *ctwt(CodecModel *m, const float *w, int ci, int co, int Kw, int s, hipStream_t st) {
+    const std::string key = "tconv#" + std::to_string((uintptr_t)w);
+    auto it = m->wt.find(key);
+    if (it != m->wt.end()) return it->second;
+    float *t = nullptr;
+    const size_t cnt = (size_t)co * ci * Kw;
+    if (!w || hipMalloc(&t, cnt * 4) != hipSuccess) return nullptr;
+    hipLaunchKernelGGL(k_wt_tconv, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, w, ci, co, Kw, s, t);
+    m->wt[key] = t;
+    m->wbytes += cnt * 4;
+    return t;
+}
+
+// a transposed conv (kernel Kw = ntap*s, stride s) as s causal convs of ntap
+// taps over the same input, one per output phase, in one k_conv launch
+// (grid z = phase) when k_conv covers it; else one implicit GEMM per phase
+static int tconv_run(CodecModel *m, const XGemm &g, hipStream_t st) {
+    const int s = g.stride, nt = g.Kw / s, ci = g.K / nt;
+    XGemm c = g;
+    c.amode = XA_ROWS; c.A = nullptr; c.bmode = XB_CONV; c.Kw = nt; c.dil = 1; c.pad = nt - 1; c.phase = 0;
+    c.wt = (const float *)16;  // shape-only probe before the relayout is made
+    if (conv_ok(c)) {
+        c.wt = ctwt(m, g.A, ci, g.co, g.Kw, s, st);
+        if (c.wt) return xgm(m, c, st);
+    }
     for (int ph = 0; ph < s; ++ph) {
-        XGemm g;
-        g.M = co; g.N = L; g.K = ci * (Kw / s);
-        g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s; g.phase = ph;
-        g.bmode = XB_TCONV; g.B = x; g.ldb = L; g.L = L; g.sa = sa; g.sb = sb;
-        g.C = out; g.ldc = L * s; g.emode = XE_BIAS_M; g.bias = bias;
-        KCK(xgm(m, g, st));
+        XGemm p = g;
+        p.phase = ph;
+        KCK(xgm(m, p, st));
     }
     return 0;
+}
+
+static int tconv(CodecModel *m, const float *x, int ci, int L, const float *w, const float *bias, int co, int Kw,
+                 int s, float *out, const float *sa, const float *sb, hipStream_t st) {
+    XGemm g;
+    g.M = co; g.N = L; g.K = ci * (Kw / s);
+    g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s;
+    g.bmode = XB_TCONV; g.B = x; g.ldb = L; g.L = L; g.sa = sa; g.sb = sb;
+    g.C = out; g.ldc = L * s; g.emode = XE_BIAS_M; g.bias = bias;
+    return tconv_run(m, g, st);
 }
 
 static int codec_transformer(CodecModel *m, const float *pc /*[lat][T]*/, int T, float *out /*[lat][T]*/) {
@@ -893,7 +947,13 @@ extern "C" int qtts_hip_transposed_conv1d(float *out, const float *in, const flo
                                           int k, int stride, int L, void *stream) {
     if (k % stride) return -1;
     CodecModel dummy;
-    return tconv(&dummy, in, ci, L, w, b, co, k, stride, out, nullptr, nullptr, (hipStream_t)stream);
+    int rc = tconv(&dummy, in, ci, L, w, b, co, k, stride, out, nullptr, nullptr, (hipStream_t)stream);
+    if (!dummy.wt.empty()) {
+        if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = -1;
+        for (auto &kv : dummy.wt) hipFree(kv.second);
+        dummy.wt.clear();
+    }
+    return rc;
 }
 
 extern "C" int qtts_hip_snake_beta(float *out, const float *x, const float *alpha, const float *inv_beta, int channels,
@@ -966,14 +1026,12 @@ int stconv(CodecModel *m, int slot, float *x, int ldx, int ci, int L, const floa
            int s, float *out, int ldo, const float *sa, const float *sb) {
     const int H = Kw / s - 1;
     if (H > 0) hist_in(m, slot, x, ldx);
-    for (int ph = 0; ph < s; ++ph) {
-        XGemm g;
-        g.M = co; g.N = L; g.K = ci * (Kw / s);
-        g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s; g.phase = ph;
-        g.bmode = XB_TCONV; g.B = x; g.ldb = ldx; g.L = L; g.tmin = -H; g.sa = sa; g.sb = sb;
-        g.C = out; g.ldc = ldo; g.emode = XE_BIAS_M; g.bias = bias;
-        KCK(xgm(m, g, m->st));
-    }
+    XGemm g;
+    g.M = co; g.N = L; g.K = ci * (Kw / s);
+    g.amode = XA_TCONV_W; g.A = w; g.co = co; g.Kw = Kw; g.stride = s;
+    g.bmode = XB_TCONV; g.B = x; g.ldb = ldx; g.L = L; g.tmin = -H; g.sa = sa; g.sb = sb;
+    g.C = out; g.ldc = ldo; g.emode = XE_BIAS_M; g.bias = bias;
+    KCK(tconv_run(m, g, m->st));
     if (H > 0) hist_out(m, slot, x, ldx, L);
     return 0;
 }

@@ -175,6 +175,28 @@ def test_transposed_conv1d_golden(gpu, i):
     np.testing.assert_allclose(out.cpu().numpy().reshape(co, L * s), K[f"tconv{i}_y"], atol=2e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("ci,co,k,s,L", [(1536, 768, 16, 8, 512), (192, 96, 6, 3, 8192), (768, 384, 10, 5, 1024),
+                                         (1024, 1024, 2, 2, 2048), (384, 192, 8, 4, 2048)])
+def test_transposed_conv1d_vocoder_shapes(gpu, ci, co, k, s, L):
+    """Vocoder-sized transposed convs (all phases in one k_conv launch, each a
+    causal conv of k/s taps) against a float64 restatement of
+    kernel_transposed_conv1d (K.c:873-940) trimmed to L*s outputs."""
+    import torch
+    rng = np.random.default_rng(ci + k + L)
+    x = rng.standard_normal((ci, L)).astype(np.float32)
+    w = (rng.standard_normal((ci, co, k)) / np.sqrt(ci * k / s)).astype(np.float32)
+    b = rng.standard_normal(co).astype(np.float32)
+    out = torch.zeros(co * L * s, device=gpu)
+    qtts.Kernels.transposed_conv1d(out, T(x, gpu), T(w, gpu), T(b, gpu), ci, co, k, s, L)
+    torch.cuda.synchronize()
+    full = np.zeros((co, (L - 1) * s + k))
+    xd = x.astype(np.float64)
+    for j in range(k):
+        full[:, j: j + (L - 1) * s + 1: s] += w[:, :, j].astype(np.float64).T @ xd
+    ref = full[:, :L * s] + b.astype(np.float64)[:, None]
+    np.testing.assert_allclose(out.cpu().numpy().reshape(co, L * s), ref, atol=2e-5, rtol=1e-4)
+
+
 def test_snake_golden(gpu):
     import torch
     x = K["snake_x"]
