@@ -136,6 +136,11 @@ int qtts_hip_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_d
  * out = rmsnorm(x) @ A^T  (c/qwen_tts_kernels.c:27 + :95) */
 int qtts_hip_rmsnorm_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_dev, const float *w_dev,
                                  float eps, int rows, int cols, int batch, void *stream);
+/* the decode-loop GEMV dispatcher on `batch` lock-step rows (w_dev NULL: no norm):
+ * batch 1 -> the batch-1 weight stream, 2..16 -> the matrix-core batch kernel
+ * (c/qwen_tts_kernels.c:27 + :95 per row) */
+int qtts_hip_decode_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_dev, const float *w_dev,
+                                float eps, int rows, int cols, int batch, void *stream);
 /* kernel_sample_top_k (c/qwen_tts_kernels.c:407) on `batch` logit rows; rng_bits
  * holds the float-bit xorshift state per row (updated in place). */
 int qtts_hip_sample_top_k(int *out_dev, const float *logits_dev, int vocab, int top_k, float top_p,

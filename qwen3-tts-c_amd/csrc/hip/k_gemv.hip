@@ -514,6 +514,10 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
 #undef QTTS_G1
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+    if (a.nb >= 2) {   // lock-step batch: the matrix-core kernel (k_gemvm.hip) where it covers the shape
+        const int rc = qtts_gemvm(a, st);
+        if (rc != 1) return rc;
+    }
     if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 256);
     int NB = a.nb <= 1 ? 1 : a.nb <= 2 ? 2 : a.nb <= 4 ? 4 : a.nb <= 8 ? 8 : 16;
     const int unit = 64 * a.ksplit;

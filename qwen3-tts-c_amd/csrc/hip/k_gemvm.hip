@@ -1,0 +1,357 @@
+// k_gemvm.hip - lock-step batch decode GEMV (2..16 utterances) on the bf16
+// matrix cores.
+//
+// y[b, r] = epilogue( sum_c W[r, c] * xin[b, c] ),  b < nb <= 16
+//
+// Replaces, for the batched decode of SURVEY.md 8e (B utterances per GPU in
+// lock step), the per-utterance kernel_matvec_bf16 / kernel_swiglu_matvec_bf16
+// calls (K.c:95-149, 213-233) and the rms_norm / residual passes around them
+// (T.c:142-247): one weight read per frame serves every utterance.
+//
+// Why the matrix cores: at batch B a weight element costs B multiply-adds.
+// On the VALU with x in LDS that is 2·B bytes of LDS reads per weight byte
+// and 8·B FMAs per 16-B load (k_gemv<NB> ran at 250 GB/s for B = 8).  One
+// v_mfma_f32_16x16x32_bf16 instead applies a 16-row x 32-column weight
+// fragment to all 16 batch rows at once.
+//
+// Exact products ("3 x bf16", as k_mgemm.hip): x = x1 + x2 + x3 with
+// x1 = bf16(x), x2 = bf16(x - x1), x3 = bf16(x - x1 - x2); bf16 x bf16
+// products are exact in fp32, so the sum differs from an fp32 GEMV only in
+// summation order (the GEMV bar of tests/test_gpu_kernels.py).
+//
+// Mapping: one workgroup = 16 weight rows (the MFMA B/N side) x all nb batch
+// rows (A/M side, padded to 16 with zeros).  The 4 waves take 32-column K
+// steps round-robin; lane l loads W[r0 + (l & 15)][32 s + 8 (l >> 4) .. +7]
+// (one 16-B load = the B fragment) and reads x[l & 15][same columns] of the
+// three planes from LDS (the A fragments).  Weight loads run U steps ahead in
+// registers, the first group issued before the prologue.  The four partial
+// 16x16 tiles are summed in wave order through LDS; wave 0 applies the
+// epilogue.
+//
+// Prologue: the nb x rows (fp32 rows, or bf16 / fp32 table rows gathered by
+// device-side ids) are RMS-normalised (K.c:27-39, x * inv * w), split once and
+// stored as three bf16 planes in LDS, so the K loop is loads + MFMAs only.
+// Whole rows up to 16 float4 per thread go through registers (one barrier
+// for the statistics); longer ones (the down projections at B >= 8) are staged
+// in column chunks after a statistics pre-pass.
+#include <algorithm>
+
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+// id of the table row that batch row b reads
+__device__ __forceinline__ int gm_row_id(const GemvArgs &a, int b) {
+    const int *p = a.ids + (size_t)b * a.ids_bstride + a.ids_off;
+    if (a.row_sel) p += (size_t)a.row_sel[b] * a.ids_rstride;
+    return *p;
+}
+
+// two f32 -> packed bf16 (round to nearest even: v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    const bf2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float lo_f(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float hi_f(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
+
+// x = x1 + x2 + x3 (each bf16, exact) for 4 values -> the three planes
+__device__ __forceinline__ void split_store(float4 v, unsigned short *hp, int plane_stride) {
+    const uint32_t a1 = pk_bf16(v.x, v.y), b1 = pk_bf16(v.z, v.w);
+    const float ex = v.x - lo_f(a1), ey = v.y - hi_f(a1), ez = v.z - lo_f(b1), ew = v.w - hi_f(b1);
+    const uint32_t a2 = pk_bf16(ex, ey), b2 = pk_bf16(ez, ew);
+    const uint32_t a3 = pk_bf16(ex - lo_f(a2), ey - hi_f(a2)), b3 = pk_bf16(ez - lo_f(b2), ew - hi_f(b2));
+    *reinterpret_cast<uint2 *>(hp) = make_uint2(a1, b1);
+    *reinterpret_cast<uint2 *>(hp + plane_stride) = make_uint2(a2, b2);
+    *reinterpret_cast<uint2 *>(hp + 2 * plane_stride) = make_uint2(a3, b3);
+}
+
+// float4 of batch row b at column c (fp32 row, or bf16 / fp32 table row by id)
+__device__ __forceinline__ float4 gm_load(const GemvArgs &a, int b, int c) {
+    if (a.table) {
+        const bf16_t *t = a.table + (size_t)gm_row_id(a, b) * a.C + c;
+        const uint2 q = *reinterpret_cast<const uint2 *>(t);
+        return make_float4(lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y));
+    }
+    if (a.table_f32) return *reinterpret_cast<const float4 *>(a.table_f32 + (size_t)gm_row_id(a, b) * a.C + c);
+    return *reinterpret_cast<const float4 *>(a.x + (size_t)b * a.ldx + c);
+}
+
+// normalise (inv / norm_w), copy out (workgroup 0), split into the planes
+__device__ __forceinline__ void gm_put(const GemvArgs &a, float4 v, int b, int c, int cl, float iv,
+                                       unsigned short *hp, int LDH, int PS) {
+    if (a.xcopy && blockIdx.x == 0 && !a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + (size_t)b * a.ldxc + c) = v;
+    if (a.norm_w) {
+        const float4 nw = *reinterpret_cast<const float4 *>(a.norm_w + c);
+        v.x = v.x * iv * nw.x; v.y = v.y * iv * nw.y; v.z = v.z * iv * nw.z; v.w = v.w * iv * nw.w;
+        if (a.xcopy && blockIdx.x == 0 && a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + (size_t)b * a.ldxc + c) = v;
+    }
+    split_store(v, hp + b * LDH + cl, PS);
+}
+
+// stage columns [c0, c0 + CCH) of the nb rows (chunked / generic path)
+__device__ __forceinline__ void gm_stage(const GemvArgs &a, const float *inv, unsigned short *hp, int LDH, int PS,
+                                         int c0, int CCH) {
+    const int n4 = CCH / 4;
+    for (int i = threadIdx.x; i < a.nb * n4; i += blockDim.x) {
+        const int b = i / n4, cl = 4 * (i - b * n4);
+        gm_put(a, gm_load(a, b, c0 + cl), b, c0 + cl, cl, a.norm_w ? inv[b] : 1.f, hp, LDH, PS);
+    }
+}
+
+// A workgroup = TPW row tiles of 16 rows x KS waves per tile (the K steps of a
+// tile dealt round-robin to its KS waves).
+// XU > 0: register prologue (whole rows, C % 256 == 0, <= XU float4 units per
+// thread: unit i = tid + blockDim*q, wave-uniform batch row); the per-64-unit
+// partial sums of squares of a row are adjacent and summed in order.
+// XU == 0: statistics pre-pass + (chunked) staging.
+template <bool NT, int U, int XU, int KS>
+__global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x, nw = nthr >> 6;
+    const int nb = a.nb, C = a.C, CCH = a.cch, LDH = CCH + 8, PS = nb * LDH;
+    const bool chunked = CCH < C;
+    unsigned short *hp = reinterpret_cast<unsigned short *>(smem);        // [3][nb][LDH] bf16 planes
+    floatx4 *red = reinterpret_cast<floatx4 *>(smem);                     // [nw][64] (after the K loop)
+    const int region = max(3 * PS * 2, nw * 64 * 16) / 4;                 // floats
+    float *inv = smem + region;                                           // [16]
+    float *part = inv + 16;                                               // [nb * C / 256]
+
+    const int tw = w / KS, ksl = w - tw * KS;                             // tile, K slice of this wave
+    const int tile = blockIdx.x * tpw + tw;
+    const int r0 = tile * 16, rl = lane & 15, kq = 8 * (lane >> 4);
+    const int row = r0 + rl < a.R ? r0 + rl : a.R - 1;
+    const v4u *wr = reinterpret_cast<const v4u *>(a.W + (size_t)row * C + kq);
+    const int nsteps = C / 32;
+    const int J = r0 < a.R ? (nsteps - ksl + KS - 1) / KS : 0;   // this wave's K steps: s = ksl + KS * j
+    const int ng = (J + U - 1) / U;
+    const int spc = CCH / 32 / KS;                    // steps per wave per chunk (chunked mode)
+
+    v4u wv[U];
+    auto load = [&](int g) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int j = g * U + u;
+            j = j < J ? j : J - 1;                    // clamp: loads stay unconditional
+            const v4u *p = wr + ((32 * (ksl + KS * j)) >> 3);
+            if constexpr (NT) wv[u] = __builtin_nontemporal_load(p);
+            else wv[u] = *p;
+        }
+    };
+    if (ng > 0) load(0);
+
+    // ---- prologue
+    if constexpr (XU > 0) {
+        const int n4 = C / 4, nu = nb * n4;
+        float4 xv[XU];
+#pragma unroll
+        for (int q = 0; q < XU; ++q) {
+            const int i = tid + nthr * q;
+            if (i < nu) xv[q] = gm_load(a, i / n4, 4 * (i % n4));
+        }
+        if (a.norm_w) {
+#pragma unroll
+            for (int q = 0; q < XU; ++q) {
+                const int i = tid + nthr * q;
+                const float4 v = xv[q];
+                const float ss = wave_sum(i < nu ? v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w : 0.f);
+                if (lane == 0 && i < nu) part[(i >> 6)] = ss;
+            }
+            __syncthreads();
+            if (tid < nb) {   // row tid: its C / 256 adjacent partials, in order
+                const int np = C / 256;
+                float ss = 0.f;
+                for (int k = 0; k < np; ++k) ss += part[tid * np + k];
+                inv[tid] = rms_inv(ss, C, a.eps);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < XU; ++q) {
+            const int i = tid + nthr * q;
+            if (i < nu) {
+                const int bb = i / n4, c = 4 * (i % n4);
+                gm_put(a, xv[q], bb, c, c, a.norm_w ? inv[bb] : 1.f, hp, LDH, PS);
+            }
+        }
+    } else {
+        if (a.norm_w) {
+            for (int bb = w; bb < nb; bb += nw) {
+                float ss = 0.f;
+                for (int c = 4 * lane; c < C; c += 256) {
+                    const float4 v = gm_load(a, bb, c);
+                    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                }
+                ss = wave_sum(ss);
+                if (lane == 0) inv[bb] = rms_inv(ss, C, a.eps);
+            }
+            __syncthreads();
+        }
+        gm_stage(a, inv, hp, LDH, PS, 0, CCH);
+    }
+    __syncthreads();
+
+    // ---- weight stream x MFMA (A = the x planes, B = the weight fragment)
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int tb = lane & 15;        // batch row of this lane's A fragment
+    int cur_ch = 0;
+    const int ngm = chunked ? (nsteps / KS + U - 1) / U : ng;   // chunked: every wave runs the same groups
+    for (int g = 0; g < ngm; ++g) {
+        v4u cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = wv[u];
+        if (g + 1 < ng) load(g + 1);
+        int cbase = 0;
+        if constexpr (XU == 0) {
+            if (chunked) {   // spc steps per wave per chunk, spc % U == 0 (host)
+                const int ch = (g * U) / spc;
+                if (ch != cur_ch) {
+                    __syncthreads();
+                    gm_stage(a, inv, hp, LDH, PS, ch * CCH, CCH);
+                    __syncthreads();
+                    cur_ch = ch;
+                }
+                cbase = cur_ch * CCH;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = g * U + u;
+            if (j < J) {
+                bf16x8 h1, h2, h3;
+                if (tb < nb) {
+                    const unsigned short *xp = hp + tb * LDH + 32 * (ksl + KS * j) - cbase + kq;
+                    h1 = *reinterpret_cast<const bf16x8 *>(xp);
+                    h2 = *reinterpret_cast<const bf16x8 *>(xp + PS);
+                    h3 = *reinterpret_cast<const bf16x8 *>(xp + 2 * PS);
+                } else {
+                    h1 = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+                    h2 = h1;
+                    h3 = h1;
+                }
+                const bf16x8 bw = __builtin_bit_cast(bf16x8, cur[u]);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h1, bw, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h2, bw, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h3, bw, acc, 0, 0, 0);
+            }
+        }
+    }
+
+    // ---- a tile's KS partials, summed in wave order; epilogue by its first wave
+    __syncthreads();   // the planes are dead: red aliases them
+    red[w * 64 + lane] = acc;
+    __syncthreads();
+    if (ksl != 0 || r0 >= a.R) return;
+    floatx4 v = red[w * 64 + lane];
+#pragma unroll
+    for (int k = 1; k < KS; ++k) v += red[(w + k) * 64 + lane];
+    const int r = r0 + rl;   // D: column = lane & 15 (weight row), row = 4 (lane >> 4) + i (batch row)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int bb = 4 * (lane >> 4) + i;
+        const float val = v[i];
+        const float up = __shfl(val, (lane & 15) < 12 ? lane + 4 : lane, 64);
+        if (bb >= nb || r >= a.R) continue;
+        float *yr = a.y + (size_t)bb * a.ldy;
+        switch (a.epi) {
+            case EPI_STORE: yr[r] = val; break;
+            case EPI_BIAS: yr[r] = val + a.bias[r]; break;
+            case EPI_BIAS_SILU: {
+                const float z = val + a.bias[r];
+                yr[r] = z / (1.0f + expf(-z));
+                break;
+            }
+            case EPI_RESID: yr[r] += val; break;
+            case EPI_SWIGLU:
+                if ((r & 7) < 4) yr[(r >> 3) * 4 + (r & 3)] = (val / (1.0f + expf(-val))) * up;
+                break;
+        }
+    }
+}
+
+}  // namespace
+
+// LDS budget for the three bf16 planes of the staged x rows (bytes): one
+// workgroup per CU at the largest.
+static constexpr int GM_PLANES_MAX = 150 * 1024;
+static int gm_planes(int nb, int cch) { return 3 * nb * (cch + 8) * 2; }
+
+// Returns 1 when the shape is not covered (the caller uses k_gemv), 0 ok,
+// -1 launch error.
+int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
+    static const char *off = getenv("QTTS_HIP_GEMVM");
+    if (off && !atoi(off)) return 1;
+    GemvArgs a = in;
+    if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32) return 1;
+    if (a.table) {
+        if (a.C % 4) return 1;
+    } else if (a.table_f32) {
+        if ((uintptr_t)a.table_f32 & 15) return 1;
+    } else if (!a.x || a.ldx % 4 || ((uintptr_t)a.x & 15)) {
+        return 1;
+    }
+    if (a.norm_w && ((uintptr_t)a.norm_w & 15)) return 1;
+    if (a.xcopy && (a.ldxc % 4 || ((uintptr_t)a.xcopy & 15))) return 1;
+    // 16 waves per workgroup where the shape allows (one workgroup per CU):
+    // KS waves per tile keep >= 2 K steps each; TPW tiles per workgroup bring
+    // the grid to about one round over the 256 CUs (the x prologue is paid
+    // once per workgroup)
+    const int nsteps = a.C / 32, T = a.R / 16;
+    int tpw = (T + 255) / 256;
+    if (tpw > 4) tpw = 4;
+    int KS = 16 / (tpw == 3 ? 4 : tpw);
+    while (KS > 4 && nsteps < 2 * KS) KS /= 2;
+    if (tpw * KS > 16) tpw = 16 / KS;
+    // column chunk: the whole row when it fits, else the fewest equal chunks
+    // of whole 32 x KS-column step rounds with an even step count per wave
+    int cch = a.C;
+    if (gm_planes(a.nb, a.C) > GM_PLANES_MAX) {
+        const int unit = 32 * KS;
+        if (a.C % unit) return 1;
+        int n = 2;
+        for (; n <= a.C / unit; ++n)
+            if ((a.C / unit) % n == 0 && gm_planes(a.nb, a.C / n) <= GM_PLANES_MAX && (a.C / unit / n) % 2 == 0)
+                break;
+        if (n > a.C / unit) return 1;
+        cch = a.C / n;
+    }
+    a.cch = cch;
+    int U;
+    if (cch < a.C) {
+        const int spc = cch / 32 / KS;
+        U = spc % 8 == 0 ? 8 : spc % 4 == 0 ? 4 : 2;
+    } else {
+        const int J = (nsteps + KS - 1) / KS;
+        U = J <= 2 ? 2 : J <= 4 ? 4 : 8;
+    }
+    const int nthr = 64 * KS * tpw, nu = a.nb * a.C / 4;
+    const int xu = (cch == a.C && a.C % 256 == 0) ? (nu + nthr - 1) / nthr : 0;
+    const int XU = xu == 0 || xu > 8 ? 0 : xu <= 4 ? 4 : 8;
+    const int region = std::max(gm_planes(a.nb, cch), nthr / 64 * 64 * 16);
+    const size_t smem = (size_t)region + (16 + (a.nb * a.C / 256 > 64 ? a.nb * a.C / 256 : 64)) * 4;
+    const dim3 grid((T + tpw - 1) / tpw);
+#define QTTS_GM(UU, XX, KK)                                                                                   \
+    if (a.nt) hipLaunchKernelGGL((k_gemvm<true, UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);            \
+    else hipLaunchKernelGGL((k_gemvm<false, UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);                \
+    qtts_last_kernel = a.nt ? "k_gemvm<true, " #UU ", " #XX ", " #KK ">" : "k_gemvm<false, " #UU ", " #XX ", " #KK ">";
+#define QTTS_GMX(UU, KK)                                       \
+    if (XU == 4) { QTTS_GM(UU, 4, KK) }                        \
+    else if (XU == 8) { QTTS_GM(UU, 8, KK) }                   \
+    else { QTTS_GM(UU, 0, KK) }
+#define QTTS_GMK(UU)                                           \
+    if (KS == 16) { QTTS_GMX(UU, 16) }                         \
+    else if (KS == 8) { QTTS_GMX(UU, 8) }                      \
+    else { QTTS_GMX(UU, 4) }
+    if (U == 8) { QTTS_GMK(8) }
+    else if (U == 4) { QTTS_GMK(4) }
+    else { QTTS_GMK(2) }
+#undef QTTS_GMK
+#undef QTTS_GMX
+#undef QTTS_GM
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

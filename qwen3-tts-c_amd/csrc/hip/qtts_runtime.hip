@@ -1206,6 +1206,15 @@ extern "C" int qtts_hip_rmsnorm_matvec_bf16(float *out, const uint16_t *A, const
     return matvec_any(a, (hipStream_t)stream);
 }
 
+// the decode dispatcher itself (qtts_gemv): batch 1 -> k_gemv1, 2..16 ->
+// k_gemvm (matrix cores) where covered, else k_gemv
+extern "C" int qtts_hip_decode_matvec_bf16(float *out, const uint16_t *A, const float *x, const float *w, float eps,
+                                           int rows, int cols, int batch, void *stream) {
+    GemvArgs a = gv(A, rows, cols, x, cols, out, rows, batch, EPI_STORE);
+    a.norm_w = w; a.eps = eps;
+    return qtts_gemv(a, (hipStream_t)stream);
+}
+
 extern "C" int qtts_hip_sample_top_k(int *out, const float *logits, int vocab, int top_k, float top_p, float temp,
                                      uint32_t *rng_bits, int batch, void *stream) {
     SampArgs s;

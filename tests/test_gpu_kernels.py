@@ -88,6 +88,35 @@ def test_rmsnorm_matvec(gpu, R, Cc, B):
     assert np.all(np.abs(got - ref) <= gemv_bound(A, xn) + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
 
 
+# lock-step batch decode shapes (k_gemvm: matrix cores, x staged whole or in
+# column chunks for the down projections at B >= 8) + the tiny model's
+DECODE_SHAPES = [(4096, 2048, 8, True), (12288, 2048, 8, True), (2048, 6144, 8, False), (2048, 6144, 16, False),
+                 (1024, 3072, 16, False), (4096, 1024, 2, True), (6144, 1024, 4, True), (2048, 1024, 16, True),
+                 (3072, 2048, 3, True), (1024, 2048, 5, False), (256, 128, 3, True), (128, 64, 2, True),
+                 (2048, 64, 7, False)]
+
+
+@pytest.mark.parametrize("R,Cc,B,norm", DECODE_SHAPES)
+def test_decode_matvec_batch(gpu, R, Cc, B, norm):
+    """The decode-loop dispatcher at batch 2..16 (one weight read serves
+    every utterance) against float64, with and without the RMSNorm prologue."""
+    import torch
+    rng = np.random.default_rng(R + Cc * 3 + B)
+    A = f32_to_bf16((rng.standard_normal((R, Cc)) / np.sqrt(Cc)).astype(np.float32))
+    x = (rng.standard_normal((B, Cc)) * 2).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(Cc)).astype(np.float32)
+    out = torch.zeros(B * R, device=gpu)
+    qtts.Kernels.decode_matvec_bf16(out, T(A, gpu, torch.int16), T(x, gpu), T(w, gpu) if norm else None, 1e-6,
+                                    R, Cc, B)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(B, R)
+    xn = x.astype(np.float64)
+    if norm:
+        xn = (x / np.sqrt((x.astype(np.float64) ** 2).mean(1, keepdims=True) + 1e-6) * w)
+    ref = xn @ bf16_f64(A).T
+    assert np.all(np.abs(got - ref) <= gemv_bound(A, xn) + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
+
+
 def sample_gpu(dev, lg, V, k, tp, temp, rng_bits):
     import torch
     B = lg.shape[0]

@@ -1,6 +1,8 @@
 // mb_gemv.cpp - GEMV configuration sweep (development tool): times the batch-1
 // weight-streaming GEMV (qtts_gemv) on the 1.7B decode shapes for each KSPLIT,
-// NT on/off, back-to-back launches captured in a HIP graph.
+// NT on/off, back-to-back launches captured in a HIP graph.  MB_BATCH=B times
+// the lock-step batch path (qtts_gemv at nb = B: k_gemvm) instead, one line
+// per shape (talker weights nt, sub-talker default policy).
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iqwen3-tts-c_amd/csrc/hip tools/mb_gemv.cpp \
 //         -Lqwen3-tts-c_amd/lib -lqwen_tts_amd -Wl,-rpath,$PWD/qwen3-tts-c_amd/lib -o tools/mb_gemv
@@ -30,6 +32,7 @@ int main() {
     // weights stay resident in the Infinity Cache across replays
     const int NW = getenv("MB_NW") ? atoi(getenv("MB_NW")) : 24;
     const bool talker_only = getenv("MB_TALKER") != nullptr;
+    const int NB = getenv("MB_BATCH") ? atoi(getenv("MB_BATCH")) : 1;
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipEvent_t e0, e1;
@@ -44,19 +47,20 @@ int main() {
             CK(hipMemset(w, 0x3c, wn * 2));
         }
         float *x, *y, *nw;
-        CK(hipMalloc(&x, s.C * 4 * 2));
-        CK(hipMalloc(&y, (size_t)s.R * 4 * 2));
+        CK(hipMalloc(&x, (size_t)s.C * 4 * NB));
+        CK(hipMalloc(&y, (size_t)s.R * 4 * NB));
         CK(hipMalloc(&nw, s.C * 4));
-        CK(hipMemset(x, 0, s.C * 8));
-        CK(hipMemset(y, 0, s.R * 8));
+        CK(hipMemset(x, 0, (size_t)s.C * 4 * NB));
+        CK(hipMemset(y, 0, (size_t)s.R * 4 * NB));
         CK(hipMemset(nw, 0, s.C * 4));
         for (int nt = 0; nt < 2; ++nt)
             for (int ks = 1; ks <= 32; ks *= 2) {
+                if (NB > 1 && (ks > 1 || nt != (s.name[0] == 't'))) continue;
                 if ((s.C / 64) % ks) continue;
                 if (s.epi == EPI_SWIGLU && ks > 4) continue;
                 GemvArgs a;
-                a.R = s.R; a.C = s.C; a.ksplit = ks; a.nt = nt; a.nb = 1; a.x = x; a.ldx = s.C; a.y = y;
-                a.ldy = s.R; a.epi = s.epi; a.norm_w = s.norm ? nw : nullptr;
+                a.R = s.R; a.C = s.C; a.ksplit = ks; a.nt = nt; a.nb = NB; a.x = x; a.ldx = s.C; a.y = y;
+                a.ldy = s.R; if (NB > 1) a.ksplit = 0; a.epi = s.epi; a.norm_w = s.norm ? nw : nullptr;
                 hipGraph_t g;
                 hipGraphExec_t ge;
                 CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
@@ -75,7 +79,9 @@ int main() {
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 const double us = ms * 1e3 / (5 * 96);
-                printf("%-28s ks=%2d nt=%d grid=%5d  %7.2f us  %6.0f GB/s\n", s.name, ks, nt, (s.R + 32 / ks - 1) / (32 / ks),
+                if (NB > 1) printf("B=%-2d %-28s %s nt=%d  %7.2f us  %6.0f GB/s\n", NB, s.name, qtts_last_kernel, nt, us,
+                                   wn * 2 / (us * 1e-6) / 1e9);
+                else printf("%-28s ks=%2d nt=%d grid=%5d  %7.2f us  %6.0f GB/s\n", s.name, ks, nt, (s.R + 32 / ks - 1) / (32 / ks),
                        us, wn * 2 / (us * 1e-6) / 1e9);
                 CK(hipGraphExecDestroy(ge));
                 CK(hipGraphDestroy(g));
