@@ -419,7 +419,68 @@ __global__ __launch_bounds__(256) void k_attn_short(AttnArgs a) {
     attn_short_wg<HD, false>(a, blockIdx.x, blockIdx.y, lq, sc);
 }
 
+// Short-context attention + the O projection split by kv head (the
+// sub-talker, GQA 2): workgroup (rb, kvh) recomputes kvh's attention (<= 16
+// keys, attn_short_wg; only rb == 0 stores the token's k / v) and multiplies
+// it with the 2*HD columns of W_o that head pair feeds, for RPW rows:
+// part[kvh][row] = W_o[row, 2 HD kvh .. 2 HD (kvh + 1)) . attn_kvh.
+// The consumer (the next GEMV's prologue, GemvArgs::xadd) sums the KV
+// partials in head order and adds the residual: x + o_proj(attn) of
+// T.c:667-676 with o_proj's dot split by head.
+// Lanes: LPS per row slot, 8 columns (16 B of bf16) per lane per load.
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, int R, float *part) {
+    constexpr int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, NJ = W2 / (8 * LPS), RPW = 256 / LPS;
+    __shared__ __attribute__((aligned(16))) float lq[4 * HD];
+    __shared__ __attribute__((aligned(16))) float att[W2];
+    __shared__ float sc[2 * 16];
+    const int tid = threadIdx.x, kvh = blockIdx.y, rb = blockIdx.x;
+    const int slot = tid / LPS, sub = tid - slot * LPS;
+    const int row = rb * RPW + slot, rowc = row < R ? row : R - 1;
+    const int AD = t.NH * HD;
+    // the weight fragment first: row `row`, columns W2*kvh + 8*(sub + LPS*j)
+    v4u wv[NJ];
+    const bf16_t *wr = Wo + (size_t)rowc * AD + W2 * kvh + 8 * sub;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
+    attn_short_wg<HD, false>(t, kvh, 0, lq, sc, att, rb == 0);
+    __syncthreads();
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        float f[8];
+        unpack8(wv[j], f);
+        const float *xp = att + 8 * (sub + LPS * j);
+        const float4 x0 = *reinterpret_cast<const float4 *>(xp);
+        const float4 x1 = *reinterpret_cast<const float4 *>(xp + 4);
+        acc = fmaf(f[0], x0.x, acc); acc = fmaf(f[1], x0.y, acc);
+        acc = fmaf(f[2], x0.z, acc); acc = fmaf(f[3], x0.w, acc);
+        acc = fmaf(f[4], x1.x, acc); acc = fmaf(f[5], x1.y, acc);
+        acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
+    }
+#pragma unroll
+    for (int o = LPS / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (sub == 0 && row < R) part[(size_t)kvh * R + row] = acc;
+}
+
 }  // namespace
+
+// Sub-talker attention + O projection by kv head (batch 1); 1 = not covered.
+int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st) {
+    const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
+    if (!(a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.S <= 16 && a.nrows == 1 &&
+          ((uintptr_t)Wo & 15) == 0 && (a.NH * a.HD) % 8 == 0))
+        return 1;
+    const int W2 = 2 * a.HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
+    const dim3 grid((R + RPW - 1) / RPW, a.KV);
+    switch (a.HD) {
+        case 128: hipLaunchKernelGGL((k_attn_o<128>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<128>"; break;
+        case 64: hipLaunchKernelGGL((k_attn_o<64>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<64>"; break;
+        case 32: hipLaunchKernelGGL((k_attn_o<32>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<32>"; break;
+        default: hipLaunchKernelGGL((k_attn_o<16>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<16>"; break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int qtts_attn_keys_per_split(int HD) { return HD >= 32 ? 256 / (HD / 32) : 256; }
 

@@ -402,6 +402,14 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
                             __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
         } else {
             v = *reinterpret_cast<const float4 *>(xrow + cc);
+            if (a.xadd) {   // residual + the O projection's per-head partials, summed in head order
+                float4 sacc = *reinterpret_cast<const float4 *>(a.xadd + cc);
+                for (int p = 1; p < a.n_xadd; ++p) {
+                    const float4 t = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + cc);
+                    sacc.x += t.x; sacc.y += t.y; sacc.z += t.z; sacc.w += t.w;
+                }
+                v.x += sacc.x; v.y += sacc.y; v.z += sacc.z; v.w += sacc.w;
+            }
         }
         if (c >= C) v = make_float4(0.f, 0.f, 0.f, 0.f);
         xv[i] = v;
@@ -486,6 +494,10 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     GemvArgs a = in;
     if (a.C % 64 || a.nb < 1 || a.nb > 16 || a.R < 1) {
         fprintf(stderr, "qtts_gemv: unsupported shape R=%d C=%d nb=%d\n", a.R, a.C, a.nb);
+        return -1;
+    }
+    if (a.xadd && !(a.nb == 1 && a.C <= 8192 && a.ldx_ok1())) {
+        fprintf(stderr, "qtts_gemv: xadd needs the batch-1 path (R=%d C=%d nb=%d)\n", a.R, a.C, a.nb);
         return -1;
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {

@@ -226,8 +226,12 @@ __device__ __forceinline__ void attn_full_wg(const AttnArgs &a, int kvh, int r, 
 // Device function: also the tail of the fused QKV GEMV (k_gemv.hip), where
 // the q|k|v row was written by other workgroups of the same launch (SC1:
 // read it with write-through loads).  lq: 4*HD floats, scs: 2*16 floats of LDS.
+// lout != nullptr: the 2*HD outputs go to LDS lout (the caller barriers);
+// wcache = false: the token's k / v are used but not stored (another
+// workgroup of the launch stores them).
 template <int HD, bool SC1>
-__device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r, float *lq, float *scs) {
+__device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r, float *lq, float *scs,
+                                              float *lout = nullptr, bool wcache = true) {
     constexpr int D4 = HD / 4, LPK = HD / 16, NK = 16;
     float (*sc)[NK] = reinterpret_cast<float (*)[NK]>(scs);
     const int tid = threadIdx.x;
@@ -285,7 +289,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
             }
         }
         reinterpret_cast<float4 *>(lq)[tid] = y;
-        if (seg >= 2 && !(a.skip && a.skip[r])) {
+        if (seg >= 2 && wcache && !(a.skip && a.skip[r])) {
             float *dst = (seg == 2 ? a.kc : a.vc) + ((size_t)r * a.S + p) * KVD + kvh * HD;
             reinterpret_cast<float4 *>(dst)[l] = y;
         }
@@ -331,6 +335,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
 #pragma unroll
         for (int t = 0; t < NK; ++t)
             if (t < n) acc += sc[go][t] * (t == p ? lq[3 * HD + dd] : vr[t]);
-        a.out[(size_t)r * a.ld_out + (2 * kvh + go) * HD + dd] = acc;
+        if (lout) lout[go * HD + dd] = acc;
+        else a.out[(size_t)r * a.ld_out + (2 * kvh + go) * HD + dd] = acc;
     }
 }

@@ -23,6 +23,10 @@ struct GemvArgs {
     int ids_bstride = 1, ids_rstride = 0, ids_off = 0;
     const int *row_sel = nullptr;
     // prologue
+    // batch-1 prologue only: x += sum_p xadd[p*ld_xadd + c] (p < n_xadd, summed
+    // in order first) -- the O projection's per-head partials (qtts_attn_o)
+    const float *xadd = nullptr;
+    int n_xadd = 0, ld_xadd = 0;
     const float *norm_w = nullptr;  // RMSNorm weights [C] (nullptr: no norm)
     float eps = 1e-6f;
     float *xcopy = nullptr;         // workgroup 0 writes x rows here
@@ -35,6 +39,7 @@ struct GemvArgs {
     int epi = EPI_STORE;
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {
+        if (xadd && (table || table_f32 || ((uintptr_t)xadd & 15) || ld_xadd % 4 || n_xadd < 1)) return false;
         if (table) return C % 4 == 0;
         const bool nw_ok = !norm_w || ((uintptr_t)norm_w & 15) == 0;
         if (table_f32) return C % 4 == 0 && ((uintptr_t)table_f32 & 15) == 0 && nw_ok;
@@ -75,6 +80,9 @@ int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st);
 // O projection with the short-context decode attention as its prologue
 // (qtts_attn_pro.h); 1 = not covered
 int qtts_gemv_att(GemvArgs a, const AttnArgs &t, int target_wg, hipStream_t st);
+// sub-talker attention + O projection split by kv head: part [KV][R]
+// (batch 1, GQA 2, <= 16 keys); 1 = not covered
+int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st);
 
 // Name of the kernel instantiation the last launcher on this thread chose
 // (diagnostics: per-kernel profile rows match rocprofv3's kernel names).

@@ -97,6 +97,7 @@ struct qtts_dev {
     // state
     int nb = 0, nrun = 0, max_frames = 0, S = 0, p_cap = 0, tr_cap = 0, rows_cap = 0;  // nb: allocated slots (strides), nrun: rows launched
     float *x_tk = nullptr, *qkv = nullptr, *att = nullptr, *hbuf = nullptr, *logits = nullptr, *tk_hid = nullptr;
+    float *x_st2 = nullptr, *opart = nullptr;   // attn_o: second residual buffer, per-head O partials
     float *x_st = nullptr, *qkv_s = nullptr, *att_s = nullptr, *h_s = nullptr, *logits_s = nullptr;
     float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
     int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
@@ -130,6 +131,7 @@ struct qtts_dev {
     bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
     bool att_pro = false;    // QTTS_HIP_ATT_PRO=1: sub-talker attention as the O GEMV's prologue
                              // (measured slower: profiles/r01d_envsweep.txt)
+    bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
     int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
@@ -336,6 +338,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->use_mfma = !(nm && atoi(nm));
     const char *ap = getenv("QTTS_HIP_ATT_PRO");
     dv->att_pro = ap && atoi(ap);
+    const char *ao = getenv("QTTS_HIP_ATTN_O");
+    dv->attn_o = !(ao && !atoi(ao));
     const char *aw = getenv("QTTS_HIP_ATT_PRO_WG");
     if (aw && atoi(aw) > 0) dv->att_pro_wg = atoi(aw);
     codec_init(&dv->codec, dims, dv->st);
@@ -445,6 +449,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(logits, float, B * d.V);
     A(tk_hid, float, B * d.H);
     A(x_st, float, B * d.Hs);
+    A(x_st2, float, B * d.Hs);
+    A(opart, float, (size_t)d.KVs * d.Hs);
     A(qkv_s, float, B * dv->QKVs());
     A(att_s, float, B * d.NHs * d.HDs);
     A(h_s, float, B * d.Is);
@@ -743,9 +749,13 @@ static int subtalker(qtts_dev *dv) {
             a.nt = 0;
             CKI(pgemv(dv, a, PK_GEMV_SUB));
         }
+        // attn_o (batch 1): attention + O projection by kv head into per-head
+        // partials, summed with the residual in the gate|up GEMV's prologue,
+        // which writes the new residual to the other buffer (xa -> xb)
+        float *xa = dv->x_st, *xb = dv->x_st2;
         for (int l = 0; l < d.Ls; ++l) {
             Layer &ly = dv->sl[l];
-            GemvArgs a = gv(ly.wqkv, QKV, d.Hs, dv->x_st, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
+            GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             AttnArgs t;
@@ -755,9 +765,22 @@ static int subtalker(qtts_dev *dv) {
             t.pos = nullptr; t.pos_const = g; t.NH = d.NHs; t.KV = d.KVs; t.HD = d.HDs; t.out = dv->att_s;
             t.ld_out = AD; t.nrows = nb; t.skip = dv->stopped;
             t.cnt = dv->att_cnt;
-            GemvArgs o = gv(ly.wo, d.Hs, AD, dv->att_s, AD, dv->x_st, d.Hs, nb, EPI_RESID);
+            GemvArgs o = gv(ly.wo, d.Hs, AD, dv->att_s, AD, xa, d.Hs, nb, EPI_RESID);
             o.nt = 0;
-            if (dv->att_pro && nb == 1 && att_pro_ok(t, AD)) {
+            bool fused_o = false;
+            if (dv->attn_o && nb == 1 && !dv->att_pro && !dv->fuse_st) {
+                CKI(pgemv(dv, a, PK_GEMV_SUB));
+                ProfScope ps(dv, PK_ATTN, (double)d.Hs * AD * 2);
+                const int rc = qtts_attn_o(t, ly.wo, d.Hs, dv->opart, st);
+                if (rc < 0) return -1;
+                if (rc == 1) {   // not covered: the attention kernel, then the O GEMV below
+                    ps.cancel();
+                    { ProfScope pa(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
+                    CKI(pgemv(dv, o, PK_GEMV_SUB));
+                } else {
+                    fused_o = true;
+                }
+            } else if (dv->att_pro && nb == 1 && att_pro_ok(t, AD)) {
                 // q|k|v rows, then attention (as the prologue) + O projection + residual
                 CKI(pgemv(dv, a, PK_GEMV_SUB));
                 CKI(pgemv_att(dv, o, t, PK_GEMV_SUB));
@@ -765,15 +788,21 @@ static int subtalker(qtts_dev *dv) {
                 CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
                 CKI(pgemv(dv, o, PK_GEMV_SUB));
             }
-            a = gv(ly.wgu, 2 * d.Is, d.Hs, dv->x_st, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
+            a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
+            if (fused_o) {
+                a.xadd = dv->opart; a.n_xadd = d.KVs; a.ld_xadd = d.Hs;
+                a.xcopy = xb; a.ldxc = d.Hs; a.xcopy_normed = 0;
+            }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
-            a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, dv->x_st, d.Hs, nb, EPI_RESID);
+            float *xo = fused_o ? xb : xa;
+            a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xo, d.Hs, nb, EPI_RESID);
             a.nt = 0;
             CKI(pgemv(dv, a, PK_GEMV_SUB));
+            if (fused_o) std::swap(xa, xb);
         }
         if (g == 0) continue;  // pass 0 produces no logits
-        GemvArgs a = gv(dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, dv->x_st, d.Hs, dv->logits_s, d.Vs, nb,
+        GemvArgs a = gv(dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, xa, d.Hs, dv->logits_s, d.Vs, nb,
                         EPI_STORE);
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
         SampArgs s;
