@@ -286,6 +286,26 @@ struct G1Stream {
     // dot of this lane's share with xs (LDS), reduced over the slot's 8 lanes
     __device__ __forceinline__ float run(const float *xs) {
         float acc = 0.f;
+        if constexpr (U1 >= 16) {   // one group (nblk <= U1, launcher): every load already issued
+#pragma unroll
+            for (int u = 0; u < U1; ++u) {
+                if (u < nblk) {
+                    float f[8];
+                    unpack8(wv[u], f);
+                    const int cl = 64 * (ks + u * ksn) + 8 * sub;
+                    const float4 x0 = *reinterpret_cast<const float4 *>(xs + cl);
+                    const float4 x1 = *reinterpret_cast<const float4 *>(xs + cl + 4);
+                    acc = fmaf(f[0], x0.x, acc); acc = fmaf(f[1], x0.y, acc);
+                    acc = fmaf(f[2], x0.z, acc); acc = fmaf(f[3], x0.w, acc);
+                    acc = fmaf(f[4], x1.x, acc); acc = fmaf(f[5], x1.y, acc);
+                    acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
+                }
+            }
+            acc += __shfl_xor(acc, 1, 64);
+            acc += __shfl_xor(acc, 2, 64);
+            acc += __shfl_xor(acc, 4, 64);
+            return acc;
+        }
         for (int g = 0; g < ng; ++g) {
             v4u cur[U1];
 #pragma unroll
@@ -365,17 +385,19 @@ __device__ __forceinline__ void g1_epilogue(const GemvArgs &a, float acc, float 
 // (replayed at 64 cycles each, cdna_hip_programming.md Guideline 17).
 constexpr int G1_HEAD = 4;   // floats in front of xs
 
+// Block size: 256 threads (the tails), or up to 1024 ("wide": one workgroup
+// per CU streaming R/256 rows, qtts_gemv) -- nslot = blockDim/8 slots.
 template <int U1, int XV, bool NT, int TAIL>
-__global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
+__global__ __launch_bounds__(TAIL == 0 ? 1024 : 256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
-    const int ksn = a.ksplit, RPW = 32 / ksn;
+    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7, nthr = blockDim.x, nslot = nthr >> 3;
+    const int ksn = a.ksplit, RPW = nslot / ksn;
     const int rloc = slot % RPW, ks = slot / RPW;
     const int row0 = blockIdx.x * RPW, row = row0 + rloc;
     const int C = a.C;
     float *xs = smem + G1_HEAD;   // [C]
-    float *red = xs + C;          // [32]
-    float *bred = red + 32;       // [4]
+    float *red = xs + C;          // [nslot]
+    float *bred = red + nslot;    // [nthr / 64]
     G1Stream<U1, NT> ws(a, row, ks, ksn, sub);
     ws.load(0);
 
@@ -393,7 +415,7 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int c = 4 * tid + 1024 * i;
+        const int c = 4 * (tid + nthr * i);
         const int cc = c < C ? c : C - 4;
         float4 v;
         if (trow) {
@@ -423,12 +445,14 @@ __global__ __launch_bounds__(256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
         ss = wave_sum(ss);
         if ((tid & 63) == 0) bred[tid >> 6] = ss;
         __syncthreads();
-        inv = rms_inv(bred[0] + bred[1] + bred[2] + bred[3], C, a.eps);
+        float st = bred[0];
+        for (int k = 1; k < (nthr >> 6); ++k) st += bred[k];
+        inv = rms_inv(st, C, a.eps);
     }
     const bool cp = a.xcopy && blockIdx.x == 0;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int c = 4 * tid + 1024 * i;
+        const int c = 4 * (tid + nthr * i);
         if (c < C) {
             float4 v = xv[i];
             if (cp && !a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + c) = v;
@@ -490,6 +514,33 @@ static int pick_ksplit(int R, int C, int epi, int target) {
     return ks;
 }
 
+// "Wide" batch-1 configuration: about one workgroup per CU (grid ~ 256),
+// each streaming ceil(R / 256) rows with up to 1024 threads, so the grid runs
+// in one round and x is staged 256 times instead of once per 32-row block.
+// QTTS_HIP_GEMV_WIDE = 0 / 1 / 2: off / talker (non-temporal) weights only /
+// every batch-1 GEMV.
+static bool gemv_wide(int nt) {
+    static const int mode = [] {
+        const char *e = getenv("QTTS_HIP_GEMV_WIDE");
+        return e ? atoi(e) : 1;
+    }();
+    return mode == 2 || (mode == 1 && nt);
+}
+static void wide_config(int R, int C, int epi, int &ks_out, int &nthr_out) {
+    const int nb64 = C / 64, quad = epi == EPI_SWIGLU ? 8 : 1;
+    int rows = (R + 255) / 256;
+    rows = (rows + quad - 1) / quad * quad;
+    for (int ks = 32; ks >= 1; ks /= 2) {
+        if (nb64 % ks || (epi == EPI_SWIGLU && ks > 4)) continue;
+        int rpw = rows;
+        while ((rpw * ks) % 8) rpw += quad;   // whole waves of 8 slots
+        if (rpw * ks > 128) continue;
+        ks_out = ks;
+        nthr_out = rpw * ks * 8;
+        return;
+    }
+}
+
 int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     GemvArgs a = in;
     if (a.C % 64 || a.nb < 1 || a.nb > 16 || a.R < 1) {
@@ -501,22 +552,30 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         return -1;
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
+        int nthr = 256;
+        if (a.ksplit <= 0 && gemv_wide(a.nt)) {
+            wide_config(a.R, a.C, a.epi, a.ksplit, nthr);
+        }
         if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
-        const int rpw = 32 / a.ksplit;
+        const int rpw = nthr / 8 / a.ksplit;
         const int grid = (a.R + rpw - 1) / rpw;
         const int nblk = a.C / 64 / a.ksplit;
-        const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
-        const size_t smem = (size_t)(G1_HEAD + a.C + 36) * sizeof(float);
+        const int xq = (a.C + 4 * nthr - 1) / (4 * nthr);
+        const int xv = xq <= 1 ? 1 : xq <= 2 ? 2 : xq <= 4 ? 4 : 8;
+        const size_t smem = (size_t)(G1_HEAD + a.C + nthr / 8 + 16) * sizeof(float);
         const TailA<0> t0{0};
 #define QTTS_G1(U, X)                                                                                 \
         if (a.nt) {                                                                                   \
-            hipLaunchKernelGGL((k_gemv1<U, X, true, 0>), dim3(grid), dim3(256), smem, st, a, t0);     \
+            hipLaunchKernelGGL((k_gemv1<U, X, true, 0>), dim3(grid), dim3(nthr), smem, st, a, t0);    \
             qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 0>";                                    \
         } else {                                                                                      \
-            hipLaunchKernelGGL((k_gemv1<U, X, false, 0>), dim3(grid), dim3(256), smem, st, a, t0);    \
+            hipLaunchKernelGGL((k_gemv1<U, X, false, 0>), dim3(grid), dim3(nthr), smem, st, a, t0);   \
             qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 0>";                                   \
         }
-        if (nblk >= 8) {
+        if (nthr != 256 && nblk > 8 && nblk <= 16) {   // wide: every weight load of a lane in one group
+            switch (xv) { case 1: QTTS_G1(16, 1) break; case 2: QTTS_G1(16, 2) break;
+                          case 4: QTTS_G1(16, 4) break; default: QTTS_G1(8, 8) break; }
+        } else if (nblk >= 8) {
             switch (xv) { case 1: QTTS_G1(8, 1) break; case 2: QTTS_G1(8, 2) break;
                           case 4: QTTS_G1(8, 4) break; default: QTTS_G1(8, 8) break; }
         } else {

@@ -54,9 +54,10 @@ int main() {
         CK(hipMemset(y, 0, (size_t)s.R * 4 * NB));
         CK(hipMemset(nw, 0, s.C * 4));
         for (int nt = 0; nt < 2; ++nt)
-            for (int ks = 1; ks <= 32; ks *= 2) {
+            for (int ks = 0; ks <= 32; ks = ks ? 2 * ks : 1) {   // ks 0: the launcher's own choice
                 if (NB > 1 && (ks > 1 || nt != (s.name[0] == 't'))) continue;
-                if ((s.C / 64) % ks) continue;
+                if (getenv("MB_AUTO") && ks != 0) continue;
+                if (ks && (s.C / 64) % ks) continue;
                 if (s.epi == EPI_SWIGLU && ks > 4) continue;
                 GemvArgs a;
                 a.R = s.R; a.C = s.C; a.ksplit = ks; a.nt = nt; a.nb = NB; a.x = x; a.ldx = s.C; a.y = y;
@@ -81,7 +82,8 @@ int main() {
                 const double us = ms * 1e3 / (5 * 96);
                 if (NB > 1) printf("B=%-2d %-28s %s nt=%d  %7.2f us  %6.0f GB/s\n", NB, s.name, qtts_last_kernel, nt, us,
                                    wn * 2 / (us * 1e-6) / 1e9);
-                else printf("%-28s ks=%2d nt=%d grid=%5d  %7.2f us  %6.0f GB/s\n", s.name, ks, nt, (s.R + 32 / ks - 1) / (32 / ks),
+                else printf("%-28s %-26s ks=%2d nt=%d grid=%5d  %7.2f us  %6.0f GB/s\n", s.name, ks ? "" : qtts_last_kernel,
+                            ks, nt, ks ? (s.R + 32 / ks - 1) / (32 / ks) : 0,
                        us, wn * 2 / (us * 1e-6) / 1e9);
                 CK(hipGraphExecDestroy(ge));
                 CK(hipGraphDestroy(g));
