@@ -177,13 +177,16 @@ __global__ __launch_bounds__(256) void k_xgemm(XGemm g) {
 // The next stage's loads are in registers while the MFMAs consume this one.
 constexpr int CV_BM = 64, CV_BN = 128, CV_BC = 16, CV_HALO = 64;   // halo >= (Kw-1)*dil (host-checked)
 
-// blockIdx.z: transposed-conv output phase (tconv_run): weights g.wt + z*KW*M*ci,
-// outputs at column n*stride + phase + z
+// blockIdx.z = phase * kz + split: the transposed-conv output phase
+// (tconv_run: weights g.wt + phase*KW*M*ci, outputs at column
+// n*stride + phase) and, when g.kz > 1, the input-channel split whose raw
+// partial tile goes to g.part[z][M][N] (k_conv_reduce applies the epilogue).
 template <int KW>
 __global__ __launch_bounds__(256) void k_conv(XGemm g) {
-    if (blockIdx.z) {
-        g.wt += (size_t)blockIdx.z * KW * g.M * (g.K / KW);
-        g.phase += blockIdx.z;
+    const int nzk = g.kz > 1 ? g.kz : 1, ph = blockIdx.z / nzk, kzi = blockIdx.z - ph * nzk;
+    if (ph) {
+        g.wt += (size_t)ph * KW * g.M * (g.K / KW);
+        g.phase += ph;
     }
     constexpr int NBW = CV_BN + CV_HALO;                     // staged window columns
     constexpr int NA4 = KW * CV_BM * CV_BC / 4 / 256;       // float4 weight loads per thread (ceil below)
@@ -196,6 +199,7 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
     const int m0 = blockIdx.y * CV_BM, n0 = blockIdx.x * CV_BN;
     const int wm = (wave >> 1) * 32, wn = (wave & 1) * 64;
     const int ci = g.K / KW, dil = g.dil, t0 = n0 - g.pad;
+    const int cpz = ci / nzk, cbeg = kzi * cpz, cend = cbeg + cpz;   // this split's input channels
     const int win = CV_BN + (KW - 1) * dil;                  // columns actually needed
     floatx16 acc0, acc1;
 #pragma unroll
@@ -223,8 +227,8 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
             rb[j] = v;
         }
     };
-    load(0);
-    for (int c0 = 0; c0 < ci; c0 += CV_BC) {
+    load(cbeg);
+    for (int c0 = cbeg; c0 < cend; c0 += CV_BC) {
 #pragma unroll
         for (int j = 0; j < NA4C; ++j) {
             const int e = tid + 256 * j;
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
             if (c < CV_BC) Bs[c][x] = rb[j];
         }
         __syncthreads();
-        if (c0 + CV_BC < ci) load(c0 + CV_BC);
+        if (c0 + CV_BC < cend) load(c0 + CV_BC);
 #pragma unroll
         for (int tap = 0; tap < KW; ++tap) {
             const int sh = tap * dil;
@@ -256,13 +260,110 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
         }
         __syncthreads();
     }
+    float *pz = nzk > 1 ? g.part + (size_t)blockIdx.z * g.M * g.N : nullptr;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int n = n0 + wn + (lane & 31);
         if (m >= g.M) continue;
+        if (pz) {
+            if (n < g.N) pz[(size_t)m * g.N + n] = acc0[r];
+            if (n + 32 < g.N) pz[(size_t)m * g.N + n + 32] = acc1[r];
+            continue;
+        }
         if (n < g.N) xg_epi(g, m, n, acc0[r]);
         if (n + 32 < g.N) xg_epi(g, m, n + 32, acc1[r]);
+    }
+}
+
+// sum of k_conv's channel-split partials (in split order) + the epilogue, per
+// (phase, m, n)
+__global__ void k_conv_reduce(XGemm g, int nph) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x, mn = (size_t)g.M * g.N;
+    if (idx >= mn * nph) return;
+    const int ph = (int)(idx / mn);
+    const size_t e = idx - (size_t)ph * mn;
+    const float *p = g.part + (size_t)ph * g.kz * mn + e;
+    float v = p[0];
+    for (int z = 1; z < g.kz; ++z) v += p[(size_t)z * mn];
+    g.phase += ph;
+    xg_epi(g, (int)(e / g.N), (int)(e % g.N), v);
+}
+
+// Weight-streaming GEMV for the codec's linears at M <= 4 rows (the first-
+// packet / small-chunk streaming decode: transformer, ConvNeXt pointwise
+// convs at T = 1..4 frames).  C[m][n] = sum_k A(m, k) * W[n][k] with fp32
+// weights W (ldb), A rows (XA_ROWS) or columns (XA_TRANS).  256 threads = 32
+// slots x 8 lanes; a lane loads 16 B (4 floats) per 32-column block; a row's
+// blocks are dealt to KS slots; A is staged in LDS; epilogue xg_epi.
+constexpr int XV_U = 8;   // loads in flight per lane
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_xgemv(XGemm g, int ks) {
+    extern __shared__ __attribute__((aligned(16))) float xsm[];
+    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
+    const int RPW = 32 / ks, rloc = slot % RPW, kss = slot / RPW;
+    const int n0 = blockIdx.x * RPW, n = n0 + rloc, nc = n < g.N ? n : g.N - 1;
+    const int K = g.K, M = g.M;
+    float *xs = xsm;                 // [M][K]
+    float *red = xs + 4 * K;         // [32][4]
+    const floatx4v *wr = reinterpret_cast<const floatx4v *>(g.B + (size_t)nc * g.ldb) + sub;
+    const int nblk = K / 32 / ks;
+    floatx4v wv[XV_U];
+    auto load = [&](int j0) {
+#pragma unroll
+        for (int u = 0; u < XV_U; ++u) {
+            int j = j0 + u;
+            j = j < nblk ? j : nblk - 1;
+            wv[u] = __builtin_nontemporal_load(wr + 8 * (kss + j * ks));
+        }
+    };
+    load(0);
+    for (int i = tid; i < M * K; i += 256) {
+        const int m = i / K, k = i - m * K;
+        xs[i] = g.amode == XA_TRANS ? g.A[(size_t)k * g.lda + m] : g.A[(size_t)m * g.lda + k];
+    }
+    __syncthreads();
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = 0; j0 < nblk; j0 += XV_U) {
+        floatx4v cur[XV_U];
+#pragma unroll
+        for (int u = 0; u < XV_U; ++u) cur[u] = wv[u];
+        if (j0 + XV_U < nblk) load(j0 + XV_U);
+#pragma unroll
+        for (int u = 0; u < XV_U; ++u) {
+            if (j0 + u < nblk) {
+                const int c = 32 * (kss + (j0 + u) * ks) + 4 * sub;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    if (m < M) {
+                        const float4 x = *reinterpret_cast<const float4 *>(xs + m * K + c);
+                        acc[m] = fmaf(cur[u][0], x.x, acc[m]); acc[m] = fmaf(cur[u][1], x.y, acc[m]);
+                        acc[m] = fmaf(cur[u][2], x.z, acc[m]); acc[m] = fmaf(cur[u][3], x.w, acc[m]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        float v = acc[m];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        acc[m] = v;
+    }
+    if (sub == 0) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) red[(kss * RPW + rloc) * 4 + m] = acc[m];
+    }
+    __syncthreads();
+    if (tid < RPW * M) {
+        const int rl = tid / M, m = tid - rl * M, nn = n0 + rl;
+        if (nn < g.N) {
+            float v = red[rl * 4 + m];
+            for (int k2 = 1; k2 < ks; ++k2) v += red[(k2 * RPW + rl) * 4 + m];
+            xg_epi(g, m, nn, v);
+        }
     }
 }
 
@@ -310,17 +411,21 @@ __global__ void k_rvq_sum(const int *codes, int T, int Q, int CB, int vq, const 
     ss[(size_t)k * T + t] = s;
     as[(size_t)k * T + t] = a;
 }
-// output projections (1x1, no bias) summed (Cd.c:178-255), sequential sums
+// output projections (1x1, no bias) summed (Cd.c:178-255): one wave per
+// output (o, t), lanes stride over k, shuffle-tree sums (s1 + s2 as the reference)
 __global__ void k_rvq_proj(const float *ps, const float *pa, const float *ss, const float *as, int vq, int half, int T,
                            int ldo, float *out) {
-#pragma clang fp contract(off)
-    const int idx = blockIdx.x * 256 + threadIdx.x;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (idx >= half * T) return;
     const int o = idx / T, t = idx - o * T;
     float s1 = 0.f, s2 = 0.f;
-    for (int k = 0; k < vq; ++k) s1 += ps[(size_t)o * vq + k] * ss[(size_t)k * T + t];
-    for (int k = 0; k < vq; ++k) s2 += pa[(size_t)o * vq + k] * as[(size_t)k * T + t];
-    out[(size_t)o * ldo + t] = s1 + s2;
+    for (int k = lane; k < vq; k += 64) {
+        s1 = fmaf(ps[(size_t)o * vq + k], ss[(size_t)k * T + t], s1);
+        s2 = fmaf(pa[(size_t)o * vq + k], as[(size_t)k * T + t], s2);
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) out[(size_t)o * ldo + t] = s1 + s2;
 }
 // depthwise causal conv k=7 (ConvNeXt dwconv), reference order b + sum_k
 // (ldx / ldy: row strides; tmin < 0 reads the streaming history in the margin)
@@ -416,6 +521,7 @@ __global__ void k_iota(int *p, int n, int zero) {
 // come in whole stages, the window halo fits and the output fills the chip
 // (small first-packet decodes keep the split-K GEMM).  QTTS_HIP_CONV=0 / 1
 // disables / forces it (tests).
+static int conv_splits(const XGemm &g);
 static bool conv_ok(const XGemm &g) {
     static const char *f = getenv("QTTS_HIP_CONV");
     if (f && !atoi(f)) return false;
@@ -426,22 +532,58 @@ static bool conv_ok(const XGemm &g) {
         (g.Kw - 1) * g.dil > CV_HALO || ((uintptr_t)g.wt & 15))
         return false;
     const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM) * (g.stride > 1 ? g.stride : 1);
-    return (f && atoi(f)) || tiles >= min_tiles;
+    return (f && atoi(f)) || tiles >= min_tiles || (g.part && conv_splits(g) > 1);
 }
 
-static int conv_launch(const XGemm &g, int nz, hipStream_t st) {
-    const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM, nz);
+// input-channel splits for a grid that would not fill the chip: up to 1024
+// workgroups, >= 2 channel stages each (QTTS_HIP_CONV_SPLIT=0 disables)
+static int conv_splits(const XGemm &g) {
+    static const char *f = getenv("QTTS_HIP_CONV_SPLIT");
+    if ((f && !atoi(f)) || !g.part) return 1;
+    const int nph = g.stride > 1 ? g.stride : 1;
+    const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM) * nph;
+    const int ci = g.K / g.Kw;
+    int nz = 1;
+    while (tiles * nz * 2 <= 1024 && (ci / CV_BC) % (nz * 2) == 0 && ci / CV_BC / (nz * 2) >= 2 &&
+           (size_t)nz * 2 * nph * g.M * g.N <= g.part_elems)
+        nz *= 2;
+    return nz;
+}
+
+static int conv_launch(const XGemm &gin, int nph, hipStream_t st) {
+    XGemm g = gin;
+    g.kz = conv_splits(g);
+    const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM, nph * g.kz);
     switch (g.Kw) {
         case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
         case 3: hipLaunchKernelGGL(k_conv<3>, cg, dim3(256), 0, st, g); break;
         case 2: hipLaunchKernelGGL(k_conv<2>, cg, dim3(256), 0, st, g); break;
         default: hipLaunchKernelGGL(k_conv<1>, cg, dim3(256), 0, st, g); break;
     }
+    if (g.kz > 1) {
+        const size_t n = (size_t)nph * g.M * g.N;
+        hipLaunchKernelGGL(k_conv_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, nph);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// k_xgemv covers a linear at <= 4 rows (QTTS_HIP_XGEMV=0 disables)
+static bool xgemv_ok(const XGemm &g) {
+    static const char *f = getenv("QTTS_HIP_XGEMV");
+    if (f && !atoi(f)) return false;
+    return g.M <= 4 && g.bmode == XB_WT && (g.amode == XA_ROWS || g.amode == XA_TRANS) && g.K % 256 == 0 &&
+           g.ldb % 4 == 0 && ((uintptr_t)g.B & 15) == 0 && (size_t)4 * g.K * 4 + 512 <= 64 * 1024;
 }
 
 int qtts_xgemm(const XGemm &g, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
+    if (xgemv_ok(g)) {
+        int ks = 1;   // KSPLIT: grid >= 512 workgroups, >= 1 block per lane
+        while (ks < 32 && (g.N + 32 / ks - 1) / (32 / ks) < 512 && g.K / 32 / (2 * ks) >= 1) ks *= 2;
+        const int rpw = 32 / ks;
+        hipLaunchKernelGGL(k_xgemv, dim3((g.N + rpw - 1) / rpw), dim3(256), (size_t)(4 * g.K + 128) * 4, st, g, ks);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (conv_ok(g)) return conv_launch(g, g.stride > 1 ? g.stride : 1, st);
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, 1);
     // split-K when the output has too few tiles to fill the chip (first-packet
@@ -751,6 +893,8 @@ static int tconv_run(CodecModel *m, const XGemm &g, hipStream_t st) {
     XGemm c = g;
     c.amode = XA_ROWS; c.A = nullptr; c.bmode = XB_CONV; c.Kw = nt; c.dil = 1; c.pad = nt - 1; c.phase = 0;
     c.wt = (const float *)16;  // shape-only probe before the relayout is made
+    c.part = m->xg_part;
+    c.part_elems = m->xg_part_elems;
     if (conv_ok(c)) {
         c.wt = ctwt(m, g.A, ci, g.co, g.Kw, s, st);
         if (c.wt) return xgm(m, c, st);
@@ -840,7 +984,7 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
     // 1. RVQ dequantise -> A [half][T]
     hipLaunchKernelGGL(k_rvq_sum, dim3(T), dim3(vq < 64 ? 64 : (vq + 63) / 64 * 64), 0, st, codes, T, d.cq, d.ccb, vq,
                        m->cb, B, Cb);
-    hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 255) / 256), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 3) / 4), dim3(256), 0, st,
                        cw(m, "decoder.quantizer.rvq_first.output_proj.weight"),
                        cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), B, Cb, vq, half, T, T, A);
     // 2. pre-conv k=3 -> B [lat][T]
@@ -1237,7 +1381,7 @@ int codec_stream_push_to(CodecModel *m, const int *codes, int ldc_codes, int Tto
         // 1. RVQ dequantise -> A [half][T]
         hipLaunchKernelGGL(k_rvq_sum, dim3(T), dim3(vq < 64 ? 64 : (vq + 63) / 64 * 64), 0, st,
                            codes + (size_t)t0 * d.cq, T, d.cq, d.ccb, vq, m->cb, S.rvq_s, S.rvq_a);
-        hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 255) / 256), dim3(256), 0, st,
+        hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 3) / 4), dim3(256), 0, st,
                            cw(m, "decoder.quantizer.rvq_first.output_proj.weight"),
                            cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), S.rvq_s, S.rvq_a, vq, half, T, ld, A);
         // 2. pre-conv k3 -> B

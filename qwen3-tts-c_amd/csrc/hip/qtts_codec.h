@@ -111,5 +111,6 @@ struct XGemm {
     int tmin = 0;                              // conv/tconv input columns t >= tmin are read (t < 0: the
                                                // streaming history kept in the buffer's left margin)
     const float *wt = nullptr;                 // XB_CONV: the weights as [Kw][M][K/Kw] (k_conv's layout)
+    int kz = 0;                                // k_conv split over input channels (set by the launcher)
 };
 int qtts_xgemm(const XGemm &g, hipStream_t st);
