@@ -587,7 +587,11 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
         c.y = a.y + (size_t)r0 * ys;
         c.nb = nr;
         int rc = 1;
-        if (nr >= 2 && dv->use_mfma) rc = qtts_mgemm(c, dv->pinv, dv->st);
+        // <= 16 rows (a custom-voice prompt): the batch decode kernel (k_gemvm,
+        // x split once per workgroup, ~1 round over the CUs) streams the
+        // weights faster than the 64-row prefill GEMM
+        if (nr >= 2 && nr <= 16 && dv->use_mfma) rc = qtts_gemvm(c, dv->st);
+        if (rc == 1 && nr >= 2 && dv->use_mfma) rc = qtts_mgemm(c, dv->pinv, dv->st);
         if (rc < 0) return -1;
         if (rc == 1) {
             nr = nr < 16 ? nr : 16;
