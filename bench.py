@@ -19,7 +19,9 @@ Also reported:
   first_packet_ms  generate() entry -> first 1920 samples available: prefill +
                    frame 0 + codec decode of that frame (the codec is causal,
                    so the first frame decodes on its own; measured after the
-                   timed region)
+                   timed region, on the process's second streaming request:
+                   the first also allocates the streaming codec's state and is
+                   reported as detail.first_packet_cold_ms)
   roofline         dominant kernel (weight-streaming GEMV), measured live with
                    HIP events on the context stream over one eager frame
   cpu_baseline     the reference c/ build (oracle/_ref/qwen-tts, scalar+OpenMP)
@@ -269,9 +271,16 @@ def main():
     if args.batch == 1:
         m.generate(prompts[0], "aiden", "english")       # non-streaming breakdown
         prefill_ms, talker_ms, codec_ms = m.c.perf_prefill_ms, m.c.perf_talker_ms, m.c.perf_codec_ms
+        # the first streaming request of the process also allocates the
+        # streaming codec's state (reported as first_packet_cold_ms); the line
+        # reports the second request, as a serving process sees it
         first = []
         m.generate_stream(prompts[0], "aiden", "english", chunk_frames=8, on_chunk=first.append)
-        fp = dict(first_packet_ms=m.c.perf_first_packet_ms, first_frame_ms=m.c.perf_first_frame_ms,
+        cold_ms = m.c.perf_first_packet_ms
+        first = []
+        m.generate_stream(prompts[0], "aiden", "english", chunk_frames=8, on_chunk=first.append)
+        fp = dict(first_packet_ms=m.c.perf_first_packet_ms, first_packet_cold_ms=cold_ms,
+                  first_frame_ms=m.c.perf_first_frame_ms,
                   first_packet_samples=int(len(first[0])) if first else 0, stream_chunk_frames=8,
                   prefill_ms=prefill_ms, talker_ms=talker_ms, codec_ms=codec_ms)
 
