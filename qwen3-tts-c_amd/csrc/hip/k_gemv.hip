@@ -547,8 +547,8 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         fprintf(stderr, "qtts_gemv: unsupported shape R=%d C=%d nb=%d\n", a.R, a.C, a.nb);
         return -1;
     }
-    if (a.xadd && !(a.nb == 1 && a.C <= 8192 && a.ldx_ok1())) {
-        fprintf(stderr, "qtts_gemv: xadd needs the batch-1 path (R=%d C=%d nb=%d)\n", a.R, a.C, a.nb);
+    if (a.xadd && a.nb == 1 && !(a.C <= 8192 && a.ldx_ok1())) {
+        fprintf(stderr, "qtts_gemv: xadd needs the batch-1 fast path (R=%d C=%d)\n", a.R, a.C);
         return -1;
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
@@ -588,6 +588,10 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     if (a.nb >= 2) {   // lock-step batch: the matrix-core kernel (k_gemvm.hip) where it covers the shape
         const int rc = qtts_gemvm(a, st);
         if (rc != 1) return rc;
+    }
+    if (a.ypart || (a.xadd && a.nb >= 2)) {
+        fprintf(stderr, "qtts_gemv: split-K partials need the batch kernel (R=%d C=%d nb=%d)\n", a.R, a.C, a.nb);
+        return -1;
     }
     if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 256);
     int NB = a.nb <= 1 ? 1 : a.nb <= 2 ? 2 : a.nb <= 4 ? 4 : a.nb <= 8 ? 8 : 16;

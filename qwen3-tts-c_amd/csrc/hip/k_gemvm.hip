@@ -79,7 +79,17 @@ __device__ __forceinline__ float4 gm_load(const GemvArgs &a, int b, int c) {
         return make_float4(lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y));
     }
     if (a.table_f32) return *reinterpret_cast<const float4 *>(a.table_f32 + (size_t)gm_row_id(a, b) * a.C + c);
-    return *reinterpret_cast<const float4 *>(a.x + (size_t)b * a.ldx + c);
+    float4 v = *reinterpret_cast<const float4 *>(a.x + (size_t)b * a.ldx + c);
+    if (a.xadd) {   // the residual plus a split-K producer's partials, summed in order first
+        const float *xp = a.xadd + (size_t)b * a.ldb_xadd + c;
+        float4 sacc = *reinterpret_cast<const float4 *>(xp);
+        for (int p = 1; p < a.n_xadd; ++p) {
+            const float4 t = *reinterpret_cast<const float4 *>(xp + (size_t)p * a.ld_xadd);
+            sacc.x += t.x; sacc.y += t.y; sacc.z += t.z; sacc.w += t.w;
+        }
+        v.x += sacc.x; v.y += sacc.y; v.z += sacc.z; v.w += sacc.w;
+    }
+    return v;
 }
 
 // normalise (inv / norm_w), copy out (workgroup 0), split into the planes
@@ -114,6 +124,16 @@ template <bool NT, int U, int XU, int KS>
 __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x, nw = nthr >> 6;
+    // split-K producer: this workgroup column takes K columns [off, off + C / kz)
+    const int ldw = a.C;
+    int woff = 0;
+    if (gridDim.y > 1) {
+        const int ce = a.C / gridDim.y;
+        woff = blockIdx.y * ce;
+        a.x += woff;
+        if (a.xadd) a.xadd += woff;
+        a.C = ce;
+    }
     const int nb = a.nb, C = a.C, CCH = a.cch, LDH = CCH + 8, PS = nb * LDH;
     const bool chunked = CCH < C;
     unsigned short *hp = reinterpret_cast<unsigned short *>(smem);        // [3][nb][LDH] bf16 planes
@@ -126,7 +146,7 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     const int tile = blockIdx.x * tpw + tw;
     const int r0 = tile * 16, rl = lane & 15, kq = 8 * (lane >> 4);
     const int row = r0 + rl < a.R ? r0 + rl : a.R - 1;
-    const v4u *wr = reinterpret_cast<const v4u *>(a.W + (size_t)row * C + kq);
+    const v4u *wr = reinterpret_cast<const v4u *>(a.W + (size_t)row * ldw + woff + kq);
     const int nsteps = C / 32;
     const int J = r0 < a.R ? (nsteps - ksl + KS - 1) / KS : 0;   // this wave's K steps: s = ksl + KS * j
     const int ng = (J + U - 1) / U;
@@ -257,6 +277,10 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
         const float val = v[i];
         const float up = __shfl(val, (lane & 15) < 12 ? lane + 4 : lane, 64);
         if (bb >= nb || r >= a.R) continue;
+        if (a.ypart) {
+            a.ypart[blockIdx.y * a.ld_ypart + (size_t)bb * a.R + r] = val;
+            continue;
+        }
         float *yr = a.y + (size_t)bb * a.ldy;
         switch (a.epi) {
             case EPI_STORE: yr[r] = val; break;
@@ -297,6 +321,15 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     }
     if (a.norm_w && ((uintptr_t)a.norm_w & 15)) return 1;
     if (a.xcopy && (a.ldxc % 4 || ((uintptr_t)a.xcopy & 15))) return 1;
+    if (a.xadd && (a.table || a.table_f32 || ((uintptr_t)a.xadd & 15) || a.ld_xadd % 4 || a.ldb_xadd % 4 ||
+                   a.n_xadd < 1))
+        return 1;
+    const int kz = a.ypart ? a.kz : 1;
+    if (a.ypart && (kz < 2 || a.norm_w || a.table || a.table_f32 || a.xcopy || a.C % (32 * kz) ||
+                    ((uintptr_t)a.ypart & 3)))
+        return 1;
+    const int Cfull = a.C;
+    a.C /= kz;   // the K extent one workgroup column takes (host-side configuration only)
     // 16 waves per workgroup where the shape allows (one workgroup per CU):
     // KS waves per tile keep >= 2 K steps each; TPW tiles per workgroup bring
     // the grid to about one round over the 256 CUs (the x prologue is paid
@@ -334,7 +367,8 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     const int XU = xu == 0 || xu > 8 ? 0 : xu <= 4 ? 4 : 8;
     const int region = std::max(gm_planes(a.nb, cch), nthr / 64 * 64 * 16);
     const size_t smem = (size_t)region + (16 + (a.nb * a.C / 256 > 64 ? a.nb * a.C / 256 : 64)) * 4;
-    const dim3 grid((T + tpw - 1) / tpw);
+    const dim3 grid((T + tpw - 1) / tpw, kz);
+    a.C = Cfull;
 #define QTTS_GM(UU, XX, KK)                                                                                   \
     if (a.nt) hipLaunchKernelGGL((k_gemvm<true, UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);            \
     else hipLaunchKernelGGL((k_gemvm<false, UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);                \

@@ -27,6 +27,13 @@ struct GemvArgs {
     // in order first) -- the O projection's per-head partials (qtts_attn_o)
     const float *xadd = nullptr;
     int n_xadd = 0, ld_xadd = 0;
+    int ldb_xadd = 0;               // batch path (k_gemvm): row b of partial p at xadd + p*ld_xadd + b*ldb_xadd
+    // batch path split-K producer (k_gemvm): kz > 1 workgroup columns each take
+    // C / kz of K and store raw partials ypart[z*ld_ypart + b*R + r] (the
+    // consumer adds them with the residual through xadd); y / epi unused
+    float *ypart = nullptr;
+    size_t ld_ypart = 0;
+    int kz = 1;
     const float *norm_w = nullptr;  // RMSNorm weights [C] (nullptr: no norm)
     float eps = 1e-6f;
     float *xcopy = nullptr;         // workgroup 0 writes x rows here

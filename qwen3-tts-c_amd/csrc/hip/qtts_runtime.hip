@@ -98,6 +98,13 @@ struct qtts_dev {
     int nb = 0, nrun = 0, max_frames = 0, S = 0, p_cap = 0, tr_cap = 0, rows_cap = 0;  // nb: allocated slots (strides), nrun: rows launched
     float *x_tk = nullptr, *qkv = nullptr, *att = nullptr, *hbuf = nullptr, *logits = nullptr, *tk_hid = nullptr;
     float *x_st2 = nullptr, *opart = nullptr;   // attn_o: second residual buffer, per-head O partials
+    // batch split-K (nb >= 2): second talker residual, O / down partials; the
+    // talker's final residual = tk_xfin + sum of tk_npend partials at tk_pend
+    float *x_tk2 = nullptr, *bpo = nullptr, *bpd = nullptr;
+    float *tk_xfin = nullptr;
+    const float *tk_pend = nullptr;
+    int tk_npend = 0;
+    bool bsplit = true;      // QTTS_HIP_BSPLIT=0: batch O / down projections without split-K
     float *x_st = nullptr, *qkv_s = nullptr, *att_s = nullptr, *h_s = nullptr, *logits_s = nullptr;
     float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
     int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
@@ -338,6 +345,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->use_mfma = !(nm && atoi(nm));
     const char *ap = getenv("QTTS_HIP_ATT_PRO");
     dv->att_pro = ap && atoi(ap);
+    const char *bs = getenv("QTTS_HIP_BSPLIT");
+    dv->bsplit = !(bs && !atoi(bs));
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
     const char *aw = getenv("QTTS_HIP_ATT_PRO_WG");
@@ -450,6 +459,9 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(tk_hid, float, B * d.H);
     A(x_st, float, B * d.Hs);
     A(x_st2, float, B * d.Hs);
+    A(x_tk2, float, B * d.H);
+    A(bpo, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
+    A(bpd, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(opart, float, (size_t)d.KVs * d.Hs);
     A(qkv_s, float, B * dv->QKVs());
     A(att_s, float, B * d.NHs * d.HDs);
@@ -654,14 +666,38 @@ static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float
     return a;
 }
 
+// Batch split-K (nb >= 2, k_gemvm): the O and down projections of R rows take
+// kz workgroup columns when R / 16 tiles would not fill the chip; they store
+// partials, and the next GEMV that reads the residual adds them (xadd) and
+// writes the new residual to the other buffer (xcopy).  0 = no split.
+static int bsplit_kz(const qtts_dev *dv, int R, int C) {
+    if (!dv->bsplit || dv->nrun < 2) return 0;
+    int kz = R / 16 >= 256 ? 1 : 256 / (R / 16);
+    if (kz > 4) kz = 4;
+    while (kz > 1 && C % (32 * kz)) kz /= 2;
+    return kz > 1 ? kz : 0;
+}
+static void split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz) {
+    g.y = nullptr; g.ypart = part; g.kz = kz; g.ld_ypart = (size_t)dv->nrun * g.R;
+}
+static void add_in(GemvArgs &g, const float *part, int n, int R, int nrun, float *xnew) {
+    g.xadd = part; g.n_xadd = n; g.ld_xadd = nrun * R; g.ldb_xadd = R;
+    if (xnew) { g.xcopy = xnew; g.ldxc = R; g.xcopy_normed = 0; }
+}
+
 static int talker_layers(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     const int nb = dv->nrun, NBA = dv->nb, QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
     hipStream_t st = dv->st;
+    const int kzo = bsplit_kz(dv, d.H, AD), kzd = bsplit_kz(dv, d.H, d.I);
+    float *xa = dv->x_tk, *xb = dv->x_tk2;
+    const float *pend = nullptr;
+    int npend = 0;
     for (int l = 0; l < d.L; ++l) {
         Layer &ly = dv->tl[l];
-        GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->x_tk, d.H, dv->qkv, QKV, nb, EPI_STORE);
+        GemvArgs a = gv(ly.wqkv, QKV, d.H, xa, d.H, dv->qkv, QKV, nb, EPI_STORE);
         a.norm_w = ly.in; a.eps = d.eps;
+        if (pend) add_in(a, pend, npend, d.H, nb, xb);
         AttnArgs t;
         t.mode = 0; t.qkv = dv->qkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
         t.rope_cos = dv->rope_cos; t.rope_sin = dv->rope_sin;
@@ -670,12 +706,20 @@ static int talker_layers(qtts_dev *dv) {
         t.skip = dv->stopped;
         t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
         CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
-        CKI(pgemv(dv, gv(ly.wo, d.H, AD, dv->att, AD, dv->x_tk, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
-        a = gv(ly.wgu, 2 * d.I, d.H, dv->x_tk, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
+        if (pend) { std::swap(xa, xb); pend = nullptr; }
+        GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
+        if (kzo) split_out(dv, o, dv->bpo, kzo);
+        CKI(pgemv(dv, o, PK_GEMV_TALKER));
+        a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
+        if (kzo) add_in(a, dv->bpo, kzo, d.H, nb, xb);
         CKI(pgemv(dv, a, PK_GEMV_TALKER));
-        CKI(pgemv(dv, gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, dv->x_tk, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
+        if (kzo) std::swap(xa, xb);
+        GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
+        if (kzd) { split_out(dv, dn, dv->bpd, kzd); pend = dv->bpd; npend = kzd; }
+        CKI(pgemv(dv, dn, PK_GEMV_TALKER));
     }
+    dv->tk_xfin = xa; dv->tk_pend = pend; dv->tk_npend = npend;
     return 0;
 }
 
@@ -700,8 +744,10 @@ static int head_sample(qtts_dev *dv, const GemvArgs &a, const SampArgs &s, int k
 // final norm + codec head; normed hidden -> tk_hid (T.c:526-530, Q.c:1295)
 static GemvArgs talker_head_args(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
-    GemvArgs a = gv(dv->head, d.V, d.H, dv->x_tk, d.H, dv->logits, d.V, dv->nrun, EPI_STORE);
+    GemvArgs a = gv(dv->head, d.V, d.H, dv->tk_xfin ? dv->tk_xfin : dv->x_tk, d.H, dv->logits, d.V, dv->nrun,
+                    EPI_STORE);
     a.norm_w = dv->tk_norm; a.eps = d.eps; a.xcopy = dv->tk_hid; a.ldxc = d.H; a.xcopy_normed = 1;
+    if (dv->tk_pend) add_in(a, dv->tk_pend, dv->tk_npend, d.H, dv->nrun, nullptr);
     return a;
 }
 static int talker_tail(qtts_dev *dv) { return pgemv(dv, talker_head_args(dv), PK_GEMV_TALKER); }
@@ -756,12 +802,18 @@ static int subtalker(qtts_dev *dv) {
         // attn_o (batch 1): attention + O projection by kv head into per-head
         // partials, summed with the residual in the gate|up GEMV's prologue,
         // which writes the new residual to the other buffer (xa -> xb)
+        // batch (nb >= 2): O / down split-K partials added by the next
+        // residual reader (bsplit_kz)
         float *xa = dv->x_st, *xb = dv->x_st2;
+        const int kzo = bsplit_kz(dv, d.Hs, AD), kzd = bsplit_kz(dv, d.Hs, d.Is);
+        const float *pend = nullptr;
+        int npend = 0;
         for (int l = 0; l < d.Ls; ++l) {
             Layer &ly = dv->sl[l];
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
+            else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
             AttnArgs t;
             t.mode = 0; t.qkv = dv->qkv_s; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
             t.rope_cos = dv->rope_cos_s; t.rope_sin = dv->rope_sin_s;
@@ -790,6 +842,9 @@ static int subtalker(qtts_dev *dv) {
                 CKI(pgemv_att(dv, o, t, PK_GEMV_SUB));
             } else {
                 CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
+                if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
+                o.y = xa;
+                if (kzo) split_out(dv, o, dv->bpo, kzo);
                 CKI(pgemv(dv, o, PK_GEMV_SUB));
             }
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
@@ -797,18 +852,21 @@ static int subtalker(qtts_dev *dv) {
             if (fused_o) {
                 a.xadd = dv->opart; a.n_xadd = d.KVs; a.ld_xadd = d.Hs;
                 a.xcopy = xb; a.ldxc = d.Hs; a.xcopy_normed = 0;
+            } else if (kzo) {
+                add_in(a, dv->bpo, kzo, d.Hs, nb, xb);
             }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
-            float *xo = fused_o ? xb : xa;
-            a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xo, d.Hs, nb, EPI_RESID);
+            if (fused_o || kzo) std::swap(xa, xb);
+            a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xa, d.Hs, nb, EPI_RESID);
             a.nt = 0;
+            if (kzd) { split_out(dv, a, dv->bpd, kzd); pend = dv->bpd; npend = kzd; }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
-            if (fused_o) std::swap(xa, xb);
         }
         if (g == 0) continue;  // pass 0 produces no logits
         GemvArgs a = gv(dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, xa, d.Hs, dv->logits_s, d.Vs, nb,
                         EPI_STORE);
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
+        if (pend) add_in(a, pend, npend, d.Hs, nb, nullptr);
         SampArgs s;
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
@@ -831,6 +889,8 @@ static int embed_sum(qtts_dev *dv, int advance) {
 }
 
 static int record_frame(qtts_dev *dv, bool with_talker) {
+    // step 0 starts from the prefill's hidden in x_tk (no pending partials)
+    dv->tk_xfin = dv->x_tk; dv->tk_pend = nullptr; dv->tk_npend = 0;
     if (with_talker) CKI(talker_layers(dv));
     CKI(talker_head_sample(dv));
     CKI(subtalker(dv));

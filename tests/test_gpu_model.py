@@ -101,9 +101,14 @@ def test_eos_stop_reported_like_reference(gpu):
         m.close()
 
 
-def test_batch_slots_match_single_runs(tiny_dir, oracle):
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_BSPLIT": "0"}])
+def test_batch_slots_match_single_runs(tiny_dir, oracle, monkeypatch, env):
     """Lock-step batch (B GEMV columns, one weight read per frame): every
-    slot's audio equals the oracle's for its own prompt / speaker."""
+    slot's audio equals the oracle's for its own prompt / speaker -- with the
+    O / down projections split over K (partials added by the next residual
+    reader) and without."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     m = qtts.QwenTTS(tiny_dir)
     try:
         prompts = [prompt_ids("short"), prompt_ids("p128", 1240), prompt_ids("p128", 1241)]
