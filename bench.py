@@ -99,6 +99,14 @@ def ensure_model_shared(md, preset, ws, local):
 
 
 def _latest_profile(pattern):
+    """The summary of the profile pass of record: profiles/LATEST names its tag
+    (written by tools/gpu_round.sh before the bench line); else the last by name."""
+    latest = os.path.join(ROOT, "profiles", "LATEST")
+    if os.path.exists(latest):
+        tag = open(latest).read().strip()
+        fs = glob.glob(os.path.join(ROOT, "profiles", tag + "_" + pattern.lstrip("*")))
+        if fs:
+            return fs[0]
     fs = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     return fs[-1] if fs else None
 

@@ -40,6 +40,7 @@ python3 $R/tools/prof_summary.py $O
 # the bench reads the newest profiles/*kernel_stats.csv / *pmc.json
 cp $O/kernel_stats.csv $R/profiles/${TAG}_kernel_stats.csv
 cp $O/pmc.json $R/profiles/${TAG}_pmc.json
+echo $TAG > $R/profiles/LATEST
 cd $R
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
 echo done
