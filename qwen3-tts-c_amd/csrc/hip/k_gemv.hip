@@ -553,7 +553,9 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
         int nthr = 256;
-        if (a.ksplit <= 0 && gemv_wide(a.nt)) {
+        // (one CU's share >= 96 KB: below that the 256-thread grid measured faster,
+        // profiles/r01x_mb_gemv_wide_u16.txt)
+        if (a.ksplit <= 0 && gemv_wide(a.nt) && (size_t)a.R * a.C * 2 / 256 >= 96 * 1024) {
             wide_config(a.R, a.C, a.epi, a.ksplit, nthr);
         }
         if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
