@@ -1,9 +1,9 @@
-"""Full-size (synthetic 1.7B, BASELINE.json configs[1]) parity and
+"""Full-size (synthetic 1.7B; 0.6B for BASELINE.json configs[1]) parity and
 size-independent properties on the GPU.
 
 At full size the oracle is slow on the CPU, so it checks a short greedy
 prefix (3 frames: talker prefill over the P128 prompt, 3 decode steps, 3
-sub-talker passes) and a 4-frame codec decode; the 128-frame benchmark
+sub-talker passes; greedy and default sampling) and a 4-frame codec decode; the 128-frame benchmark
 workload is checked through properties: determinism, identical slots for
 identical inputs in a lock-step batch, code ranges, waveform length and range.
 """
@@ -37,10 +37,11 @@ def test_full_greedy_prefix_and_codec_vs_oracle(full_tts, full_dir):
     o = Oracle(full_dir)
     try:
         s, l = lookup_ids(o.cfg, "aiden", "english")
-        codes_o, _ = o.generate_codes(ids, s, l, max_tokens=4096, fixed=3, seed=42, **GREEDY)
-        full_tts.set_params(max_tokens=4096, fixed=3, seed=42, **GREEDY)
-        full_tts.generate(ids, "aiden", "english")
-        np.testing.assert_array_equal(full_tts.last_codes(), codes_o)
+        for pp in (GREEDY, DEFAULT):   # greedy, then the default sampling (top-k 50 / 0.9 / 1.05)
+            codes_o, _ = o.generate_codes(ids, s, l, max_tokens=4096, fixed=3, seed=42, **pp)
+            full_tts.set_params(max_tokens=4096, fixed=3, seed=42, **pp)
+            full_tts.generate(ids, "aiden", "english")
+            np.testing.assert_array_equal(full_tts.last_codes(), codes_o)
         rng = np.random.default_rng(0)
         codes = rng.integers(0, 2048, size=(4, 16)).astype(np.int32)
         a = full_tts.codec_decode(codes)
@@ -75,3 +76,22 @@ def test_full_batch_identical_slots(full_tts):
     np.testing.assert_array_equal(audio[0], audio[2])
     assert not np.array_equal(audio[0], audio[1])
     assert all(len(x) == 32 * 1920 for x in audio)
+
+
+def test_06b_greedy_prefix_vs_oracle(gpu):
+    """BASELINE.json configs[1] (0.6B, batch 1, greedy, P128): a 3-frame
+    prefix bit-exact against the oracle (no sub-talker input projection:
+    H == H_s)."""
+    md = model_dir("0.6b")
+    ids = prompt_ids("p128")
+    o = Oracle(md)
+    m = qtts.QwenTTS(md)
+    try:
+        s, l = lookup_ids(o.cfg, "aiden", "english")
+        codes_o, _ = o.generate_codes(ids, s, l, max_tokens=4096, fixed=3, seed=42, **GREEDY)
+        m.set_params(max_tokens=4096, fixed=3, seed=42, **GREEDY)
+        m.generate(ids, "aiden", "english")
+        np.testing.assert_array_equal(m.last_codes(), codes_o)
+    finally:
+        m.close()
+        o.close()
