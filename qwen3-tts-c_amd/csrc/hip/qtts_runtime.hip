@@ -139,6 +139,10 @@ struct qtts_dev {
     bool att_pro = false;    // QTTS_HIP_ATT_PRO=1: sub-talker attention as the O GEMV's prologue
                              // (measured slower: profiles/r01d_envsweep.txt)
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
+    int attn_o_tmax = 0;     // QTTS_HIP_ATTN_O_TALKER=S: talker attention + O fused while the key
+                             // capacity <= S (opt-in: 30 vs 17 us per layer at S ~150,
+                             // profiles/r01aj_envsweep_attn_o_talker.txt)
+    int attn_o_rps = 2;      // QTTS_HIP_ATTN_O_RPS: W_o rows per slot of the fused talker kernel
     int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
@@ -347,6 +351,10 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->att_pro = ap && atoi(ap);
     const char *bs = getenv("QTTS_HIP_BSPLIT");
     dv->bsplit = !(bs && !atoi(bs));
+    const char *aot = getenv("QTTS_HIP_ATTN_O_TALKER");
+    if (aot) dv->attn_o_tmax = atoi(aot);
+    const char *aor = getenv("QTTS_HIP_ATTN_O_RPS");
+    if (aor) dv->attn_o_rps = atoi(aor);
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
     const char *aw = getenv("QTTS_HIP_ATT_PRO_WG");
@@ -462,7 +470,7 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(x_tk2, float, B * d.H);
     A(bpo, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(bpd, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
-    A(opart, float, (size_t)d.KVs * d.Hs);
+    A(opart, float, (size_t)d.KVs * d.Hs > (size_t)d.KV * d.H ? (size_t)d.KVs * d.Hs : (size_t)d.KV * d.H);
     A(qkv_s, float, B * dv->QKVs());
     A(att_s, float, B * d.NHs * d.HDs);
     A(h_s, float, B * d.Is);
@@ -705,16 +713,38 @@ static int talker_layers(qtts_dev *dv) {
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
         t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
-        CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
-        if (pend) { std::swap(xa, xb); pend = nullptr; }
-        GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
-        if (kzo) split_out(dv, o, dv->bpo, kzo);
-        CKI(pgemv(dv, o, PK_GEMV_TALKER));
+        // batch 1, small key capacity: attention + O by kv head in one launch
+        // (k_attn_o_dec), per-head partials summed in the gate|up prologue
+        bool fused_o = false;
+        if (nb == 1 && dv->S <= dv->attn_o_tmax && !dv->fuse_attn) {
+            CKI(pgemv(dv, a, PK_GEMV_TALKER));
+            ProfScope ps(dv, PK_ATTN, (double)d.H * AD * 2);
+            const int rc = qtts_attn_o_dec(t, ly.wo, d.H, dv->opart, dv->attn_o_rps, st);
+            if (rc < 0) return -1;
+            if (rc == 1) {
+                ps.cancel();
+                { ProfScope pa(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
+                CKI(pgemv(dv, gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
+            } else {
+                fused_o = true;
+            }
+        } else {
+            CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
+            if (pend) { std::swap(xa, xb); pend = nullptr; }
+            GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
+            if (kzo) split_out(dv, o, dv->bpo, kzo);
+            CKI(pgemv(dv, o, PK_GEMV_TALKER));
+        }
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
-        if (kzo) add_in(a, dv->bpo, kzo, d.H, nb, xb);
+        if (fused_o) {
+            a.xadd = dv->opart; a.n_xadd = d.KV; a.ld_xadd = d.H;
+            a.xcopy = xb; a.ldxc = d.H; a.xcopy_normed = 0;
+        } else if (kzo) {
+            add_in(a, dv->bpo, kzo, d.H, nb, xb);
+        }
         CKI(pgemv(dv, a, PK_GEMV_TALKER));
-        if (kzo) std::swap(xa, xb);
+        if (fused_o || kzo) std::swap(xa, xb);
         GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
         if (kzd) { split_out(dv, dn, dv->bpd, kzd); pend = dv->bpd; npend = kzd; }
         CKI(pgemv(dv, dn, PK_GEMV_TALKER));
