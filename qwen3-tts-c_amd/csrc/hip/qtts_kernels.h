@@ -81,6 +81,14 @@ struct AttnArgs {
     float *part = nullptr;
     int *cnt = nullptr;
     int nsplit = 0;
+    // talker decode only: extra workgroups (grid z >= nrows, pf_z per (kv, split))
+    // read the next GEMVs' weights [pf0, +pf0_bytes) and [pf1, +pf1_bytes) while
+    // the latency-bound attention leaves HBM idle, so those GEMVs find them in
+    // the Infinity Cache; pf_sink: a scratch word that keeps the reads live
+    const void *pf0 = nullptr, *pf1 = nullptr;
+    size_t pf0_bytes = 0, pf1_bytes = 0;
+    int pf_z = 0;
+    unsigned *pf_sink = nullptr;
 };
 int qtts_attn_keys_per_split(int HD);
 int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st);

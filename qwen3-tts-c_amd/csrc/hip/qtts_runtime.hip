@@ -143,6 +143,12 @@ struct qtts_dev {
                              // capacity <= S (opt-in: 30 vs 17 us per layer at S ~150,
                              // profiles/r01aj_envsweep_attn_o_talker.txt)
     int attn_o_rps = 2;      // QTTS_HIP_ATTN_O_RPS: W_o rows per slot of the fused talker kernel
+    // talker attention prefetch (AttnArgs::pf*): the O weights (QTTS_HIP_PF_O) and
+    // the first QTTS_HIP_PF_GU MB of gate|up, by about QTTS_HIP_PF_WG workgroups.
+    // Opt-in: the attention launch grows by more than the GEMVs gain (23.3 vs
+    // 22.3 audio-s/s with O + 24 MB, profiles/r01al_envsweep_prefetch.txt)
+    int pf_o = 1, pf_gu_mb = 24, pf_wg = 0;
+    unsigned *pf_sink = nullptr;
     int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
 
@@ -351,6 +357,9 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->att_pro = ap && atoi(ap);
     const char *bs = getenv("QTTS_HIP_BSPLIT");
     dv->bsplit = !(bs && !atoi(bs));
+    if (const char *e = getenv("QTTS_HIP_PF_O")) dv->pf_o = atoi(e);
+    if (const char *e = getenv("QTTS_HIP_PF_GU")) dv->pf_gu_mb = atoi(e);
+    if (const char *e = getenv("QTTS_HIP_PF_WG")) dv->pf_wg = atoi(e);
     const char *aot = getenv("QTTS_HIP_ATTN_O_TALKER");
     if (aot) dv->attn_o_tmax = atoi(aot);
     const char *aor = getenv("QTTS_HIP_ATTN_O_RPS");
@@ -468,6 +477,7 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(x_st, float, B * d.Hs);
     A(x_st2, float, B * d.Hs);
     A(x_tk2, float, B * d.H);
+    A(pf_sink, unsigned, 16);
     A(bpo, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(bpd, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(opart, float, (size_t)d.KVs * d.Hs > (size_t)d.KV * d.H ? (size_t)d.KVs * d.Hs : (size_t)d.KV * d.H);
@@ -713,6 +723,14 @@ static int talker_layers(qtts_dev *dv) {
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
         t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
+        {   // next GEMVs' weights into the Infinity Cache while attention runs
+            const size_t gu = (size_t)2 * d.I * d.H * 2, gpf = (size_t)dv->pf_gu_mb << 20;
+            t.pf0 = ly.wo; t.pf0_bytes = dv->pf_o ? (size_t)d.H * AD * 2 : 0;
+            t.pf1 = ly.wgu; t.pf1_bytes = gpf < gu ? gpf : gu;
+            const int ch = qtts_attn_keys_per_split(d.HD), ns = (dv->S + ch - 1) / ch;
+            t.pf_z = (dv->pf_wg + d.KV * ns - 1) / (d.KV * ns);
+            t.pf_sink = dv->pf_sink;
+        }
         // batch 1, small key capacity: attention + O by kv head in one launch
         // (k_attn_o_dec), per-head partials summed in the gate|up prologue
         bool fused_o = false;

@@ -1,5 +1,5 @@
 set -eo pipefail
-O=gpurun_out/r01aj; mkdir -p $O; rm -f gpurun_out/envsweep/sweep.txt
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { rc=$?; [ $rc -eq 1 ] || exit $rc; }
-timeout -k 10 900 bash tools/env_sweep.sh "X=1" "QTTS_HIP_ATTN_O_TALKER=0" "QTTS_HIP_ATTN_O_RPS=1" "QTTS_HIP_ATTN_O_RPS=4" > $O/sweep_out.txt 2>&1
+O=gpurun_out/r01al; mkdir -p $O; rm -f gpurun_out/envsweep/sweep.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -k "e2e or full or batch" -v -p no:cacheprovider --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { rc=$?; [ $rc -eq 1 ] || exit $rc; }
+timeout -k 10 1000 bash tools/env_sweep.sh "X=1" "QTTS_HIP_PF_WG=0" "QTTS_HIP_PF_GU=0" "QTTS_HIP_PF_GU=50" "QTTS_HIP_PF_GU=12" > $O/sweep_out.txt 2>&1
 echo done
