@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_qk_prep(AttnArgs a) {
 // Prefetch workgroup of k_attn_dec: workgroup i of np reads its share of the
 // two byte ranges in 4 KB rows (16 B per lane, 8 loads in flight) and folds
 // them into one word that is stored only on an impossible match.
-__device__ __noinline__ void attn_prefetch(const AttnArgs &a) {
+__device__ __forceinline__ void attn_prefetch(const AttnArgs &a) {
     const int np = gridDim.x * gridDim.y * a.pf_z;
     const int i = ((blockIdx.z - a.nrows) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     const size_t tot = a.pf0_bytes + a.pf1_bytes;

@@ -145,8 +145,8 @@ struct qtts_dev {
     int attn_o_rps = 2;      // QTTS_HIP_ATTN_O_RPS: W_o rows per slot of the fused talker kernel
     // talker attention prefetch (AttnArgs::pf*): the O weights (QTTS_HIP_PF_O) and
     // the first QTTS_HIP_PF_GU MB of gate|up, by about QTTS_HIP_PF_WG workgroups.
-    // Opt-in: the attention launch grows by more than the GEMVs gain (23.3 vs
-    // 22.3 audio-s/s with O + 24 MB, profiles/r01al_envsweep_prefetch.txt)
+    // Opt-in: the attention launch grows by more than the GEMVs gain (23.9 vs
+    // 22.8 audio-s/s with O + 24 MB, profiles/r01am_envsweep_prefetch_inline.txt)
     int pf_o = 1, pf_gu_mb = 24, pf_wg = 0;
     unsigned *pf_sink = nullptr;
     int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
