@@ -176,6 +176,45 @@ __global__ __launch_bounds__(256) void k_qk_prep(AttnArgs a) {
     (void)red;
 }
 
+// prefill, one wave per (row, head): q / k heads normalised + rotated (q in
+// place, k -> cache), v heads -> cache; no LDS, no barrier.  grid (rows,
+// ceil((NH + 2 KV) / 4)), 256 threads.  HD = 128: a lane holds e and e + 64
+// (its own rotate-half partner); HD <= 64: one element, partner one xor away.
+__global__ __launch_bounds__(256) void k_qk_prep_w(AttnArgs a) {
+    const int r = blockIdx.x, w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int HD = a.HD, NH = a.NH, KV = a.KV, KVD = KV * HD;
+    const int hh = blockIdx.y * 4 + w;
+    if (hh >= NH + 2 * KV) return;
+    const int b = a.row_b[r], p = a.pos[r];
+    float *row = const_cast<float *>(a.qkv) + (size_t)r * a.ld_qkv;
+    float *kdst = a.kc + ((size_t)b * a.S + p) * KVD, *vdst = a.vc + ((size_t)b * a.S + p) * KVD;
+    if (hh >= NH + KV) {   // v head: copy to the cache
+        const int vh = hh - NH - KV;
+        for (int i = l; i < HD; i += 64) vdst[vh * HD + i] = row[(NH + KV) * HD + vh * HD + i];
+        return;
+    }
+    const float *src = row + hh * HD;
+    const float *nw = hh < NH ? a.qn_w : a.kn_w;
+    const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
+    const int half = HD >> 1;
+    float y0, y1 = 0.f;
+    if (HD == 128) {
+        const float x0 = src[l], x1 = src[l + 64];
+        const float iv = rms_inv(wave_sum(x0 * x0 + x1 * x1), HD, a.eps);
+        const float n0 = x0 * iv * nw[l], n1 = x1 * iv * nw[l + 64];
+        y0 = n0 * cs[l] - n1 * sn[l];
+        y1 = n1 * cs[l + 64] + n0 * sn[l + 64];
+    } else {
+        const float x0 = l < HD ? src[l] : 0.f;
+        const float iv = rms_inv(wave_sum(x0 * x0), HD, a.eps);
+        const float n0 = l < HD ? x0 * iv * nw[l] : 0.f;
+        const float pn = __shfl_xor(n0, half, 64);
+        y0 = l < HD ? (l < half ? n0 * cs[l] - pn * sn[l] : n0 * cs[l] + pn * sn[l]) : 0.f;
+    }
+    float *dst = hh < NH ? row + hh * HD : kdst + (hh - NH) * HD;
+    if (HD == 128) { dst[l] = y0; dst[l + 64] = y1; }
+    else if (l < HD) dst[l] = y0;
+}
 
 // ---------------------------------------------------------------------------
 // Decode attention, split over keys (flash-decoding) for one kv head per
@@ -735,6 +774,12 @@ int qtts_qk_prep(const AttnArgs &a, hipStream_t st) {
     if ((a.NH + a.KV) * a.HD > 4096) {
         fprintf(stderr, "qtts_qk_prep: (NH+KV)*HD=%d exceeds 4096\n", (a.NH + a.KV) * a.HD);
         return -1;
+    }
+    static const bool old_prep = getenv("QTTS_HIP_QK_PREP_BLOCK") != nullptr;
+    if (!old_prep && (a.HD == 128 || (a.HD <= 64 && (a.HD & (a.HD - 1)) == 0))) {
+        const dim3 grid(a.nrows, (a.NH + 2 * a.KV + 3) / 4);
+        hipLaunchKernelGGL(k_qk_prep_w, grid, dim3(256), 0, st, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     hipLaunchKernelGGL(k_qk_prep, dim3(a.nrows), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;

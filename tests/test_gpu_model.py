@@ -262,7 +262,8 @@ def test_cli_stream_flag(tiny_dir):
                                  {"QTTS_HIP_PTAB": "0"}, {"QTTS_HIP_NO_SHORT_ATTN": "1"},
                                  {"QTTS_HIP_FUSE_ST": "1"}, {"QWEN_TTS_HIP_OVERLAP": "1"}, {"QTTS_HIP_ATTN_O": "0"},
                                  {"QTTS_HIP_ATTN_O_TALKER": "4096"},
-                                 {"QTTS_HIP_ATTN_O_TALKER": "4096", "QTTS_HIP_ATTN_O_RPS": "4"}])
+                                 {"QTTS_HIP_ATTN_O_TALKER": "4096", "QTTS_HIP_ATTN_O_RPS": "4"},
+                                 {"QTTS_HIP_QK_PREP_BLOCK": "1"}])
 def test_e2e_subtalker_attention_variants(tiny_dir, monkeypatch, env):
     """Alternative sub-talker paths stay bit-exact: attention as the O GEMV's
     prologue (opt-in, two grids), the per-pass input projection instead of the
