@@ -1,6 +1,4 @@
 set -eo pipefail
-O=gpurun_out/r01ao; mkdir -p $O; rm -f gpurun_out/envsweep/sweep.txt
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { rc=$?; [ $rc -eq 1 ] || exit $rc; }
-timeout -k 10 1000 bash tools/env_sweep.sh "X=1" "QTTS_HIP_QK_PREP_BLOCK=1" > $O/sweep_out.txt 2>&1
-cp gpurun_out/envsweep/tmp.json $O/last.json
+O=gpurun_out/r01aq; mkdir -p $O; rm -f gpurun_out/envsweep/sweep.txt
+timeout -k 10 1000 bash tools/env_sweep.sh "X=1" "QTTS_HIP_XADD_TARGET=256" "QTTS_HIP_XADD_TARGET=128" "QTTS_HIP_XADD_TARGET=1024" "X=2" > $O/sweep_out.txt 2>&1
 echo done
