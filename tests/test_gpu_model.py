@@ -231,6 +231,12 @@ def test_generate_stream_equals_generate(tiny_dir):
         assert s.shape == full.shape and np.abs(s - full).max() < 1e-5
         np.testing.assert_array_equal(m.last_codes(), E["greedy_codes"])
         assert 0 < m.c.perf_first_packet_ms < m.c.perf_total_ms
+        # later streams on the same context (reused stream state): identical audio
+        for _ in range(2):
+            chunks2 = []
+            s2 = m.generate_stream(prompt_ids("short"), "aiden", "english", chunk_frames=4, on_chunk=chunks2.append)
+            np.testing.assert_array_equal(s2, s)
+            np.testing.assert_array_equal(chunks2[0], chunks[0])
     finally:
         m.close()
 
