@@ -858,6 +858,9 @@ static int subtalker(qtts_dev *dv) {
         int npend = 0;
         for (int l = 0; l < d.Ls; ++l) {
             Layer &ly = dv->sl[l];
+            // pass 0 produces no logits: its last layer only has to store its k / v
+            // (ST_FORWARD of pass 1 restarts from its own input, T.c:704-714)
+            const bool kv_only = g == 0 && l == d.Ls - 1;
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
@@ -893,8 +896,9 @@ static int subtalker(qtts_dev *dv) {
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 o.y = xa;
                 if (kzo) split_out(dv, o, dv->bpo, kzo);
-                CKI(pgemv(dv, o, PK_GEMV_SUB));
+                if (!kv_only) CKI(pgemv(dv, o, PK_GEMV_SUB));
             }
+            if (kv_only) break;
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
             if (fused_o) {

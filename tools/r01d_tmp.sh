@@ -1,7 +1,5 @@
 set -eo pipefail
-O=gpurun_out/r01as; mkdir -p $O
-timeout -k 10 300 python3 tools/prof_stream.py > $O/stream.txt 2>&1
-QTTS_HIP_CODEC_G1=0 timeout -k 10 300 python3 tools/prof_stream.py > $O/stream_off.txt 2>&1
-timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 > $O/b1.json 2> $O/b1.err
-QTTS_HIP_CODEC_G1=0 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 > $O/b0.json 2> $O/b0.err
+O=gpurun_out/r01au; mkdir -p $O; rm -f gpurun_out/envsweep/sweep.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { rc=$?; [ $rc -eq 1 ] || exit $rc; }
+timeout -k 10 1000 bash tools/env_sweep.sh "X=1" "X=2" > $O/sweep_out.txt 2>&1
 echo done
