@@ -503,7 +503,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     __shared__ __attribute__((aligned(16))) float lq[4 * HD];
     __shared__ __attribute__((aligned(16))) float att[W2];
     __shared__ float sc[2 * 16];
-    const int tid = threadIdx.x, kvh = blockIdx.y, rb = blockIdx.x;
+    const int tid = threadIdx.x, kvh = blockIdx.y, rb = blockIdx.x, b = blockIdx.z;   // b: batch row
     const int slot = tid / LPS, sub = tid - slot * LPS;
     const int row = rb * RPW + slot, rowc = row < R ? row : R - 1;
     const int AD = t.NH * HD;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     const bf16_t *wr = Wo + (size_t)rowc * AD + W2 * kvh + 8 * sub;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
-    attn_short_wg<HD, false>(t, kvh, 0, lq, sc, att, rb == 0);
+    attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0);
     __syncthreads();
     float acc = 0.f;
 #pragma unroll
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     }
 #pragma unroll
     for (int o = LPS / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (sub == 0 && row < R) part[(size_t)kvh * R + row] = acc;
+    if (sub == 0 && row < R) part[((size_t)kvh * gridDim.z + b) * R + row] = acc;
 }
 
 // Talker decode attention + O projection by kv head (batch 1, GQA 2), for
@@ -712,14 +712,15 @@ int qtts_attn_o_dec(const AttnArgs &a, const bf16_t *Wo, int R, float *part, int
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Sub-talker attention + O projection by kv head (batch 1); 1 = not covered.
+// Sub-talker attention + O projection by kv head, rows b < nrows (grid z):
+// part[(kvh * nrows + b) * R + row]; 1 = not covered.
 int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st) {
     const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
-    if (!(a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.S <= 16 && a.nrows == 1 &&
+    if (!(a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.S <= 16 && a.nrows >= 1 &&
           ((uintptr_t)Wo & 15) == 0 && (a.NH * a.HD) % 8 == 0))
         return 1;
     const int W2 = 2 * a.HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
-    const dim3 grid((R + RPW - 1) / RPW, a.KV);
+    const dim3 grid((R + RPW - 1) / RPW, a.KV, a.nrows);
     switch (a.HD) {
         case 128: hipLaunchKernelGGL((k_attn_o<128>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<128>"; break;
         case 64: hipLaunchKernelGGL((k_attn_o<64>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<64>"; break;

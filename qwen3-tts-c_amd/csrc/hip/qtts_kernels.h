@@ -95,8 +95,8 @@ int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st);
 // O projection with the short-context decode attention as its prologue
 // (qtts_attn_pro.h); 1 = not covered
 int qtts_gemv_att(GemvArgs a, const AttnArgs &t, int target_wg, hipStream_t st);
-// sub-talker attention + O projection split by kv head: part [KV][R]
-// (batch 1, GQA 2, <= 16 keys); 1 = not covered
+// sub-talker attention + O projection split by kv head: part [KV][nrows][R]
+// (GQA 2, <= 16 keys); 1 = not covered
 int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st);
 // talker decode attention (any key count, 64-key online-softmax chunks) + O
 // projection by kv head (batch 1, GQA 2); rps W_o rows per slot; 1 = not covered

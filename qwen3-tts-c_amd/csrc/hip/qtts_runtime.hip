@@ -480,7 +480,7 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(pf_sink, unsigned, 16);
     A(bpo, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(bpd, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
-    A(opart, float, (size_t)d.KVs * d.Hs > (size_t)d.KV * d.H ? (size_t)d.KVs * d.Hs : (size_t)d.KV * d.H);
+    A(opart, float, (size_t)B * ((size_t)d.KVs * d.Hs > (size_t)d.KV * d.H ? (size_t)d.KVs * d.Hs : (size_t)d.KV * d.H));
     A(qkv_s, float, B * dv->QKVs());
     A(att_s, float, B * d.NHs * d.HDs);
     A(h_s, float, B * d.Is);
@@ -875,15 +875,21 @@ static int subtalker(qtts_dev *dv) {
             GemvArgs o = gv(ly.wo, d.Hs, AD, dv->att_s, AD, xa, d.Hs, nb, EPI_RESID);
             o.nt = 0;
             bool fused_o = false;
+            // (batch 1 only: at batch 8 / 16 the per-row recompute measured slower than
+            // the separate attention + split-K O projection, 98 vs 107 / 132 vs 155
+            // audio-s/s, profiles/r01av_bench_batch_attn_o.txt)
             if (dv->attn_o && nb == 1 && !dv->att_pro && !dv->fuse_st) {
                 CKI(pgemv(dv, a, PK_GEMV_SUB));
+                if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 ProfScope ps(dv, PK_ATTN, (double)d.Hs * AD * 2);
                 const int rc = qtts_attn_o(t, ly.wo, d.Hs, dv->opart, st);
                 if (rc < 0) return -1;
                 if (rc == 1) {   // not covered: the attention kernel, then the O GEMV below
                     ps.cancel();
                     { ProfScope pa(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
-                    CKI(pgemv(dv, o, PK_GEMV_SUB));
+                    o.y = xa;
+                    if (kzo) split_out(dv, o, dv->bpo, kzo);
+                    if (!kv_only) CKI(pgemv(dv, o, PK_GEMV_SUB));
                 } else {
                     fused_o = true;
                 }
@@ -902,8 +908,7 @@ static int subtalker(qtts_dev *dv) {
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
             if (fused_o) {
-                a.xadd = dv->opart; a.n_xadd = d.KVs; a.ld_xadd = d.Hs;
-                a.xcopy = xb; a.ldxc = d.Hs; a.xcopy_normed = 0;
+                add_in(a, dv->opart, d.KVs, d.Hs, nb, xb);
             } else if (kzo) {
                 add_in(a, dv->bpo, kzo, d.Hs, nb, xb);
             }
