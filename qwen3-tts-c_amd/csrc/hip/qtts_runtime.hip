@@ -126,6 +126,7 @@ struct qtts_dev {
     // codec overlapped with the decode (qtts_dev_codec_async_*): its own stream,
     // ordered after the frames it decodes by an event; output stays on device
     hipStream_t cst = nullptr;
+    int codec_cus = 0, cu_mask_style = 0;   // QTTS_HIP_CODEC_CUS / QTTS_HIP_CU_MASK_STYLE
     hipEvent_t cev = nullptr;
     float *cwav = nullptr;
     size_t cwav_cap = 0;
@@ -330,6 +331,19 @@ extern "C" int qtts_dev_put_tensor(qtts_dev_t *dv, const char *cname, const void
     return 0;
 }
 
+// CU masks of the decode (codec = false) and codec streams: style 0 gives the
+// codec the top codec_cus CU indices, style 1 every (ncu / codec_cus)-th CU.
+static void cu_masks(const qtts_dev *dv, bool codec, std::vector<uint32_t> &m) {
+    int ncu = 256;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv->device);
+    const int n = std::min(dv->codec_cus, ncu - 1), stride = std::max(1, ncu / std::max(1, n));
+    m.assign((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) {
+        const bool c = dv->cu_mask_style == 1 ? (i % stride == stride - 1 && i / stride < n) : i >= ncu - n;
+        if (c == codec) m[i >> 5] |= 1u << (i & 31);
+    }
+}
+
 extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     if (hipSetDevice(device) != hipSuccess) {
         fprintf(stderr, "qtts: cannot select HIP device %d\n", device);
@@ -338,7 +352,23 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     qtts_dev *dv = new qtts_dev();
     dv->d = *dims;
     dv->device = device;
-    if (hipStreamCreateWithFlags(&dv->st, hipStreamNonBlocking) != hipSuccess) {
+    // QTTS_HIP_CODEC_CUS=N (opt-in, with the overlapped codec): the decode
+    // stream and the codec stream get disjoint CU masks (N CUs for the codec),
+    // so a long codec workgroup never holds a CU a decode kernel waits for.
+    {
+        const char *cc = getenv("QTTS_HIP_CODEC_CUS");
+        const char *cs = getenv("QTTS_HIP_CU_MASK_STYLE");
+        dv->codec_cus = cc ? atoi(cc) : 0;
+        dv->cu_mask_style = cs ? atoi(cs) : 0;
+    }
+    if (dv->codec_cus > 0) {
+        std::vector<uint32_t> m;
+        cu_masks(dv, false, m);
+        if (hipExtStreamCreateWithCUMask(&dv->st, (uint32_t)m.size(), m.data()) != hipSuccess) {
+            delete dv;
+            return nullptr;
+        }
+    } else if (hipStreamCreateWithFlags(&dv->st, hipStreamNonBlocking) != hipSuccess) {
         delete dv;
         return nullptr;
     }
@@ -1196,7 +1226,13 @@ extern "C" int qtts_dev_codec_async_begin(qtts_dev_t *dv, int max_frames) {
     if (!dv->cst) {
         int lo = 0, hi = 0;
         CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
+        if (dv->codec_cus > 0) {
+            std::vector<uint32_t> m;
+            cu_masks(dv, true, m);
+            CK(hipExtStreamCreateWithCUMask(&dv->cst, (uint32_t)m.size(), m.data()));
+        } else {
+            CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
+        }
         CK(hipEventCreateWithFlags(&dv->cev, hipEventDisableTiming));
     }
     const size_t need = (size_t)max_frames * 1920;
