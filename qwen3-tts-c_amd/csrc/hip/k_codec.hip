@@ -26,10 +26,28 @@ namespace {
 
 constexpr int BM = 64, BN = 64, BK = 32;
 
-__device__ __forceinline__ float snake1(float x, float a, float ib) {
-    const float s = sinf(x * a);
-    return x + ib * s * s;
+// sin^2(r): the sign of sin drops out, so one Cody-Waite step by pi
+// (pi = PI_HI + PI_LO; both products exact inside the fmas, k exact below
+// 2^24) and the odd Taylor series through y^13 on [-pi/2, pi/2] (truncation
+// < 1e-9) give sinf(r)^2 to 2.2e-7 absolute (checked over |r| <= 8192) in
+// ~15 instructions instead of the general sinf's ~90 plus its inlined
+// large-argument path.
+__device__ __forceinline__ float sin2(float r) {
+    const float k = rintf(r * 0.318309886183790672f);
+    float y = fmaf(-k, 3.14159274101257324f, r);
+    y = fmaf(-k, -8.74227765734758577e-08f, y);
+    const float y2 = y * y;
+    float p = 1.6059043836821613e-10f;                 // 1/13!
+    p = fmaf(p, y2, -2.5052108385441720e-08f);         // -1/11!
+    p = fmaf(p, y2, 2.7557319223985893e-06f);          // 1/9!
+    p = fmaf(p, y2, -1.9841269841269841e-04f);         // -1/7!
+    p = fmaf(p, y2, 8.3333333333333333e-03f);          // 1/5!
+    p = fmaf(p, y2, -1.6666666666666667e-01f);         // -1/3!
+    const float sn = fmaf(y * y2, p, y);
+    return sn * sn;
 }
+
+__device__ __forceinline__ float snake1(float x, float a, float ib) { return x + ib * sin2(x * a); }
 
 __device__ __forceinline__ float loadB(const XGemm &g, int k, int n) {
     if (k >= g.K || n >= g.N) return 0.f;
@@ -273,6 +291,184 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
         }
         if (n < g.N) xg_epi(g, m, n, acc0[r]);
         if (n + 32 < g.N) xg_epi(g, m, n + 32, acc1[r]);
+    }
+}
+
+// k_conv on the bf16 matrix cores (QTTS_HIP_CONV_BF, default on): same
+// tiles, grid, splits and epilogues, fp32-equivalent products.  The weights
+// and the staged input are split exactly into three bf16 planes, w = w1 + w2
+// + w3 and x = x1 + x2 + x3, and the six products with i + j <= 4 are
+// accumulated (the three dropped ones are below 2^-24 of |w x|):
+//   v_mfma_f32_32x32x16_bf16 is 16x the fp32-input MFMA's rate, so six of
+//   them cost 3/8 of the eight v_mfma_f32_32x32x2_f32 a 16-channel stage
+//   took.
+// LDS rows are 16 channels (32 B) with the two 16-B halves swapped on odd
+// 8-row groups: conflict-free ds_read_b128 fragments.  The weight planes
+// follow the fp32 relayout in the same allocation (wt_planes).
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int CB_SNAKE_MAX = 1536;   // input channels per split whose SnakeBeta parameters k_convb stages
+
+__device__ __forceinline__ int cb_swz(int row, int half) { return row * 16 + 8 * (half ^ ((row >> 3) & 1)); }
+
+__device__ __forceinline__ uint32_t cb_pk(float lo, float hi) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    const bf2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float cb_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float cb_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
+
+// 8 floats -> three bf16 planes (16 B each)
+__device__ __forceinline__ void cb_split8(const float (&v)[8], uint4 &p1, uint4 &p2, uint4 &p3) {
+    uint32_t a[4], b[4], c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a[i] = cb_pk(v[2 * i], v[2 * i + 1]);
+        const float e0 = v[2 * i] - cb_lo(a[i]), e1 = v[2 * i + 1] - cb_hi(a[i]);
+        b[i] = cb_pk(e0, e1);
+        c[i] = cb_pk(e0 - cb_lo(b[i]), e1 - cb_hi(b[i]));
+    }
+    p1 = make_uint4(a[0], a[1], a[2], a[3]);
+    p2 = make_uint4(b[0], b[1], b[2], b[3]);
+    p3 = make_uint4(c[0], c[1], c[2], c[3]);
+}
+
+// WN waves along t (2 or 4): a 64 x 64*WN tile per workgroup of 128*WN
+// threads; the staged weights serve WN waves per 32-row half.
+template <int KW, int WN>
+__global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
+    constexpr int NT = 128 * WN, BNT = 64 * WN;
+    const int nzk = g.kz > 1 ? g.kz : 1, ph = blockIdx.z / nzk, kzi = blockIdx.z - ph * nzk;
+    const int nph = gridDim.z / nzk, ci = g.K / KW;
+    const size_t ps = (size_t)nph * g.M * g.K;   // plane stride (elements)
+    const unsigned short *wb = reinterpret_cast<const unsigned short *>(g.wt + ps) + (size_t)ph * KW * g.M * ci;
+    g.phase += ph;
+    constexpr int NBW = BNT + CV_HALO;
+    constexpr int NA = 3 * KW * CV_BM * 2;                   // 16-B weight items per stage
+    constexpr int NAT = (NA + NT - 1) / NT;
+    constexpr int NBT = (2 * NBW + NT - 1) / NT;             // (half, column) input items per thread
+    __shared__ __attribute__((aligned(16))) unsigned short As[3 * KW * CV_BM * 16];
+    __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * NBW * 16];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int m0 = blockIdx.y * CV_BM, n0 = blockIdx.x * BNT;
+    const int wm = (wave / WN) * 32, wn = (wave % WN) * 64;
+    const int dil = g.dil, t0 = n0 - g.pad;
+    const int cpz = ci / nzk, cbeg = kzi * cpz, cend = cbeg + cpz;
+    const int win = BNT + (KW - 1) * dil;
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
+    uint4 ra[NAT];
+    float rb[NBT][8];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int j = 0; j < NAT; ++j) {
+            const int e = tid + NT * j;
+            const int p = e / (KW * CV_BM * 2), rem = e - p * (KW * CV_BM * 2);
+            const int tap = rem / (CV_BM * 2), m = (rem >> 1) % CV_BM, h = rem & 1;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (e < NA && m0 + m < g.M)
+                v = *reinterpret_cast<const uint4 *>(wb + p * ps + ((size_t)tap * g.M + m0 + m) * ci + c0 + 8 * h);
+            ra[j] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < NBT; ++j) {
+            const int e = tid + NT * j, h = e / NBW, x = e - h * NBW, t = t0 + x;
+            const bool ok = h < 2 && x < win && t >= g.tmin && t < g.L;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rb[j][q] = ok ? g.B[(size_t)(c0 + 8 * h + q) * g.ldb + t] : 0.f;
+        }
+    };
+    load(cbeg);
+    // SnakeBeta of the input channels is applied when a stage is written to
+    // LDS (its loads have landed by then), its parameters staged once
+    __shared__ float Ssa[CB_SNAKE_MAX], Ssb[CB_SNAKE_MAX];
+    const bool snake = g.sa != nullptr;
+    if (snake) {
+        for (int c = tid; c < cpz; c += NT) { Ssa[c] = g.sa[cbeg + c]; Ssb[c] = g.sb[cbeg + c]; }
+        __syncthreads();
+    }
+    const int r = lane & 31, hh = lane >> 5;
+    for (int c0 = cbeg; c0 < cend; c0 += CV_BC) {
+#pragma unroll
+        for (int j = 0; j < NAT; ++j) {
+            const int e = tid + NT * j;
+            if (e < NA) {
+                const int pt = e / (CV_BM * 2), m = (e >> 1) % CV_BM, h = e & 1;   // pt = plane * KW + tap
+                *reinterpret_cast<uint4 *>(&As[pt * CV_BM * 16 + cb_swz(m, h)]) = ra[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NBT; ++j) {
+            const int e = tid + NT * j, h = e / NBW, x = e - h * NBW;
+            if (h < 2) {
+                if (snake) {
+                    const int cl = c0 - cbeg + 8 * h;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) rb[j][q] = snake1(rb[j][q], Ssa[cl + q], Ssb[cl + q]);
+                }
+                uint4 p1, p2, p3;
+                cb_split8(rb[j], p1, p2, p3);
+                const int o = cb_swz(x, h);
+                *reinterpret_cast<uint4 *>(&Bs[o]) = p1;
+                *reinterpret_cast<uint4 *>(&Bs[NBW * 16 + o]) = p2;
+                *reinterpret_cast<uint4 *>(&Bs[2 * NBW * 16 + o]) = p3;
+            }
+        }
+        __syncthreads();
+        if (c0 + CV_BC < cend) load(c0 + CV_BC);
+#pragma unroll
+        for (int tap = 0; tap < KW; ++tap) {
+            const int sh = tap * dil, oa = cb_swz(wm + r, hh);
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(&As[(0 * KW + tap) * CV_BM * 16 + oa]);
+            const bf16x8 a2 = *reinterpret_cast<const bf16x8 *>(&As[(1 * KW + tap) * CV_BM * 16 + oa]);
+            const bf16x8 a3 = *reinterpret_cast<const bf16x8 *>(&As[(2 * KW + tap) * CV_BM * 16 + oa]);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int ob = cb_swz(wn + 32 * nb + r + sh, hh);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(&Bs[ob]);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(&Bs[NBW * 16 + ob]);
+                const bf16x8 b3 = *reinterpret_cast<const bf16x8 *>(&Bs[2 * NBW * 16 + ob]);
+                floatx16 &acc = nb ? acc1 : acc0;
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    float *pz = nzk > 1 ? g.part + (size_t)blockIdx.z * g.M * g.N : nullptr;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m = m0 + wm + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + (lane & 31);
+        if (m >= g.M) continue;
+        if (pz) {
+            if (n < g.N) pz[(size_t)m * g.N + n] = acc0[i];
+            if (n + 32 < g.N) pz[(size_t)m * g.N + n + 32] = acc1[i];
+            continue;
+        }
+        if (n < g.N) xg_epi(g, m, n, acc0[i]);
+        if (n + 32 < g.N) xg_epi(g, m, n + 32, acc1[i]);
+    }
+}
+
+// w (fp32, n elements) -> three exact bf16 planes at planes[p * n + i]
+__global__ void k_wt_split(const float *w, size_t n, unsigned short *planes) {
+    const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (i >= n) return;
+    const float v0 = w[i], v1 = i + 1 < n ? w[i + 1] : 0.f;
+    const uint32_t a = cb_pk(v0, v1);
+    const float e0 = v0 - cb_lo(a), e1 = v1 - cb_hi(a);
+    const uint32_t b = cb_pk(e0, e1);
+    const uint32_t c = cb_pk(e0 - cb_lo(b), e1 - cb_hi(b));
+    const uint32_t pl[3] = {a, b, c};
+    for (int p = 0; p < 3; ++p) {
+        planes[p * n + i] = (unsigned short)(pl[p] & 0xFFFFu);
+        if (i + 1 < n) planes[p * n + i + 1] = (unsigned short)(pl[p] >> 16);
     }
 }
 
@@ -554,11 +750,38 @@ static int conv_launch(const XGemm &gin, int nph, hipStream_t st) {
     XGemm g = gin;
     g.kz = conv_splits(g);
     const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM, nph * g.kz);
-    switch (g.Kw) {
-        case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
-        case 3: hipLaunchKernelGGL(k_conv<3>, cg, dim3(256), 0, st, g); break;
-        case 2: hipLaunchKernelGGL(k_conv<2>, cg, dim3(256), 0, st, g); break;
-        default: hipLaunchKernelGGL(k_conv<1>, cg, dim3(256), 0, st, g); break;
+    static const char *fb = getenv("QTTS_HIP_CONV_BF");
+    static const bool bf_on = !fb || atoi(fb);
+    const bool bf = bf_on && (!g.sa || g.K / g.Kw / (g.kz > 1 ? g.kz : 1) <= CB_SNAKE_MAX);
+    if (bf) {
+        // 256-column tiles where the grid still holds >= 2 workgroups per CU
+        // (QTTS_HIP_CONV_WN=2 keeps 128)
+        static const char *fw = getenv("QTTS_HIP_CONV_WN");
+        static const int wn_max = fw ? atoi(fw) : 4;
+        const int tiles4 = ((g.N + 255) / 256) * cg.y * cg.z;
+        if (wn_max >= 4 && tiles4 >= 512) {
+            const dim3 c4((g.N + 255) / 256, cg.y, cg.z);
+            switch (g.Kw) {
+                case 7: hipLaunchKernelGGL((k_convb<7, 4>), c4, dim3(512), 0, st, g); break;
+                case 3: hipLaunchKernelGGL((k_convb<3, 4>), c4, dim3(512), 0, st, g); break;
+                case 2: hipLaunchKernelGGL((k_convb<2, 4>), c4, dim3(512), 0, st, g); break;
+                default: hipLaunchKernelGGL((k_convb<1, 4>), c4, dim3(512), 0, st, g); break;
+            }
+        } else {
+            switch (g.Kw) {
+                case 7: hipLaunchKernelGGL((k_convb<7, 2>), cg, dim3(256), 0, st, g); break;
+                case 3: hipLaunchKernelGGL((k_convb<3, 2>), cg, dim3(256), 0, st, g); break;
+                case 2: hipLaunchKernelGGL((k_convb<2, 2>), cg, dim3(256), 0, st, g); break;
+                default: hipLaunchKernelGGL((k_convb<1, 2>), cg, dim3(256), 0, st, g); break;
+            }
+        }
+    } else {
+        switch (g.Kw) {
+            case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
+            case 3: hipLaunchKernelGGL(k_conv<3>, cg, dim3(256), 0, st, g); break;
+            case 2: hipLaunchKernelGGL(k_conv<2>, cg, dim3(256), 0, st, g); break;
+            default: hipLaunchKernelGGL(k_conv<1>, cg, dim3(256), 0, st, g); break;
+        }
     }
     if (g.kz > 1) {
         const size_t n = (size_t)nph * g.M * g.N;
@@ -611,6 +834,13 @@ static float *cw(CodecModel *m, const std::string &n) {
     return it == m->w.end() ? nullptr : it->second;
 }
 
+// a relayout of cnt floats is followed in its allocation (cnt * 10 bytes) by
+// its three bf16 planes (k_convb)
+static void wt_planes(float *t, size_t cnt, hipStream_t st) {
+    hipLaunchKernelGGL(k_wt_split, dim3((unsigned)((cnt / 2 + 256) / 256)), dim3(256), 0, st, t, cnt,
+                       reinterpret_cast<unsigned short *>(t + cnt));
+}
+
 // conv weight `n` ([co][ci][Kw]) re-laid as [Kw][co][ci] for k_conv, made on first use
 static const float *cwt(CodecModel *m, const std::string &n, int co, int ci, int Kw) {
     auto it = m->wt.find(n);
@@ -618,10 +848,11 @@ static const float *cwt(CodecModel *m, const std::string &n, int co, int ci, int
     const float *w = cw(m, n);
     float *t = nullptr;
     const size_t cnt = (size_t)co * ci * Kw;
-    if (!w || hipMalloc(&t, cnt * 4) != hipSuccess) return nullptr;
+    if (!w || hipMalloc(&t, cnt * 10) != hipSuccess) return nullptr;
     hipLaunchKernelGGL(k_wt_relayout, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, m->st, w, co, ci, Kw, t);
+    wt_planes(t, cnt, m->st);
     m->wt[n] = t;
-    m->wbytes += cnt * 4;
+    m->wbytes += cnt * 10;
     return t;
 }
 
@@ -878,10 +1109,11 @@ static const float *ctwt(CodecModel *m, const float *w, int ci, int co, int Kw, 
     if (it != m->wt.end()) return it->second;
     float *t = nullptr;
     const size_t cnt = (size_t)co * ci * Kw;
-    if (!w || hipMalloc(&t, cnt * 4) != hipSuccess) return nullptr;
+    if (!w || hipMalloc(&t, cnt * 10) != hipSuccess) return nullptr;
     hipLaunchKernelGGL(k_wt_tconv, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, w, ci, co, Kw, s, t);
+    wt_planes(t, cnt, st);
     m->wt[key] = t;
-    m->wbytes += cnt * 4;
+    m->wbytes += cnt * 10;
     return t;
 }
 
@@ -1078,8 +1310,9 @@ extern "C" int qtts_hip_causal_conv1d(float *out, const float *in, const float *
     g.C = out; g.ldc = L; g.emode = XE_BIAS_M; g.bias = b;
     float *t = nullptr;
     const size_t cnt = (size_t)co * ci * k;
-    if (hipMalloc(&t, cnt * 4) != hipSuccess) return -1;
+    if (hipMalloc(&t, cnt * 10) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_wt_relayout, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, w, co, ci, k, t);
+    wt_planes(t, cnt, st);
     g.wt = t;
     const int rc = qtts_xgemm(g, st);
     if (hipStreamSynchronize(st) != hipSuccess) { hipFree(t); return -1; }
