@@ -86,6 +86,12 @@ int qtts_dev_begin(qtts_dev_t *dev, int nb, int max_frames, int max_prefill, con
  *   p_len, n_trailing prefill / trailing lengths; pad_row = text row of tts_pad */
 int qtts_dev_prompt(qtts_dev_t *dev, int b, const int *text_ids, int n_text, const int *plan, int nplan,
                     int p_len, int n_trailing, int pad_row);
+/* Voice-clone inputs consumed by the next qtts_dev_prompt (no c/ counterpart;
+ * modeling_qwen3_tts.py:1967-2019, 2150-2190): reference codes
+ * [n_ref][num_code_groups] that plan codec ids <= -3 address (-3 - frame: the
+ * frame's 16 group embeddings summed), and the speaker x-vector [hidden] that
+ * codec id -2 adds (NULL: none). */
+int qtts_dev_prompt_ref(qtts_dev_t *dev, const int *ref_codes, int n_ref, const float *spk);
 /* Talker prefill of all nb slots (leaves each slot's last raw hidden). */
 int qtts_dev_prefill(qtts_dev_t *dev);
 /* Enqueues frame `step` (step 0: codec_head on the prefill hidden; step > 0:

@@ -208,6 +208,21 @@ void qwen_tts_set_device(int device);
  * set; returns 0 when every utterance produced audio. */
 int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                             const char *const *languages, float **out_audio, int *out_samples);
+/* Voice clone (no c/ counterpart: the Python reference's generate_voice_clone,
+ * qwen3_tts_model.py:506-630, modeling_qwen3_tts.py:1967-2232).  The
+ * reference-audio encoders are not part of this library: the caller passes
+ * the 12 Hz codes of the reference audio (ref_codes [n_ref_frames][16]) and/or
+ * the speaker encoder's x-vector (spk_embed [talker hidden]).
+ *   ICL mode  : ref_codes + ref_text (ids CSV of
+ *               "<|im_start|>assistant\n{ref}<|im_end|>\n"), spk_embed optional;
+ *               the audio is decoded from reference ++ generated codes and the
+ *               reference part cut off, as the Python reference does.
+ *   x-vector  : ref_codes NULL / n_ref_frames 0, spk_embed set.
+ * non_streaming selects the non-streaming text layout.  Returns malloc'd PCM
+ * (caller frees); NULL on error. */
+float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                     const int *ref_codes, int n_ref_frames, const float *spk_embed,
+                                     const char *language, int non_streaming, int *out_samples);
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);

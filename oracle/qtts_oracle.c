@@ -811,15 +811,128 @@ API int orc_build_prompt(orc_t *m, const int *ids, int n, int spk, int lang,
     return P;
 }
 
-/* Q.c:1059-1443 minus I/O: returns the number of generated frames; codes
- * [frames,16]; *stop = 1 eos / 2 max_tokens; audio via orc_codec_decode. */
-API int orc_generate_codes(orc_t *m, const int *ids, int n, int spk, int lang,
-                           const orc_params_t *pp, int *codes, int max_frames, int *stop) {
-    int H = m->d[D_H], V = m->d[D_V], G = m->d[D_G], eos = m->d[D_EOS];
+/* Voice-clone (ICL) prompt: the Python reference's layout, which the c/
+ * reference does not have (modeling_qwen3_tts.py:2104-2190 + generate_icl_prompt
+ * :1967-2019).  PARITY UNPINNED: no C oracle and the Python package is not
+ * importable here; this restates its published layout in the
+ * fp32 arithmetic of the c/ path (embeddings bf16 -> f32, sums in f32).
+ *   prefill = proj(ids[0:3]),
+ *             (tts_pad x (nc-2), tts_bos) + [prefix codec ids.., spk_vec?, pad]
+ *             then ICL rows, text_embed = proj(ref_ids[3:-2] ++ ids[3:-5]) ++ tts_eos,
+ *                            codec_embed = codec_emb(bos) ++ sum_g emb_g(ref_codes[f][g])
+ *     non_streaming: text_embed + codec_emb(pad) ; codec_embed + tts_pad ; trailing = [tts_pad]
+ *     streaming:     text longer:  text_embed[:Lc] + codec_embed ; trailing = text_embed[Lc:]
+ *                    else: (text_embed ++ tts_pad..) + codec_embed ; trailing = [tts_pad]
+ * spk_vec (H floats, the speaker encoder's x-vector) or NULL; ref_codes may be
+ * NULL / n_ref_frames 0 (x-vector-only mode: the plain layout with the vector
+ * in the speaker slot).  Returns the prefill length; prefill must hold
+ * 10 + n_ref_ids + n + n_ref_frames rows, trailing n + n_ref_ids + 1 rows. */
+static void ref_frame_sum(orc_t *m, const int *fr, float *dst) {
+    int H = m->d[D_H], G = m->d[D_G], Vs = m->d[D_VS], V = m->d[D_V];
+    const tens_t *ce = find(m, "talker.model.codec_embedding.weight");
+    for (int i = 0; i < H; i++) dst[i] = 0.0f;
+    if (fr[0] >= 0 && fr[0] < V)
+        for (int i = 0; i < H; i++) dst[i] += el(ce, (long)fr[0] * H + i);
+    for (int g = 1; g < G; g++) {
+        if (fr[g] < 0 || fr[g] >= Vs) continue;
+        const tens_t *e = findf(m, "talker.code_predictor.model.codec_embedding.%d.weight", g - 1, 0);
+        for (int i = 0; i < H; i++) dst[i] += el(e, (long)fr[g] * H + i);
+    }
+}
+API int orc_build_icl_prompt(orc_t *m, const int *ids, int n, const int *ref_ids, int n_ref_ids,
+                             const int *ref_codes, int n_ref_frames, const float *spk_vec, int lang,
+                             int non_streaming, float *prefill, float *trailing, int *n_trailing) {
+    int H = m->d[D_H];
     if (n < 8) return -1;
-    float *prefill = calloc((size_t)16 * H, sizeof(float)), *trail = calloc((size_t)n * H, sizeof(float));
-    int ntr = 0;
-    int P = orc_build_prompt(m, ids, n, spk, lang, prefill, trail, &ntr);
+    int pre[8], np = 0;
+    if (lang < 0) { pre[np++] = m->d[D_NOTHINK]; pre[np++] = m->d[D_THINK_BOS]; pre[np++] = m->d[D_THINK_EOS]; }
+    else { pre[np++] = m->d[D_THINK]; pre[np++] = m->d[D_THINK_BOS]; pre[np++] = lang; pre[np++] = m->d[D_THINK_EOS]; }
+    const int spk_slot = spk_vec ? np : -1;
+    if (spk_vec) pre[np++] = -2;
+    pre[np++] = m->d[D_PAD];
+    pre[np++] = m->d[D_BOS];
+    float *pad = malloc(H * sizeof(float)), *bos = malloc(H * sizeof(float)), *eos = malloc(H * sizeof(float));
+    orc_embed_text(m, 151671, pad); orc_embed_text(m, 151672, bos); orc_embed_text(m, 151673, eos);
+    int P = 0;
+    for (int i = 0; i < 3; i++) orc_embed_text(m, ids[i], prefill + (size_t)P++ * H);
+    for (int i = 0; i < np - 1; i++) {
+        float *d = prefill + (size_t)P++ * H;
+        memcpy(d, i < np - 2 ? pad : bos, H * sizeof(float));
+        if (i == spk_slot) { for (int k = 0; k < H; k++) d[k] += spk_vec[k]; }
+        else add_codec_emb(m, pre[i], d);
+    }
+    if ((!ref_codes || n_ref_frames <= 0) && non_streaming) {   /* M.py:2203-2226 */
+        for (int i = 0; i < n - 8; i++) {
+            float *d = prefill + (size_t)P++ * H;
+            orc_embed_text(m, ids[3 + i], d);
+            add_codec_emb(m, m->d[D_PAD], d);
+        }
+        float *d = prefill + (size_t)P++ * H;
+        memcpy(d, eos, H * sizeof(float));
+        add_codec_emb(m, m->d[D_PAD], d);
+        d = prefill + (size_t)P++ * H;
+        memcpy(d, pad, H * sizeof(float));
+        add_codec_emb(m, m->d[D_BOS], d);
+        memcpy(trailing, pad, H * sizeof(float));
+        *n_trailing = 1;
+        free(pad); free(bos); free(eos);
+        return P;
+    }
+    if (!ref_codes || n_ref_frames <= 0) {      /* x-vector only: the plain tail (M.py:2191-2202, 2227-2232) */
+        float *d = prefill + (size_t)P++ * H;
+        orc_embed_text(m, ids[3], d);
+        add_codec_emb(m, m->d[D_BOS], d);
+        int nt = (n - 4 - 5) + 1; if (nt < 1) nt = 1;
+        for (int i = 0; i < nt - 1; i++) orc_embed_text(m, ids[4 + i], trailing + (size_t)i * H);
+        memcpy(trailing + (size_t)(nt - 1) * H, eos, H * sizeof(float));
+        *n_trailing = nt;
+        free(pad); free(bos); free(eos);
+        return P;
+    }
+    const int nr = n_ref_ids - 5 > 0 ? n_ref_ids - 5 : 0, nx = n - 8 > 0 ? n - 8 : 0;
+    const int Lt = nr + nx + 1, Lc = n_ref_frames + 1, G = m->d[D_G];
+    float *te = malloc((size_t)Lt * H * sizeof(float)), *cemb = malloc((size_t)Lc * H * sizeof(float));
+    for (int i = 0; i < nr; i++) orc_embed_text(m, ref_ids[3 + i], te + (size_t)i * H);
+    for (int i = 0; i < nx; i++) orc_embed_text(m, ids[3 + i], te + (size_t)(nr + i) * H);
+    memcpy(te + (size_t)(Lt - 1) * H, eos, H * sizeof(float));
+    for (int k = 0; k < H; k++) cemb[k] = 0.0f;
+    add_codec_emb(m, m->d[D_BOS], cemb);
+    for (int f = 0; f < n_ref_frames; f++) ref_frame_sum(m, ref_codes + (size_t)f * G, cemb + (size_t)(f + 1) * H);
+    if (non_streaming) {
+        for (int i = 0; i < Lt; i++) {
+            float *d = prefill + (size_t)P++ * H;
+            memcpy(d, te + (size_t)i * H, H * sizeof(float));
+            add_codec_emb(m, m->d[D_PAD], d);
+        }
+        for (int j = 0; j < Lc; j++) {
+            float *d = prefill + (size_t)P++ * H;
+            for (int k = 0; k < H; k++) d[k] = pad[k] + cemb[(size_t)j * H + k];
+        }
+        memcpy(trailing, pad, H * sizeof(float));
+        *n_trailing = 1;
+    } else {
+        for (int j = 0; j < Lc; j++) {
+            float *d = prefill + (size_t)P++ * H;
+            const float *t = j < Lt ? te + (size_t)j * H : pad;
+            for (int k = 0; k < H; k++) d[k] = t[k] + cemb[(size_t)j * H + k];
+        }
+        if (Lt > Lc) {
+            memcpy(trailing, te + (size_t)Lc * H, (size_t)(Lt - Lc) * H * sizeof(float));
+            *n_trailing = Lt - Lc;
+        } else {
+            memcpy(trailing, pad, H * sizeof(float));
+            *n_trailing = 1;
+        }
+    }
+    free(te); free(cemb); free(pad); free(bos); free(eos);
+    return P;
+}
+
+/* Q.c:1282-1373 decode loop from an already-built prompt: returns the number
+ * of generated frames; codes [frames,16]; *stop = 1 eos / 2 max_tokens. */
+API int orc_generate_from_prompt(orc_t *m, const float *prefill, int P, const float *trail, int ntr,
+                                 const orc_params_t *pp, int *codes, int max_frames, int *stop) {
+    int H = m->d[D_H], V = m->d[D_V], G = m->d[D_G], eos = m->d[D_EOS];
     float *pad = malloc(H * sizeof(float));
     orc_embed_text(m, 151671, pad);
     orc_talker_prefill(m, prefill, P, NULL);
@@ -858,6 +971,20 @@ API int orc_generate_codes(orc_t *m, const int *ids, int n, int spk, int lang,
         const float *tt = step < ntr ? trail + (size_t)step * H : pad;
         for (int i = 0; i < H; i++) nx[i] += tt[i];
     }
-    free(prefill); free(trail); free(pad); free(hist); free(lg); free(nx);
+    free(pad); free(hist); free(lg); free(nx);
+    return ng;
+}
+
+/* Q.c:1059-1443 minus I/O: returns the number of generated frames; codes
+ * [frames,16]; *stop = 1 eos / 2 max_tokens; audio via orc_codec_decode. */
+API int orc_generate_codes(orc_t *m, const int *ids, int n, int spk, int lang,
+                           const orc_params_t *pp, int *codes, int max_frames, int *stop) {
+    int H = m->d[D_H];
+    if (n < 8) return -1;
+    float *prefill = calloc((size_t)16 * H, sizeof(float)), *trail = calloc((size_t)n * H, sizeof(float));
+    int ntr = 0;
+    int P = orc_build_prompt(m, ids, n, spk, lang, prefill, trail, &ntr);
+    int ng = orc_generate_from_prompt(m, prefill, P, trail, ntr, pp, codes, max_frames, stop);
+    free(prefill); free(trail);
     return ng;
 }

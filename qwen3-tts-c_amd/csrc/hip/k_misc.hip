@@ -27,7 +27,10 @@ __global__ __launch_bounds__(256) void k_embed_sum(EmbedSumArgs a) {
     if (a.advance && blockIdx.x == 0 && threadIdx.x == 0) a.kv_len[b] += 1;
 }
 
-// prompt rows (c/qwen_tts.c:1192-1243): dst = proj_row (+ codec_emb[id])
+// prompt rows (c/qwen_tts.c:1192-1243): dst = proj_row (+ codec_emb[id]);
+// voice clone (modeling_qwen3_tts.py:1967-2019, 2150-2190): + the speaker
+// x-vector, or + a reference frame's group-embedding sum (0 + e_0 + ... + e_15
+// in that order, out-of-range codes contribute nothing; oracle ref_frame_sum)
 __global__ __launch_bounds__(256) void k_prompt(PromptArgs a) {
 #pragma clang fp contract(off)
     const int e = blockIdx.y;
@@ -35,9 +38,19 @@ __global__ __launch_bounds__(256) void k_prompt(PromptArgs a) {
     const int src = pl[0], cid = pl[1], kind = pl[2], b = pl[3], slot = pl[4];
     float *dst = kind == 0 ? a.prefill + ((size_t)b * a.p_cap + slot) * a.H
                            : a.trailing + ((size_t)b * a.tr_cap + slot) * a.H;
+    const int f = -3 - cid;
+    const int *fr = cid <= -3 && f < a.n_ref ? a.ref_codes + (size_t)f * a.G : nullptr;
     for (int d = blockIdx.x * 256 + threadIdx.x; d < a.H; d += gridDim.x * 256) {
         float v = a.proj[(size_t)src * a.H + d];
         if (cid >= 0) v += bf2f(a.codec_emb[(size_t)cid * a.H + d]);
+        else if (cid == -2 && a.spk) v += a.spk[d];
+        else if (fr) {
+            float s = 0.0f;
+            if (fr[0] >= 0 && fr[0] < a.V) s += bf2f(a.codec_emb[(size_t)fr[0] * a.H + d]);
+            for (int g = 1; g < a.G; ++g)
+                if (fr[g] >= 0 && fr[g] < a.Vs) s += bf2f(a.st_emb[((size_t)(g - 1) * a.Vs + fr[g]) * a.H + d]);
+            v += s;
+        }
         dst[d] = v;
     }
 }

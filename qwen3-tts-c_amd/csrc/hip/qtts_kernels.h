@@ -152,9 +152,15 @@ int qtts_embed_sum(const EmbedSumArgs &a, hipStream_t st);
 // prompt assembly: prefill rows [B][p_cap][H] and trailing rows [B][tr_cap][H]
 struct PromptArgs {
     const float *proj = nullptr;   // projected text rows [nrows][H]
-    const int *plan = nullptr;     // per output row: {proj_row, codec_id(-1 none), dest_kind(0 prefill/1 trailing), b, slot}
+    const int *plan = nullptr;     // per output row: {proj_row, codec_id, dest_kind(0 prefill/1 trailing), b, slot}
+                                   // codec_id >= 0 codec_emb row, -1 none, -2 spk vector,
+                                   // <= -3 reference frame (-3 - id): sum of its G group embeddings
     int nplan = 0, H = 0;
     const bf16_t *codec_emb = nullptr;
+    const bf16_t *st_emb = nullptr;   // [G-1][Vs][H] sub-talker input embeddings (reference frames)
+    const float *spk = nullptr;       // [H] speaker x-vector (voice clone)
+    const int *ref_codes = nullptr;   // [n_ref][G] reference codes (voice clone ICL)
+    int n_ref = 0, G = 0, V = 0, Vs = 0;
     float *prefill = nullptr;
     int p_cap = 0;
     float *trailing = nullptr;

@@ -118,6 +118,10 @@ struct qtts_dev {
     float *px = nullptr, *pqkv = nullptr, *patt = nullptr, *ph = nullptr, *pt1 = nullptr, *pproj = nullptr;
     int *prow_b = nullptr, *ppos = nullptr, *psrc = nullptr, *pids = nullptr, *pplan = nullptr, *plast = nullptr;
     int ids_cap = 0;
+    // voice-clone prompt inputs of the next qtts_dev_prompt (qtts_dev_prompt_ref)
+    int *pref = nullptr;
+    float *pspk = nullptr;
+    int pref_cap = 0, n_pref = 0, has_spk = 0;
     std::vector<int> p_len_h, n_tr_h;
     qtts_gen_params_t par{};
     bool have_par = false;
@@ -1049,6 +1053,30 @@ static int ensure_trailing(qtts_dev *dv, int n_tr) {
     return 0;
 }
 
+// voice-clone inputs for the next qtts_dev_prompt: reference codes
+// [n_ref][G] (plan codec ids <= -3) and the speaker x-vector [H] (id -2)
+extern "C" int qtts_dev_prompt_ref(qtts_dev_t *dv, const int *ref_codes, int n_ref, const float *spk) {
+    if (!dv || n_ref < 0 || (n_ref > 0 && !ref_codes)) return -1;
+    hipSetDevice(dv->device);
+    const qtts_dims_t &d = dv->d;
+    if (!dv->pspk) {
+        dv->pspk = (float *)dalloc(dv, (size_t)d.H * 4, true);
+        if (!dv->pspk) return -1;
+    }
+    if (n_ref > dv->pref_cap) {
+        const int cap = n_ref < 512 ? 512 : n_ref;
+        dv->pref = (int *)dalloc(dv, (size_t)cap * d.G * 4, true);   // lives with the weights (freed at destroy)
+        if (!dv->pref) return -1;
+        dv->pref_cap = cap;
+    }
+    CK(hipStreamSynchronize(dv->st));
+    if (n_ref > 0) CK(hipMemcpy(dv->pref, ref_codes, (size_t)n_ref * d.G * 4, hipMemcpyHostToDevice));
+    if (spk) CK(hipMemcpy(dv->pspk, spk, (size_t)d.H * 4, hipMemcpyHostToDevice));
+    dv->n_pref = n_ref;
+    dv->has_spk = spk != nullptr;
+    return 0;
+}
+
 extern "C" int qtts_dev_prompt(qtts_dev_t *dv, int b, const int *text_ids, int n_text, const int *plan, int nplan,
                                int p_len, int n_trailing, int pad_row) {
     if (!dv || b < 0 || b >= dv->nb || p_len > dv->p_cap || n_text < 1) return -1;
@@ -1056,10 +1084,11 @@ extern "C" int qtts_dev_prompt(qtts_dev_t *dv, int b, const int *text_ids, int n
     const qtts_dims_t &d = dv->d;
     CKI(ensure_trailing(dv, n_trailing));
     CK(hipStreamSynchronize(dv->st));
-    if (n_text > dv->ids_cap) {
+    if (n_text > dv->ids_cap || nplan > 4 * dv->ids_cap) {
         int cap = n_text < 256 ? 256 : n_text;
+        if (4 * cap < nplan) cap = (nplan + 3) / 4;
         dv->pids = (int *)dalloc(dv, (size_t)cap * 4, false);
-        dv->pplan = (int *)dalloc(dv, (size_t)cap * 4 * 5 + 64, false);
+        dv->pplan = (int *)dalloc(dv, (size_t)4 * cap * 5 * 4, false);   // 4 * cap plan rows of 5 ints
         dv->pt1 = (float *)dalloc(dv, (size_t)cap * d.TH * 4, false);
         dv->pproj = (float *)dalloc(dv, (size_t)cap * d.H * 4, false);
         if (!dv->pids || !dv->pplan || !dv->pt1 || !dv->pproj) return -1;
@@ -1081,7 +1110,11 @@ extern "C" int qtts_dev_prompt(qtts_dev_t *dv, int b, const int *text_ids, int n
     PromptArgs pa;
     pa.proj = dv->pproj; pa.plan = dv->pplan; pa.nplan = nplan; pa.H = d.H; pa.codec_emb = dv->codec_emb;
     pa.prefill = dv->prefill; pa.p_cap = dv->p_cap; pa.trailing = dv->trailing; pa.tr_cap = dv->tr_cap;
+    pa.st_emb = dv->st_emb; pa.G = d.G; pa.V = d.V; pa.Vs = d.Vs;
+    pa.spk = dv->has_spk ? dv->pspk : nullptr;
+    pa.ref_codes = dv->n_pref > 0 ? dv->pref : nullptr; pa.n_ref = dv->n_pref;
     CKI(qtts_prompt_assemble(pa, dv->st));
+    dv->n_pref = 0; dv->has_spk = 0;   // consumed
     if (pad_row >= 0) CK(hipMemcpyAsync(dv->pad_emb, dv->pproj + (size_t)pad_row * d.H, (size_t)d.H * 4,
                                         hipMemcpyDeviceToDevice, dv->st));
     CK(hipMemcpyAsync(dv->n_trailing + b, &n_trailing, 4, hipMemcpyHostToDevice, dv->st));

@@ -406,6 +406,80 @@ static int build_prompt(const qwen_tts_ctx_t *ctx, const int *ids, int n, int sp
     return 0;
 }
 
+/* Voice clone (no c/ counterpart; the Python reference's layout,
+ * modeling_qwen3_tts.py:2104-2232 + generate_icl_prompt :1967-2019; restated
+ * by oracle/qtts_oracle.c orc_build_icl_prompt).  The speaker x-vector takes
+ * the speaker-id slot (plan codec id -2); reference frames are plan codec ids
+ * -3 - f (their 16 group embeddings summed on the device). */
+typedef struct {
+    const int *ref_ids;      /* ids of "<|im_start|>assistant\n{ref_text}<|im_end|>\n" (ICL) */
+    int n_ref_ids;
+    const int *ref_codes;    /* [n_ref][16] codes of the reference audio; NULL: x-vector only */
+    int n_ref;
+    const float *spk;        /* [hidden] speaker x-vector or NULL */
+    int non_streaming;
+} vclone_t;
+
+static int build_icl_prompt(const qwen_tts_ctx_t *ctx, const int *ids, int n, const vclone_t *vc, int lang, int b,
+                            prompt_t *pr) {
+    const qwen_tts_config_t *c = &ctx->config;
+    int prefix[8], np = 0;
+    if (lang < 0) {
+        prefix[np++] = c->codec_nothink_id; prefix[np++] = c->codec_think_bos_id; prefix[np++] = c->codec_think_eos_id;
+    } else {
+        prefix[np++] = c->codec_think_id; prefix[np++] = c->codec_think_bos_id; prefix[np++] = lang;
+        prefix[np++] = c->codec_think_eos_id;
+    }
+    if (vc->spk) prefix[np++] = -2;
+    prefix[np++] = c->codec_pad_id;
+    prefix[np++] = c->codec_bos_id;
+    const int icl = vc->ref_codes && vc->n_ref > 0;
+    const int nr = icl && vc->n_ref_ids > 5 ? vc->n_ref_ids - 5 : 0, nx = n - 8 > 0 ? n - 8 : 0;
+    /* text rows: 0-2 role, 3 pad, 4 bos, 5 eos, 6.. ref content ++ text content */
+    /* (a plain-tail prompt of 8 ids still projects ids[3], as build_prompt does) */
+    pr->n_text = 6 + nr + (!icl && nx == 0 ? 1 : nx);
+    pr->text = (int *)malloc(pr->n_text * sizeof(int));
+    int *t = pr->text;
+    t[0] = ids[0]; t[1] = ids[1]; t[2] = ids[2];
+    t[3] = QWEN_TTS_TOKEN_TTS_PAD; t[4] = QWEN_TTS_TOKEN_TTS_BOS; t[5] = QWEN_TTS_TOKEN_TTS_EOS;
+    for (int i = 0; i < nr; i++) t[6 + i] = vc->ref_ids[3 + i];
+    for (int i = 0; i < nx; i++) t[6 + nr + i] = ids[3 + i];
+    if (!icl && nx == 0) t[6] = ids[3];
+    const int Lt = nr + nx + 1, Lc = icl ? vc->n_ref + 1 : 0;
+    pr->plan = (int *)malloc((size_t)(3 + np + 2 * (Lt + Lc) + 4) * 5 * sizeof(int));
+    int k = 0, P = 0, nt = 0;
+#define ROW(src, cid, kind, slot) do { int *r_ = pr->plan + 5 * k++; r_[0] = src; r_[1] = cid; r_[2] = kind; r_[3] = b; r_[4] = slot; } while (0)
+#define TROW(j) ((j) < nr + nx ? 6 + (j) : 5)
+#define CID(j) ((j) == 0 ? c->codec_bos_id : -3 - ((j) - 1))
+    for (int i = 0; i < 3; i++) ROW(i, -1, 0, P++);
+    for (int i = 0; i < np - 1; i++) ROW(i < np - 2 ? 3 : 4, prefix[i], 0, P++);
+    if (!icl && !vc->non_streaming) {           /* x-vector only: the plain tail */
+        ROW(6, c->codec_bos_id, 0, P++);        /* ids[3] = text row 6 */
+        for (int j = 1; j < nx; j++) ROW(6 + j, -1, 1, nt++);
+        ROW(5, -1, 1, nt++);
+    } else if (!icl) {                          /* x-vector only, non-streaming (M.py:2203-2226) */
+        for (int j = 0; j < Lt; j++) ROW(TROW(j), c->codec_pad_id, 0, P++);
+        ROW(3, c->codec_bos_id, 0, P++);
+        ROW(3, -1, 1, nt++);
+    } else if (vc->non_streaming) {
+        for (int j = 0; j < Lt; j++) ROW(TROW(j), c->codec_pad_id, 0, P++);
+        for (int j = 0; j < Lc; j++) ROW(3, CID(j), 0, P++);
+        ROW(3, -1, 1, nt++);
+    } else {
+        for (int j = 0; j < Lc; j++) ROW(j < Lt ? TROW(j) : 3, CID(j), 0, P++);
+        if (Lt > Lc) for (int j = Lc; j < Lt; j++) ROW(TROW(j), -1, 1, nt++);
+        else ROW(3, -1, 1, nt++);
+    }
+#undef CID
+#undef TROW
+#undef ROW
+    pr->nplan = k;
+    pr->p_len = P;
+    pr->n_trailing = nt;
+    pr->pad_row = 3;
+    return 0;
+}
+
 static void lookup(const qwen_tts_ctx_t *ctx, const char *speaker, const char *language, int *spk, int *lang) {
     const qwen_tts_config_t *c = &ctx->config;
     *spk = -1;
@@ -439,7 +513,7 @@ typedef struct {                 /* streaming output of run_batch (nb == 1) */
 
 static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                      const char *const *languages, float **audio, int *samples, double t_start,
-                     const stream_t *stream) {
+                     const stream_t *stream, const vclone_t *vc) {
     qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
     const qwen_tts_config_t *c = &ctx->config;
     const int G = c->num_code_groups;
@@ -462,7 +536,8 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             }
         int spk, lang;
         lookup(ctx, speakers ? speakers[b] : NULL, languages ? languages[b] : NULL, &spk, &lang);
-        build_prompt(ctx, ids, n, spk, lang, b, &pr[b]);
+        if (vc) build_icl_prompt(ctx, ids, n, vc, lang, b, &pr[b]);
+        else build_prompt(ctx, ids, n, spk, lang, b, &pr[b]);
         free(ids);
         if (pr[b].p_len > max_p) max_p = pr[b].p_len;
     }
@@ -473,7 +548,8 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     params_of(ctx, &gp);
     if (qtts_dev_begin(dev, nb, max_tokens, max_p, &gp) != 0) goto out;
     for (int b = 0; b < nb; b++)
-        if (qtts_dev_prompt(dev, b, pr[b].text, pr[b].n_text, pr[b].plan, pr[b].nplan, pr[b].p_len,
+        if ((vc && qtts_dev_prompt_ref(dev, vc->ref_codes, vc->ref_codes ? vc->n_ref : 0, vc->spk) != 0) ||
+            qtts_dev_prompt(dev, b, pr[b].text, pr[b].n_text, pr[b].plan, pr[b].nplan, pr[b].p_len,
                             pr[b].n_trailing, pr[b].pad_row) != 0)
             goto out;
     double t_prefill = now_ms();
@@ -501,7 +577,7 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
      * streaming decode).  Off by default: sharing the CUs slowed the latency-
      * bound decode by more than the codec time it hides (profiles/r01g_envsweep.txt). */
     const char *ov_env = getenv("QWEN_TTS_HIP_OVERLAP");
-    const int overlap = !stream && nb == 1 && ov_env && atoi(ov_env);
+    const int overlap = !stream && !vc && nb == 1 && ov_env && atoi(ov_env);
     const int ov_chunk = 16;
     int ov_done = 0;
     if (overlap && qtts_dev_codec_async_begin(dev, max_tokens) != 0) {
@@ -608,6 +684,29 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             rc = -1;
         }
         ctx->perf_codec_ms = now_ms() - t_codec;
+    } else if (vc && vc->ref_codes && vc->n_ref > 0) {
+        /* voice clone: decode reference ++ generated codes, keep the part after
+         * the reference (qwen3_tts_model.py:612-630, the same float cut) */
+        audio[0] = NULL;
+        samples[0] = 0;
+        const int tot = vc->n_ref + ctx->last_frames;
+        int *all = (int *)malloc((size_t)tot * G * sizeof(int)), nw = 0;
+        if (all && ctx->last_frames > 0) {
+            memcpy(all, vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
+            memcpy(all + (size_t)vc->n_ref * G, ctx->last_codes, (size_t)ctx->last_frames * G * sizeof(int));
+            float *w = qtts_dev_codec_decode_host(dev, all, tot, &nw);
+            const int cut = (int)((double)vc->n_ref / (double)tot * (double)nw);
+            if (w && nw > cut) {
+                memmove(w, w + cut, (size_t)(nw - cut) * sizeof(float));
+                audio[0] = w;
+                samples[0] = nw - cut;
+            } else {
+                free(w);
+            }
+        }
+        free(all);
+        if (!audio[0]) rc = -1;
+        ctx->perf_codec_ms = now_ms() - t_codec;
     } else {
         for (int b = 0; b < nb; b++) {
             audio[b] = NULL;
@@ -634,7 +733,7 @@ float *qwen_tts_generate(qwen_tts_ctx_t *ctx, const char *text, const char *spea
     float *audio = NULL;
     int n = 0;
     const char *texts[1] = {text}, *spk[1] = {speaker}, *lang[1] = {language};
-    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start, NULL);
+    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start, NULL, NULL);
     if (rc != 0 || !audio || n <= 0) {
         free(audio);
         *out_samples = 0;
@@ -652,7 +751,52 @@ float *qwen_tts_generate(qwen_tts_ctx_t *ctx, const char *text, const char *spea
 int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                             const char *const *languages, float **out_audio, int *out_samples) {
     if (!ctx || nb < 1 || !texts || !out_audio || !out_samples) return -1;
-    return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms(), NULL);
+    return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms(), NULL, NULL);
+}
+
+float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                     const int *ref_codes, int n_ref_frames, const float *spk_embed,
+                                     const char *language, int non_streaming, int *out_samples) {
+    if (!ctx || !out_samples) return NULL;
+    *out_samples = 0;
+    const int icl = ref_codes && n_ref_frames > 0;
+    if (!icl && !spk_embed) {
+        fprintf(stderr, "Error: voice clone needs reference codes or a speaker embedding\n");
+        return NULL;
+    }
+    vclone_t vc = {0};
+    int *rid = NULL;
+    if (icl) {
+        vc.n_ref_ids = ref_text ? parse_ids(ref_text, &rid) : 0;
+        if (vc.n_ref_ids < 5) {
+            fprintf(stderr, "Error: ICL voice clone needs the reference text ids (chat template, >= 5 ids)\n");
+            free(rid);
+            return NULL;
+        }
+        for (int i = 0; i < vc.n_ref_ids; i++)
+            if (rid[i] < 0 || rid[i] >= ctx->config.talker_text_vocab) {
+                fprintf(stderr, "Error: text token id %d out of range\n", rid[i]);
+                free(rid);
+                return NULL;
+            }
+        vc.ref_ids = rid;
+        vc.ref_codes = ref_codes;
+        vc.n_ref = n_ref_frames;
+    }
+    vc.spk = spk_embed;
+    vc.non_streaming = non_streaming;
+    double t_start = now_ms();
+    float *audio = NULL;
+    int n = 0;
+    const char *texts[1] = {text}, *lang[1] = {language};
+    int rc = run_batch(ctx, 1, texts, NULL, lang, &audio, &n, t_start, NULL, &vc);
+    free(rid);
+    if (rc != 0 || !audio || n <= 0) {
+        free(audio);
+        return NULL;
+    }
+    *out_samples = n;
+    return audio;
 }
 
 float *qwen_tts_generate_stream(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
@@ -665,7 +809,7 @@ float *qwen_tts_generate_stream(qwen_tts_ctx_t *ctx, const char *text, const cha
     int n = 0;
     const char *texts[1] = {text}, *spk[1] = {speaker}, *lang[1] = {language};
     ctx->perf_first_packet_ms = 0;
-    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start, &st);
+    int rc = run_batch(ctx, 1, texts, spk, lang, &audio, &n, t_start, &st, NULL);
     if (rc != 0 || !audio || n <= 0) {
         free(audio);
         return NULL;

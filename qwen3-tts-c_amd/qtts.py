@@ -65,9 +65,9 @@ EXPORTS = [
     "qwen_tts_talker_prefill", "qwen_tts_talker_forward", "qwen_tts_subtalker_generate", "qwen_tts_codec_decode",
     "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
-    "qwen_tts_codec_stream_push",
+    "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
-    "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
+    "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
     "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
     "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_decode_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
@@ -119,6 +119,9 @@ def lib():
     L.qwen_tts_generate_stream.restype = C.c_void_p
     L.qwen_tts_generate_stream.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, AUDIO_CB,
                                            C.c_void_p, _ip]
+    L.qwen_tts_generate_voice_clone.restype = C.c_void_p
+    L.qwen_tts_generate_voice_clone.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, _ip, C.c_int, _fp,
+                                                C.c_char_p, C.c_int, _ip]
     L.qwen_tts_codec_stream_begin.argtypes = [C.POINTER(Ctx), C.c_int]
     L.qwen_tts_codec_stream_push.argtypes = [C.POINTER(Ctx), _ip, C.c_int, _fp]
     L.qtts_hip_device_count.restype = C.c_int
@@ -186,6 +189,23 @@ class QwenTTS:
         n = C.c_int(0)
         p = lib().qwen_tts_generate(self.ctx, csv, speaker.encode() if speaker else None,
                                     language.encode() if language else None, C.byref(n))
+        return _take_audio(p, n.value)
+
+    def generate_voice_clone(self, ids, ref_ids=None, ref_codes=None, spk_embed=None, language=None,
+                             non_streaming=False):
+        """Voice clone from reference codes [T, 16] (+ the reference text ids)
+        and / or a speaker x-vector (include/qwen_tts.h
+        qwen_tts_generate_voice_clone; the Python reference's
+        generate_voice_clone minus its audio encoders)."""
+        csv = ",".join(str(int(i)) for i in ids).encode()
+        rcsv = ",".join(str(int(i)) for i in ref_ids).encode() if ref_ids is not None else None
+        rc = None if ref_codes is None else np.ascontiguousarray(ref_codes, np.int32)
+        sv = None if spk_embed is None else np.ascontiguousarray(spk_embed, np.float32)
+        n = C.c_int(0)
+        p = lib().qwen_tts_generate_voice_clone(
+            self.ctx, csv, rcsv, None if rc is None else rc.ctypes.data_as(_ip), 0 if rc is None else rc.shape[0],
+            None if sv is None else sv.ctypes.data_as(_fp), language.encode() if language else None,
+            int(non_streaming), C.byref(n))
         return _take_audio(p, n.value)
 
     def generate_batch(self, id_lists, speakers=None, languages=None):

@@ -80,6 +80,12 @@ def _lib_oracle():
     lib.orc_generate_codes.restype = C.c_int
     lib.orc_generate_codes.argtypes = [C.c_void_p, _ip, C.c_int, C.c_int, C.c_int, C.POINTER(OrcParams),
                                        _ip, C.c_int, _ip]
+    lib.orc_build_icl_prompt.restype = C.c_int
+    lib.orc_build_icl_prompt.argtypes = [C.c_void_p, _ip, C.c_int, _ip, C.c_int, _ip, C.c_int, _fp, C.c_int,
+                                         C.c_int, _fp, _fp, _ip]
+    lib.orc_generate_from_prompt.restype = C.c_int
+    lib.orc_generate_from_prompt.argtypes = [C.c_void_p, _fp, C.c_int, _fp, C.c_int, C.POINTER(OrcParams),
+                                             _ip, C.c_int, _ip]
     return lib
 
 
@@ -166,6 +172,34 @@ class Oracle:
         ntr = C.c_int(0)
         P = self.lib.orc_build_prompt(self.h, iptr(ids), len(ids), spk, lang, fptr(pre), fptr(tr), C.byref(ntr))
         return pre[:P].copy(), tr[:ntr.value].copy()
+
+    def build_icl_prompt(self, ids, ref_ids=None, ref_codes=None, spk_vec=None, lang=-1, non_streaming=False):
+        """Voice-clone prompt (oracle/qtts_oracle.c orc_build_icl_prompt; parity unpinned)."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        rid = np.ascontiguousarray(ref_ids if ref_ids is not None else [], dtype=np.int32)
+        rc = None if ref_codes is None else np.ascontiguousarray(ref_codes, dtype=np.int32)
+        nrf = 0 if rc is None else rc.shape[0]
+        H = self.cfg["H"]
+        pre = np.zeros((12 + len(rid) + len(ids) + nrf, H), np.float32)
+        tr = np.zeros((len(ids) + len(rid) + 2, H), np.float32)
+        ntr = C.c_int(0)
+        sv = None if spk_vec is None else np.ascontiguousarray(spk_vec, dtype=np.float32)
+        P = self.lib.orc_build_icl_prompt(self.h, iptr(ids), len(ids), iptr(rid), len(rid),
+                                          None if rc is None else iptr(rc), nrf, None if sv is None else fptr(sv),
+                                          lang, int(non_streaming), fptr(pre), fptr(tr), C.byref(ntr))
+        assert P > 0
+        return pre[:P].copy(), tr[:ntr.value].copy()
+
+    def generate_from_prompt(self, prefill, trailing, max_frames=4096, **params):
+        p = make_params(**params)
+        cap = min(max_frames, p.fixed if p.fixed > 0 else p.max_tokens)
+        codes = np.zeros((max(cap, 1), self.cfg["G"]), np.int32)
+        stop = C.c_int(0)
+        pre = np.ascontiguousarray(prefill, np.float32)
+        tr = np.ascontiguousarray(trailing, np.float32)
+        n = self.lib.orc_generate_from_prompt(self.h, fptr(pre), pre.shape[0], fptr(tr), tr.shape[0], C.byref(p),
+                                              iptr(codes), cap, C.byref(stop))
+        return codes[:n].copy(), stop.value
 
     def generate_codes(self, ids, spk=-1, lang=-1, max_frames=4096, **params):
         ids = np.ascontiguousarray(ids, dtype=np.int32)

@@ -68,6 +68,23 @@ def test_codec_edge_lengths(tts_tiny, oracle):
         audio_close(tts_tiny.codec_decode(codes), oracle.codec_decode(codes))
 
 
+@pytest.mark.parametrize("P", [17, 64, 65, 200])
+def test_long_prefill_vs_oracle(tts_tiny, oracle, P):
+    """ICL-length prefill (100-250 prompt rows, T.c:254-472):
+    rows past 16 go to the 64-row MFMA GEMM (k_mgemm) in chunks, attention
+    runs causal over the whole prompt; the next decode step then reads all P
+    cached keys.  Hidden and logits against the oracle at the stage bar."""
+    rng = np.random.default_rng(100 + P)
+    H = S["prefill_embeds"].shape[1]
+    e = (rng.standard_normal((P, H)) * 0.5).astype(np.float32)
+    np.testing.assert_allclose(tts_tiny.prefill(e), oracle.prefill(e), atol=1e-4, rtol=1e-4)
+    x = (rng.standard_normal(H) * 0.5).astype(np.float32)
+    lg, hid = tts_tiny.step(x)
+    lgo, hido = oracle.step(x)
+    np.testing.assert_allclose(lg, lgo, atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(hid, hido, atol=1e-4, rtol=1e-4)
+
+
 def _gen(m, name):
     fx, pp, fixed, mx, seed = RUNS[name]
     m.set_params(max_tokens=mx, fixed=fixed, seed=seed, **pp)

@@ -1,0 +1,104 @@
+"""Voice clone (the ICL prompt and its long prefill).
+
+The c/ reference has no voice-clone path; the layout follows the Python
+reference (modeling_qwen3_tts.py:1967-2019 generate_icl_prompt, :2104-2232
+prompt assembly; qwen3_tts_model.py:612-630 decode-with-reference and cut).
+The oracle restates it (oracle/qtts_oracle.c orc_build_icl_prompt).  PARITY
+UNPINNED against the Python reference itself (not importable here, SURVEY.md
+§8c): the pin is the oracle's own identity with the c/-pinned plain prompt
+(x-vector-only without a vector == the custom-voice layout).  The audio
+encoders (ECAPA speaker encoder, 12 Hz tokenizer encoder, §8f N3) are out of
+scope: tests feed synthetic reference codes and x-vectors.
+
+Bars: codes bit-exact (greedy and default sampling), audio as test_gpu_model.
+"""
+import numpy as np
+import pytest
+
+from oracle_py import DEFAULT, GREEDY
+from qtts_io import lookup_ids
+from synth_model import prompt_ids
+
+REF_IDS = [151644, 77091, 198] + list(range(3000, 3012)) + [151645, 198]   # 12 content ids
+
+
+def _inputs(o, T, seed=0, spk=False):
+    rng = np.random.default_rng(seed)
+    codes = rng.integers(0, min(o.cfg["V"], o.cfg["Vs"]), size=(T, o.cfg["G"])).astype(np.int32)
+    sv = (rng.standard_normal(o.cfg["H"]) * 0.05).astype(np.float32) if spk else None
+    return codes, sv
+
+
+# ------------------------------------------------------------------ CPU: the oracle's layout
+def test_xvector_only_without_vector_is_plain_prompt(oracle):
+    _, lang = lookup_ids(oracle.cfg, "aiden", "english")
+    ids = prompt_ids("short")
+    for l in (-1, lang):
+        a = oracle.build_prompt(ids, -1, l)
+        b = oracle.build_icl_prompt(ids, lang=l)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("T,ns", [(5, 0), (20, 0), (20, 1), (3, 1)])
+def test_icl_layout_lengths(oracle, T, ns):
+    _, lang = lookup_ids(oracle.cfg, "aiden", "english")
+    ids = prompt_ids("short")
+    codes, sv = _inputs(oracle, T, spk=True)
+    pre, tr = oracle.build_icl_prompt(ids, REF_IDS, codes, sv, lang, ns)
+    head = 3 + (4 + 1 + 2) - 1                       # role + tag/lang/spk/pad rows
+    Lt, Lc = (len(REF_IDS) - 5) + (len(ids) - 8) + 1, T + 1
+    if ns:
+        assert pre.shape[0] == head + Lt + Lc and tr.shape[0] == 1
+    else:
+        assert pre.shape[0] == head + Lc
+        assert tr.shape[0] == (Lt - Lc if Lt > Lc else 1)
+    pad = oracle.embed_text(151671)
+    if ns or Lt <= Lc:
+        np.testing.assert_array_equal(tr[0], pad)
+    else:   # the text that did not fit under the reference frames, then tts_eos
+        np.testing.assert_array_equal(tr[-1], oracle.embed_text(151673))
+        nr = len(REF_IDS) - 5
+        first = REF_IDS[3 + Lc] if Lc < nr else ids[3 + Lc - nr]
+        np.testing.assert_array_equal(tr[0], oracle.embed_text(first))
+
+
+# ------------------------------------------------------------------ GPU: HIP path vs oracle
+CASES = {
+    # name: (ref frames, spk vector, non_streaming, params)
+    "icl_text_shorter": (20, False, 0, GREEDY),
+    "icl_text_longer": (4, False, 0, GREEDY),
+    "icl_nonstream_spk": (12, True, 1, GREEDY),
+    "icl_spk_sampled": (12, True, 0, DEFAULT),
+    "icl_long_prefill": (150, True, 0, GREEDY),     # ~160 prefill rows: the 64-row MFMA GEMM
+    "xvec_only": (0, True, 0, GREEDY),
+    "xvec_only_nonstream": (0, True, 1, GREEDY),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_voice_clone_vs_oracle(tts_tiny, oracle, name):
+    from test_gpu_model import audio_close
+    T, spk, ns, pp = CASES[name]
+    _, lang = lookup_ids(oracle.cfg, "aiden", "english")
+    ids = prompt_ids("short")
+    codes, sv = _inputs(oracle, max(T, 1), seed=T, spk=spk)
+    rc = codes if T > 0 else None
+    fixed = 4
+    m = tts_tiny
+    m.set_params(max_tokens=4096, fixed=fixed, seed=42, **pp)
+    a = m.generate_voice_clone(ids, REF_IDS if T else None, rc, sv, "english", ns)
+    got = m.last_codes()
+    pre, tr = oracle.build_icl_prompt(ids, REF_IDS if T else None, rc, sv, lang, ns)
+    want, _ = oracle.generate_from_prompt(pre, tr, max_tokens=4096, fixed=fixed, seed=42, **pp)
+    np.testing.assert_array_equal(got, want)
+    full = oracle.codec_decode(np.concatenate([codes, want]) if T else want)
+    tot = T + len(want)
+    cut = int(T / tot * full.shape[0])
+    audio_close(a, full[cut:])
+
+
+@pytest.mark.gpu
+def test_voice_clone_needs_codes_or_vector(tts_tiny):
+    assert tts_tiny.generate_voice_clone(prompt_ids("short")) is None
