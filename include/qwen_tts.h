@@ -223,6 +223,14 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
 float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
                                      const int *ref_codes, int n_ref_frames, const float *spk_embed,
                                      const char *language, int non_streaming, int *out_samples);
+/* nb voice-clone utterances in lock-step frames (BASELINE C5: batch 8 on one
+ * GPU); per-slot arrays as above (ref_codes[b] / spk_embeds[b] may be NULL).
+ * Returns 0 when every utterance produced audio. */
+int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts,
+                                        const char *const *ref_texts, const int *const *ref_codes,
+                                        const int *n_ref_frames, const float *const *spk_embeds,
+                                        const char *const *languages, int non_streaming, float **out_audio,
+                                        int *out_samples);
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);

@@ -513,7 +513,7 @@ typedef struct {                 /* streaming output of run_batch (nb == 1) */
 
 static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                      const char *const *languages, float **audio, int *samples, double t_start,
-                     const stream_t *stream, const vclone_t *vc) {
+                     const stream_t *stream, const vclone_t *vcs /* [nb] or NULL */) {
     qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
     const qwen_tts_config_t *c = &ctx->config;
     const int G = c->num_code_groups;
@@ -536,7 +536,7 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             }
         int spk, lang;
         lookup(ctx, speakers ? speakers[b] : NULL, languages ? languages[b] : NULL, &spk, &lang);
-        if (vc) build_icl_prompt(ctx, ids, n, vc, lang, b, &pr[b]);
+        if (vcs) build_icl_prompt(ctx, ids, n, &vcs[b], lang, b, &pr[b]);
         else build_prompt(ctx, ids, n, spk, lang, b, &pr[b]);
         free(ids);
         if (pr[b].p_len > max_p) max_p = pr[b].p_len;
@@ -548,7 +548,7 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     params_of(ctx, &gp);
     if (qtts_dev_begin(dev, nb, max_tokens, max_p, &gp) != 0) goto out;
     for (int b = 0; b < nb; b++)
-        if ((vc && qtts_dev_prompt_ref(dev, vc->ref_codes, vc->ref_codes ? vc->n_ref : 0, vc->spk) != 0) ||
+        if ((vcs && qtts_dev_prompt_ref(dev, vcs[b].ref_codes, vcs[b].ref_codes ? vcs[b].n_ref : 0, vcs[b].spk) != 0) ||
             qtts_dev_prompt(dev, b, pr[b].text, pr[b].n_text, pr[b].plan, pr[b].nplan, pr[b].p_len,
                             pr[b].n_trailing, pr[b].pad_row) != 0)
             goto out;
@@ -577,7 +577,7 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
      * streaming decode).  Off by default: sharing the CUs slowed the latency-
      * bound decode by more than the codec time it hides (profiles/r01g_envsweep.txt). */
     const char *ov_env = getenv("QWEN_TTS_HIP_OVERLAP");
-    const int overlap = !stream && !vc && nb == 1 && ov_env && atoi(ov_env);
+    const int overlap = !stream && !vcs && nb == 1 && ov_env && atoi(ov_env);
     const int ov_chunk = 16;
     int ov_done = 0;
     if (overlap && qtts_dev_codec_async_begin(dev, max_tokens) != 0) {
@@ -684,34 +684,33 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             rc = -1;
         }
         ctx->perf_codec_ms = now_ms() - t_codec;
-    } else if (vc && vc->ref_codes && vc->n_ref > 0) {
-        /* voice clone: decode reference ++ generated codes, keep the part after
-         * the reference (qwen3_tts_model.py:612-630, the same float cut) */
-        audio[0] = NULL;
-        samples[0] = 0;
-        const int tot = vc->n_ref + ctx->last_frames;
-        int *all = (int *)malloc((size_t)tot * G * sizeof(int)), nw = 0;
-        if (all && ctx->last_frames > 0) {
-            memcpy(all, vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
-            memcpy(all + (size_t)vc->n_ref * G, ctx->last_codes, (size_t)ctx->last_frames * G * sizeof(int));
-            float *w = qtts_dev_codec_decode_host(dev, all, tot, &nw);
-            const int cut = (int)((double)vc->n_ref / (double)tot * (double)nw);
-            if (w && nw > cut) {
-                memmove(w, w + cut, (size_t)(nw - cut) * sizeof(float));
-                audio[0] = w;
-                samples[0] = nw - cut;
-            } else {
-                free(w);
-            }
-        }
-        free(all);
-        if (!audio[0]) rc = -1;
-        ctx->perf_codec_ms = now_ms() - t_codec;
     } else {
         for (int b = 0; b < nb; b++) {
             audio[b] = NULL;
             samples[b] = 0;
             if (ngen[b] <= 0) { rc = -1; continue; }
+            if (vcs && vcs[b].ref_codes && vcs[b].n_ref > 0) {
+                /* voice clone: decode reference ++ generated codes, keep the part
+                 * after the reference (qwen3_tts_model.py:612-630, same float cut) */
+                const vclone_t *vc = &vcs[b];
+                const int tot = vc->n_ref + ngen[b];
+                int *all = (int *)malloc((size_t)tot * G * sizeof(int)), nw = 0;
+                if (all && qtts_dev_get_codes(dev, b, all + (size_t)vc->n_ref * G, ngen[b]) == ngen[b]) {
+                    memcpy(all, vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
+                    float *w = qtts_dev_codec_decode_host(dev, all, tot, &nw);
+                    const int cut = (int)((double)vc->n_ref / (double)tot * (double)nw);
+                    if (w && nw > cut) {
+                        memmove(w, w + cut, (size_t)(nw - cut) * sizeof(float));
+                        audio[b] = w;
+                        samples[b] = nw - cut;
+                    } else {
+                        free(w);
+                    }
+                }
+                free(all);
+                if (!audio[b]) rc = -1;
+                continue;
+            }
             audio[b] = qtts_dev_codec_slot(dev, b, ngen[b], &samples[b]);
             if (!audio[b] || samples[b] <= 0) rc = -1;
         }
@@ -754,44 +753,65 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
     return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms(), NULL, NULL);
 }
 
+int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts,
+                                        const char *const *ref_texts, const int *const *ref_codes,
+                                        const int *n_ref_frames, const float *const *spk_embeds,
+                                        const char *const *languages, int non_streaming, float **out_audio,
+                                        int *out_samples) {
+    if (!ctx || nb < 1 || !texts || !out_audio || !out_samples) return -1;
+    for (int b = 0; b < nb; b++) { out_audio[b] = NULL; out_samples[b] = 0; }
+    vclone_t *vcs = (vclone_t *)calloc(nb, sizeof(vclone_t));
+    int rc = vcs ? 0 : -1;
+    for (int b = 0; b < nb && rc == 0; b++) {
+        vclone_t *vc = &vcs[b];
+        const int *codes = ref_codes ? ref_codes[b] : NULL;
+        const int nref = n_ref_frames ? n_ref_frames[b] : 0;
+        vc->spk = spk_embeds ? spk_embeds[b] : NULL;
+        vc->non_streaming = non_streaming;
+        if (!(codes && nref > 0)) {
+            if (!vc->spk) {
+                fprintf(stderr, "Error: voice clone needs reference codes or a speaker embedding\n");
+                rc = -1;
+            }
+            continue;
+        }
+        int *rid = NULL;
+        vc->n_ref_ids = ref_texts && ref_texts[b] ? parse_ids(ref_texts[b], &rid) : 0;
+        vc->ref_ids = rid;
+        if (vc->n_ref_ids < 5) {
+            fprintf(stderr, "Error: ICL voice clone needs the reference text ids (chat template, >= 5 ids)\n");
+            rc = -1;
+            continue;
+        }
+        for (int i = 0; i < vc->n_ref_ids; i++)
+            if (rid[i] < 0 || rid[i] >= ctx->config.talker_text_vocab) {
+                fprintf(stderr, "Error: text token id %d out of range\n", rid[i]);
+                rc = -1;
+                break;
+            }
+        vc->ref_codes = codes;
+        vc->n_ref = nref;
+    }
+    if (rc == 0) rc = run_batch(ctx, nb, texts, NULL, languages, out_audio, out_samples, now_ms(), NULL, vcs);
+    if (vcs)
+        for (int b = 0; b < nb; b++) free((void *)vcs[b].ref_ids);
+    free(vcs);
+    return rc;
+}
+
 float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
                                      const int *ref_codes, int n_ref_frames, const float *spk_embed,
                                      const char *language, int non_streaming, int *out_samples) {
     if (!ctx || !out_samples) return NULL;
     *out_samples = 0;
-    const int icl = ref_codes && n_ref_frames > 0;
-    if (!icl && !spk_embed) {
-        fprintf(stderr, "Error: voice clone needs reference codes or a speaker embedding\n");
-        return NULL;
-    }
-    vclone_t vc = {0};
-    int *rid = NULL;
-    if (icl) {
-        vc.n_ref_ids = ref_text ? parse_ids(ref_text, &rid) : 0;
-        if (vc.n_ref_ids < 5) {
-            fprintf(stderr, "Error: ICL voice clone needs the reference text ids (chat template, >= 5 ids)\n");
-            free(rid);
-            return NULL;
-        }
-        for (int i = 0; i < vc.n_ref_ids; i++)
-            if (rid[i] < 0 || rid[i] >= ctx->config.talker_text_vocab) {
-                fprintf(stderr, "Error: text token id %d out of range\n", rid[i]);
-                free(rid);
-                return NULL;
-            }
-        vc.ref_ids = rid;
-        vc.ref_codes = ref_codes;
-        vc.n_ref = n_ref_frames;
-    }
-    vc.spk = spk_embed;
-    vc.non_streaming = non_streaming;
-    double t_start = now_ms();
     float *audio = NULL;
     int n = 0;
-    const char *texts[1] = {text}, *lang[1] = {language};
-    int rc = run_batch(ctx, 1, texts, NULL, lang, &audio, &n, t_start, NULL, &vc);
-    free(rid);
-    if (rc != 0 || !audio || n <= 0) {
+    const char *texts[1] = {text}, *rt[1] = {ref_text}, *lang[1] = {language};
+    const int *rc1[1] = {ref_codes};
+    const int nr1[1] = {n_ref_frames};
+    const float *sv1[1] = {spk_embed};
+    if (qwen_tts_generate_voice_clone_batch(ctx, 1, texts, rt, rc1, nr1, sv1, lang, non_streaming, &audio, &n) != 0 ||
+        !audio || n <= 0) {
         free(audio);
         return NULL;
     }

@@ -66,6 +66,7 @@ EXPORTS = [
     "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
     "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
+    "qwen_tts_generate_voice_clone_batch",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -122,6 +123,10 @@ def lib():
     L.qwen_tts_generate_voice_clone.restype = C.c_void_p
     L.qwen_tts_generate_voice_clone.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, _ip, C.c_int, _fp,
                                                 C.c_char_p, C.c_int, _ip]
+    L.qwen_tts_generate_voice_clone_batch.restype = C.c_int
+    L.qwen_tts_generate_voice_clone_batch.argtypes = [C.POINTER(Ctx), C.c_int, C.POINTER(C.c_char_p),
+                                                      C.POINTER(C.c_char_p), C.POINTER(_ip), _ip, C.POINTER(_fp),
+                                                      C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p), _ip]
     L.qwen_tts_codec_stream_begin.argtypes = [C.POINTER(Ctx), C.c_int]
     L.qwen_tts_codec_stream_push.argtypes = [C.POINTER(Ctx), _ip, C.c_int, _fp]
     L.qtts_hip_device_count.restype = C.c_int
@@ -207,6 +212,25 @@ class QwenTTS:
             None if sv is None else sv.ctypes.data_as(_fp), language.encode() if language else None,
             int(non_streaming), C.byref(n))
         return _take_audio(p, n.value)
+
+    def generate_voice_clone_batch(self, id_lists, ref_id_lists, ref_codes, spk_embeds=None, languages=None,
+                                   non_streaming=False):
+        """nb voice-clone utterances in lock step (BASELINE C5).  Returns (rc, [audio])."""
+        nb = len(id_lists)
+        enc = lambda ids: ",".join(str(int(i)) for i in ids).encode() if ids is not None else None
+        tx = (C.c_char_p * nb)(*[enc(i) for i in id_lists])
+        rt = (C.c_char_p * nb)(*[enc(i) for i in (ref_id_lists or [None] * nb)])
+        keep = [None if c is None else np.ascontiguousarray(c, np.int32) for c in (ref_codes or [None] * nb)]
+        rc = (_ip * nb)(*[None if c is None else c.ctypes.data_as(_ip) for c in keep])
+        nr = (C.c_int * nb)(*[0 if c is None else c.shape[0] for c in keep])
+        sk = [None if v is None else np.ascontiguousarray(v, np.float32) for v in (spk_embeds or [None] * nb)]
+        sv = (_fp * nb)(*[None if v is None else v.ctypes.data_as(_fp) for v in sk])
+        lg = (C.c_char_p * nb)(*[(s.encode() if s else None) for s in (languages or [None] * nb)])
+        out = (C.c_void_p * nb)()
+        ns = (C.c_int * nb)()
+        r = lib().qwen_tts_generate_voice_clone_batch(self.ctx, nb, tx, rt, rc, nr, sv, lg, int(non_streaming), out,
+                                                      ns)
+        return r, [_take_audio(out[i], ns[i]) for i in range(nb)]
 
     def generate_batch(self, id_lists, speakers=None, languages=None):
         nb = len(id_lists)

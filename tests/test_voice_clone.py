@@ -102,3 +102,27 @@ def test_voice_clone_vs_oracle(tts_tiny, oracle, name):
 @pytest.mark.gpu
 def test_voice_clone_needs_codes_or_vector(tts_tiny):
     assert tts_tiny.generate_voice_clone(prompt_ids("short")) is None
+
+
+@pytest.mark.gpu
+def test_voice_clone_batch_slots_vs_oracle(tts_tiny, oracle):
+    """Lock-step voice-clone batch (BASELINE C5): slots with different
+    reference lengths, one x-vector-only slot and different prompts; every
+    slot's audio equals the oracle's for its own prompt, reference and cut."""
+    from test_gpu_model import audio_close
+    prompts = [prompt_ids("short"), prompt_ids("p128", 1240), prompt_ids("p128", 1241)]
+    refs = [_inputs(oracle, 9, seed=1, spk=True), _inputs(oracle, 30, seed=2), _inputs(oracle, 1, seed=3, spk=True)]
+    codes = [refs[0][0], refs[1][0], None]
+    spk = [refs[0][1], None, refs[2][1]]
+    rids = [REF_IDS, REF_IDS[:3] + [4000, 4001] + REF_IDS[-2:], None]
+    _, lang = lookup_ids(oracle.cfg, "aiden", "english")
+    for pp in (GREEDY, DEFAULT):
+        tts_tiny.set_params(max_tokens=4096, fixed=6, seed=42, **pp)
+        rc, audio = tts_tiny.generate_voice_clone_batch(prompts, rids, codes, spk, ["english"] * 3)
+        assert rc == 0
+        for b in range(3):
+            pre, tr = oracle.build_icl_prompt(prompts[b], rids[b], codes[b], spk[b], lang, 0)
+            want, _ = oracle.generate_from_prompt(pre, tr, max_tokens=4096, fixed=6, seed=42, **pp)
+            T = 0 if codes[b] is None else codes[b].shape[0]
+            full = oracle.codec_decode(np.concatenate([codes[b], want]) if T else want)
+            audio_close(audio[b], full[int(T / (T + len(want)) * full.shape[0]):])
