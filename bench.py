@@ -217,6 +217,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--model-dir", default=None)
+    ap.add_argument("--voice-clone", action="store_true",
+                    help="BASELINE C5: ICL voice clone (63 synthetic reference frames + reference text + x-vector "
+                         "per utterance; the audio encoders are out of scope), decode of reference ++ generated")
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
@@ -245,7 +248,26 @@ def main():
     m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
     prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
 
+    vc = None
+    if args.voice_clone:
+        # 5 s of reference audio = 63 frames at 12.5 Hz, seeded codes; reference
+        # text = chat template around 20 seeded ids; x-vector of the talker width
+        import numpy as np
+        H = m.cfg.talker_hidden
+        vc = []
+        for i, sd in enumerate(rank_prompt_seeds(rank, args.batch)):
+            r = np.random.default_rng(sd + 7)
+            codes = r.integers(0, 2048, size=(63, m.cfg.num_code_groups)).astype(np.int32)
+            rids = [151644, 77091, 198] + r.integers(1000, 100000, size=20).tolist() + [151645, 198]
+            vc.append((rids, codes, (r.standard_normal(H) * 0.05).astype(np.float32)))
+
     def one_step():
+        if vc is not None:
+            rc, aud = m.generate_voice_clone_batch(prompts, [v[0] for v in vc], [v[1] for v in vc],
+                                                   [v[2] for v in vc], ["english"] * args.batch)
+            if rc != 0:
+                raise RuntimeError("voice-clone generation failed")
+            return sum(len(a) for a in aud)
         if args.batch == 1:
             a = m.generate(prompts[0], "aiden", "english")
             if a is None:
@@ -276,7 +298,7 @@ def main():
     # wall time from the call to the first audio chunk (frame 0 decoded by the
     # exact streaming codec and on the host) ----
     fp = None
-    if args.batch == 1:
+    if args.batch == 1 and vc is None:
         m.generate(prompts[0], "aiden", "english")       # non-streaming breakdown
         prefill_ms, talker_ms, codec_ms = m.c.perf_prefill_ms, m.c.perf_talker_ms, m.c.perf_codec_ms
         # the first streaming request of the process also allocates the
@@ -292,7 +314,7 @@ def main():
                   first_packet_samples=int(len(first[0])) if first else 0, stream_chunk_frames=8,
                   prefill_ms=prefill_ms, talker_ms=talker_ms, codec_ms=codec_ms)
 
-    roof = None if args.no_profile else profile_roofline(m, qtts.lib())
+    roof = None if args.no_profile or vc is not None else profile_roofline(m, qtts.lib())
     m.close()
 
     cpu = None
@@ -314,7 +336,9 @@ def main():
             "dtype": "fp32 activations x bf16 weights (fp32 accumulate)",
             "data": "synthetic (seeded random-init weights of the 1.7B architecture, tools/synth_model.py)",
             "config": {"workload": f"Qwen3-TTS-{args.preset} synthetic, P128 prompt, fixed {args.frames} frames "
-                                   f"({args.frames * 0.08:.2f} s audio), default sampling, batch {args.batch} per GPU",
+                                   f"({args.frames * 0.08:.2f} s audio), default sampling, batch {args.batch} per GPU"
+                                   + (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, "
+                                      "codec over reference ++ generated (reference part cut)" if vc else ""),
                        "global_batch": args.batch * ws, "frames": args.frames,
                        "parallelism": f"dp{ws} (independent replicas, no collective in the data path)"},
         }

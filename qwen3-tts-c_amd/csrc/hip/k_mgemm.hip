@@ -53,7 +53,14 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
     const int r0 = blockIdx.x * 16;
     const int rl = lane & 15, kq = 8 * (lane >> 4);
     const int row = r0 + rl < a.R ? r0 + rl : a.R - 1;
-    const int M = a.nb, C = a.C;
+    // grid.y walks 64-row chunks of the activations: the workgroups of one
+    // weight tile share an XCD's L2 (gridDim.x % 8 == 0 -> same XCD for every y)
+    const int t0 = blockIdx.y * 64;
+    const int M = a.nb - t0 < 64 ? a.nb - t0 : 64, C = a.C;
+    const float *xb = a.x ? a.x + (size_t)t0 * a.ldx : nullptr;
+    const int *idb = a.ids ? a.ids + (size_t)t0 * a.ids_bstride : nullptr;
+    const float *invb = inv ? inv + t0 : nullptr;
+    float *yb = a.y + (size_t)t0 * a.ldy;
     const bf16_t *wr = a.W + (size_t)row * C + kq;
     floatx4 acc[MT];
 #pragma unroll
@@ -76,21 +83,21 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
             float xv[8];
             if (t < M) {
                 if (a.table) {
-                    const int id = a.ids[(size_t)t * a.ids_bstride];
+                    const int id = idb[(size_t)t * a.ids_bstride];
                     const v4u q = *reinterpret_cast<const v4u *>(a.table + (size_t)id * C + k0 + kq);
                     float f[8];
                     unpack8(q, f);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) xv[j] = f[j];
                 } else {
-                    const float *xr = a.x + (size_t)t * a.ldx + k0 + kq;
+                    const float *xr = xb + (size_t)t * a.ldx + k0 + kq;
                     const float4 x0 = *reinterpret_cast<const float4 *>(xr);
                     const float4 x1 = *reinterpret_cast<const float4 *>(xr + 4);
                     xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w;
                     xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
                 }
                 if (a.norm_w) {
-                    const float iv = inv[t];
+                    const float iv = invb[t];
 #pragma unroll
                     for (int j = 0; j < 8; ++j) xv[j] = xv[j] * iv * nw[j];
                 }
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
             float val = v[i];
             const float up = __shfl(val, lane + 4 < 64 ? lane + 4 : lane, 64);
             if (t >= M || r >= a.R) continue;
-            float *yr = a.y + (size_t)t * a.ldy;
+            float *yr = yb + (size_t)t * a.ldy;
             switch (a.epi) {
                 case EPI_STORE: yr[r] = val; break;
                 case EPI_BIAS: yr[r] = val + a.bias[r]; break;
@@ -148,15 +155,16 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
 
 }  // namespace
 
-// Multi-row projection on the matrix cores.  `inv_scratch` (>= nb floats)
-// receives the per-row 1/rms when a.norm_w is set.  Returns 1 when the shape
-// is not covered (caller uses qtts_gemv), 0 ok, -1 error.
+// Multi-row projection on the matrix cores, any number of rows (64-row chunks
+// on grid.y of one launch).  `inv_scratch` (>= nb floats) receives the
+// per-row 1/rms when a.norm_w is set.  Returns 1 when the shape is not
+// covered (caller uses qtts_gemv), 0 ok, -1 error.
 int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st) {
-    if (a.nb < 2 || a.nb > 64 || a.C % 32 || a.R % 16 || a.xcopy || a.table_f32 || (a.norm_w && !inv_scratch) ||
+    if (a.nb < 2 || a.C % 32 || a.R % 16 || a.xcopy || a.table_f32 || (a.norm_w && !inv_scratch) ||
         (a.table && a.norm_w) || (!a.table && (a.ldx % 4 || ((uintptr_t)a.x & 15))) || (a.C % 8))
         return 1;
     if (a.norm_w) hipLaunchKernelGGL(k_row_rms, dim3(a.nb), dim3(256), 0, st, a.x, a.ldx, a.C, a.eps, inv_scratch);
-    const dim3 grid(a.R / 16);
+    const dim3 grid(a.R / 16, (a.nb + 63) / 64);
     if (a.nb <= 16) hipLaunchKernelGGL((k_mgemm<1>), grid, dim3(256), 0, st, a, inv_scratch);
     else if (a.nb <= 32) hipLaunchKernelGGL((k_mgemm<2>), grid, dim3(256), 0, st, a, inv_scratch);
     else hipLaunchKernelGGL((k_mgemm<4>), grid, dim3(256), 0, st, a, inv_scratch);

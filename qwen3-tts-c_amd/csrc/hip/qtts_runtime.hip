@@ -156,6 +156,7 @@ struct qtts_dev {
     unsigned *pf_sink = nullptr;
     int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
+    int pinv_cap = 0;
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
     int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
@@ -546,7 +547,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(ppos, int, R);
     A(psrc, int, R);
     A(plast, int, B);
-    A(pinv, float, 64);
+    dv->pinv_cap = dv->rows_cap > 64 ? dv->rows_cap : 64;
+    A(pinv, float, dv->pinv_cap);
     {
         const int gph = d.NH / d.KV;
         dv->att_nsplit = (dv->S + qtts_attn_keys_per_split(d.HD) - 1) / qtts_attn_keys_per_split(d.HD);
@@ -639,10 +641,17 @@ static int pgemv_att(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kin
     return qtts_gemv_att(a, t, dv->att_pro_wg, dv->st) == 0 ? 0 : -1;
 }
 // Multi-row projection over `rows` activation rows (prefill, text
-// projection): the matrix-core kernel in chunks of 64 rows, else the GEMV in
-// chunks of 16.  Row r of x / y / ids is at r*ldx / r*ldy / r*ids_bstride.
+// projection): > 64 rows in one matrix-core launch (64-row chunks on its
+// grid.y), else the matrix-core kernel / batch GEMV / GEMV in chunks of 64 /
+// 16.  Row r of x / y / ids is at r*ldx / r*ldy / r*ids_bstride.
 static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
     const int xs = a.ldx, ys = a.ldy;
+    if (rows > 64 && dv->use_mfma && (!a.norm_w || rows <= dv->pinv_cap)) {
+        GemvArgs c = a;
+        c.nb = rows;
+        const int rc = qtts_mgemm(c, dv->pinv, dv->st);
+        if (rc <= 0) return rc;
+    }
     for (int r0 = 0; r0 < rows;) {
         GemvArgs c = a;
         int nr = rows - r0 < 64 ? rows - r0 : 64;
