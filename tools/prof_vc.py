@@ -14,14 +14,15 @@ from synth_model import ensure_model, prompt_ids  # noqa: E402
 md = ensure_model("/tmp/qtts_test_models/1.7b", "1.7b")
 m = qtts.QwenTTS(md)
 m.set_params(max_tokens=128, fixed=128, seed=42)
-for nb in (1, 8):
+only = os.environ.get("QTTS_VC_ONLY")   # "8": batch-8 clone only (under rocprofv3)
+for nb in ((8,) if only else (1, 8)):
     prompts = [prompt_ids("p128", seed=1234 + i) for i in range(nb)]
     r = np.random.default_rng(7)
     vc = [([151644, 77091, 198] + r.integers(1000, 100000, size=20).tolist() + [151645, 198],
            r.integers(0, 2048, size=(63, 16)).astype(np.int32), (r.standard_normal(2048) * 0.05).astype(np.float32))
           for _ in range(nb)]
-    for mode in ("plain", "clone"):
-        for it in range(3):
+    for mode in (("clone",) if only else ("plain", "clone")):
+        for it in range(1 if only else 3):
             t = time.perf_counter()
             if mode == "plain":
                 rc, _ = m.generate_batch(prompts, ["aiden"] * nb, ["english"] * nb)
