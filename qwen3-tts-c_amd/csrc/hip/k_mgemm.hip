@@ -46,13 +46,17 @@ __global__ __launch_bounds__(256) void k_row_rms(const float *x, int ldx, int C,
     if (threadIdx.x == 0) inv[blockIdx.x] = rms_inv(s, C, eps);
 }
 
-template <int MT>
+// NW > 1 (many activation rows): the workgroup covers NW weight tiles, so the
+// activation fragments (and their split) are loaded once per NW tiles -- the
+// activation re-reads from L2, R/16 per chunk at NW = 1, bound the > 64-row
+// case.  Per-wave K partition and the in-order wave reduction are those of
+// NW = 1, so the results are bit-identical.
+template <int MT, int NW>
 __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
-    __shared__ floatx4 red[4][MT][64];
+    __shared__ floatx4 red[4][MT][NW][64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r0 = blockIdx.x * 16;
+    const int r0 = blockIdx.x * 16 * NW;
     const int rl = lane & 15, kq = 8 * (lane >> 4);
-    const int row = r0 + rl < a.R ? r0 + rl : a.R - 1;
     // grid.y walks 64-row chunks of the activations: the workgroups of one
     // weight tile share an XCD's L2 (gridDim.x % 8 == 0 -> same XCD for every y)
     const int t0 = blockIdx.y * 64;
@@ -61,15 +65,23 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
     const int *idb = a.ids ? a.ids + (size_t)t0 * a.ids_bstride : nullptr;
     const float *invb = inv ? inv + t0 : nullptr;
     float *yb = a.y + (size_t)t0 * a.ldy;
-    const bf16_t *wr = a.W + (size_t)row * C + kq;
-    floatx4 acc[MT];
+    const bf16_t *wr[NW];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NW; ++n) {
+        const int row = r0 + 16 * n + rl < a.R ? r0 + 16 * n + rl : a.R - 1;
+        wr[n] = a.W + (size_t)row * C + kq;
+    }
+    floatx4 acc[MT][NW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int n = 0; n < NW; ++n) acc[mt][n] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int nsteps = C / 32;
     for (int s = w; s < nsteps; s += 4) {
         const int k0 = 32 * s;
-        const v4u wq = *reinterpret_cast<const v4u *>(wr + k0);
-        const bf16x8 bw = __builtin_bit_cast(bf16x8, wq);
+        bf16x8 bw[NW];
+#pragma unroll
+        for (int n = 0; n < NW; ++n) bw[n] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const v4u *>(wr[n] + k0));
         float nw[8];
         if (a.norm_w) {
             const float4 n0 = *reinterpret_cast<const float4 *>(a.norm_w + k0 + kq);
@@ -116,19 +128,25 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
                 h2[j] = b2;
                 h3[j] = f2bf_rn(e2);
             }
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h1, bw, acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h2, bw, acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h3, bw, acc[mt], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NW; ++n) {
+                acc[mt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h1, bw[n], acc[mt][n], 0, 0, 0);
+                acc[mt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h2, bw[n], acc[mt][n], 0, 0, 0);
+                acc[mt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h3, bw[n], acc[mt][n], 0, 0, 0);
+            }
         }
     }
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) red[w][mt][lane] = acc[mt];
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int n = 0; n < NW; ++n) red[w][mt][n][lane] = acc[mt][n];
     __syncthreads();
-    // wave mt' finishes M tile mt' (sum over waves in order)
-    for (int mt = w; mt < MT; mt += 4) {
-        floatx4 v = red[0][mt][lane];
-        for (int ww = 1; ww < 4; ++ww) v += red[ww][mt][lane];
-        const int r = r0 + rl;   // C/D: col = lane & 15 (weight row), row = (lane >> 4) * 4 + i (token)
+    // wave j % 4 finishes output tile j = (mt, n) (sum over waves in order)
+    for (int j = w; j < MT * NW; j += 4) {
+        const int mt = j / NW, n = j % NW;
+        floatx4 v = red[0][mt][n][lane];
+        for (int ww = 1; ww < 4; ++ww) v += red[ww][mt][n][lane];
+        const int r = r0 + 16 * n + rl;   // C/D: col = lane & 15 (weight row), row = (lane >> 4) * 4 + i (token)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int t = mt * 16 + (lane >> 4) * 4 + i;
@@ -164,10 +182,16 @@ int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st) {
         (a.table && a.norm_w) || (!a.table && (a.ldx % 4 || ((uintptr_t)a.x & 15))) || (a.C % 8))
         return 1;
     if (a.norm_w) hipLaunchKernelGGL(k_row_rms, dim3(a.nb), dim3(256), 0, st, a.x, a.ldx, a.C, a.eps, inv_scratch);
-    const dim3 grid(a.R / 16, (a.nb + 63) / 64);
-    if (a.nb <= 16) hipLaunchKernelGGL((k_mgemm<1>), grid, dim3(256), 0, st, a, inv_scratch);
-    else if (a.nb <= 32) hipLaunchKernelGGL((k_mgemm<2>), grid, dim3(256), 0, st, a, inv_scratch);
-    else hipLaunchKernelGGL((k_mgemm<4>), grid, dim3(256), 0, st, a, inv_scratch);
-    qtts_last_kernel = a.nb <= 16 ? "k_mgemm<1>" : a.nb <= 32 ? "k_mgemm<2>" : "k_mgemm<4>";
+    const int nch = (a.nb + 63) / 64;
+    // > 64 rows: widest weight tile group that still gives >= 256 workgroups
+    const int nw = nch < 2 || a.R % 64 ? 1 : a.R / 64 * nch >= 256 ? 4 : a.R % 32 == 0 && a.R / 32 * nch >= 256 ? 2 : 1;
+    const dim3 grid(a.R / (16 * nw), nch);
+    if (nw == 4) hipLaunchKernelGGL((k_mgemm<4, 4>), grid, dim3(256), 0, st, a, inv_scratch);
+    else if (nw == 2) hipLaunchKernelGGL((k_mgemm<4, 2>), grid, dim3(256), 0, st, a, inv_scratch);
+    else if (a.nb <= 16) hipLaunchKernelGGL((k_mgemm<1, 1>), grid, dim3(256), 0, st, a, inv_scratch);
+    else if (a.nb <= 32) hipLaunchKernelGGL((k_mgemm<2, 1>), grid, dim3(256), 0, st, a, inv_scratch);
+    else hipLaunchKernelGGL((k_mgemm<4, 1>), grid, dim3(256), 0, st, a, inv_scratch);
+    qtts_last_kernel = nw == 4 ? "k_mgemm<4,4>" : nw == 2 ? "k_mgemm<4,2>"
+                     : a.nb <= 16 ? "k_mgemm<1>" : a.nb <= 32 ? "k_mgemm<2>" : "k_mgemm<4>";
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
