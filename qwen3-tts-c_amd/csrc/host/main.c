@@ -40,7 +40,12 @@ static void usage(const char *prog) {
             "  --subtalker-temperature F (0.9)   --subtalker-top-k N (50)   --subtalker-top-p F (1.0)\n"
             "  --benchmark-runs N (1)  --benchmark-warmup N (0)\n"
             "  --device N (HIP device, default 0)   --batch N (lock-step batch of N copies, default 1)\n"
-            "  --stream N (streaming decode, audio chunks every N frames after the first)\n",
+            "  --stream N (streaming decode, audio chunks every N frames after the first)\n"
+            "voice clone (include/qwen_tts.h qwen_tts_generate_voice_clone; audio encoders not included):\n"
+            "  --ref-codes <file>  12 Hz codes of the reference audio, 16 ints per frame (any separators)\n"
+            "  --ref-text <ids>    ids of \"<|im_start|>assistant\\n{ref text}<|im_end|>\\n\" (ICL mode)\n"
+            "  --xvector <file>    speaker-encoder x-vector, talker-hidden floats (any separators)\n"
+            "  --non-streaming     non-streaming text layout\n",
             prog);
 }
 
@@ -66,6 +71,27 @@ static char *read_ids_file(const char *path) {
     return buf;
 }
 
+/* whitespace / comma separated numbers of a text file (voice-clone inputs) */
+static double *read_numbers(const char *path, int *n_out) {
+    char *buf = read_ids_file(path);
+    if (!buf) return NULL;
+    int cap = 1024, n = 0;
+    double *v = (double *)malloc(cap * sizeof(double));
+    for (char *p = buf; *p;) {
+        while (*p && (*p == ',' || *p == ' ' || *p == '\t')) p++;
+        if (!*p) break;
+        char *end = NULL;
+        const double x = strtod(p, &end);
+        if (end == p) { fprintf(stderr, "Error: bad number in %s near '%.16s'\n", path, p); free(v); free(buf); return NULL; }
+        if (n == cap) v = (double *)realloc(v, (cap *= 2) * sizeof(double));
+        v[n++] = x;
+        p = end;
+    }
+    free(buf);
+    *n_out = n;
+    return v;
+}
+
 static void progress(int step, int total, void *u) {
     (void)total;
     (void)u;
@@ -77,7 +103,8 @@ static void progress(int step, int total, void *u) {
 
 int main(int argc, char **argv) {
     const char *dir = NULL, *ids = NULL, *ids_file = NULL, *spk = NULL, *lang = NULL, *out = "output.wav";
-    int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1, stream_chunk = 0;
+    int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1, stream_chunk = 0, non_streaming = 0;
+    const char *ref_codes_file = NULL, *ref_text = NULL, *xvec_file = NULL;
     float temp = -1, st_temp = -1, top_p = -1, st_top_p = -1, rep = -1;
     int top_k = -1, st_top_k = -1, max_tokens = -1, fixed = -1, seed = -1;
     for (int i = 1; i < argc; i++) {
@@ -106,6 +133,10 @@ int main(int argc, char **argv) {
         else if (ARG("--device")) device = (int)strtol(argv[++i], NULL, 10);
         else if (ARG("--batch")) batch = (int)strtol(argv[++i], NULL, 10);
         else if (ARG("--stream")) stream_chunk = (int)strtol(argv[++i], NULL, 10);
+        else if (ARG("--ref-codes")) ref_codes_file = argv[++i];
+        else if (ARG("--ref-text")) ref_text = argv[++i];
+        else if (ARG("--xvector")) xvec_file = argv[++i];
+        else if (!strcmp(a, "--non-streaming")) non_streaming = 1;
         else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); return 0; }
         else {
             fprintf(stderr, "Unknown option: %s\n", a);
@@ -125,6 +156,39 @@ int main(int argc, char **argv) {
         if (!(file_ids = read_ids_file(ids_file))) return 1;
         ids = file_ids;
     }
+    /* voice clone inputs */
+    int *ref_codes = NULL, n_ref = 0;
+    float *xvec = NULL;
+    int n_xvec = 0;
+    const int clone = ref_codes_file || xvec_file;
+    if (clone && (batch != 1 || stream_chunk > 0)) {
+        fprintf(stderr, "Error: voice clone runs at --batch 1 without --stream\n");
+        free(file_ids);
+        return 1;
+    }
+    if (ref_codes_file) {
+        int n = 0;
+        double *v = read_numbers(ref_codes_file, &n);
+        if (!v || n < 16 || n % 16) {
+            fprintf(stderr, "Error: --ref-codes needs 16 ints per frame (%d numbers read)\n", n);
+            free(v); free(file_ids);
+            return 1;
+        }
+        n_ref = n / 16;
+        ref_codes = (int *)malloc((size_t)n * sizeof(int));
+        for (int i = 0; i < n; i++) ref_codes[i] = (int)v[i];
+        free(v);
+    }
+    if (xvec_file) {
+        int n = 0;
+        double *v = read_numbers(xvec_file, &n);
+        if (!v || n < 1) { free(v); free(ref_codes); free(file_ids); return 1; }
+        n_xvec = n;
+        xvec = (float *)malloc((size_t)n * sizeof(float));
+        for (int i = 0; i < n; i++) xvec[i] = (float)v[i];
+        free(v);
+        if (verbose >= 1) fprintf(stderr, "x-vector: %d floats\n", n);
+    }
     qwen_tts_verbose = verbose;
     if (device >= 0) qwen_tts_set_device(device);
     if (verbose >= 1) fprintf(stderr, "Loading model from %s...\n", dir);
@@ -132,6 +196,12 @@ int main(int argc, char **argv) {
     if (!ctx) {
         fprintf(stderr, "Error: failed to load model\n");
         free(file_ids);
+        return 1;
+    }
+    if (xvec && n_xvec != ctx->config.talker_hidden) {
+        fprintf(stderr, "Error: --xvector has %d floats, the talker hidden size is %d\n", n_xvec,
+                ctx->config.talker_hidden);
+        qwen_tts_free(ctx); free(ref_codes); free(xvec); free(file_ids);
         return 1;
     }
     if (temp >= 0) ctx->temperature = temp;
@@ -160,7 +230,10 @@ int main(int argc, char **argv) {
         float *ra = NULL;
         int rn = 0;
         long total_samples = 0;
-        if (batch == 1 && stream_chunk > 0) {
+        if (clone) {
+            ra = qwen_tts_generate_voice_clone(ctx, ids, ref_text, ref_codes, n_ref, xvec, lang, non_streaming, &rn);
+            total_samples = rn;
+        } else if (batch == 1 && stream_chunk > 0) {
             ra = qwen_tts_generate_stream(ctx, ids, spk, lang, stream_chunk, NULL, NULL, &rn);
             total_samples = rn;
         } else if (batch == 1) {
@@ -223,5 +296,7 @@ int main(int argc, char **argv) {
     free(audio);
     qwen_tts_free(ctx);
     free(file_ids);
+    free(ref_codes);
+    free(xvec);
     return rc;
 }

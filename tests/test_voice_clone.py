@@ -126,3 +126,32 @@ def test_voice_clone_batch_slots_vs_oracle(tts_tiny, oracle):
             T = 0 if codes[b] is None else codes[b].shape[0]
             full = oracle.codec_decode(np.concatenate([codes[b], want]) if T else want)
             audio_close(audio[b], full[int(T / (T + len(want)) * full.shape[0]):])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns", [0, 1])
+def test_cli_voice_clone_flags(tiny_dir, tts_tiny, oracle, ns):
+    """qwen-tts --ref-codes / --ref-text / --xvector [--non-streaming] writes
+    the same wav as the API call on the same inputs (text files in, as a
+    caller of the audio encoders would write them)."""
+    import os
+    import subprocess
+    import tempfile
+
+    import qtts
+    codes, sv = _inputs(oracle, 10, seed=5, spk=True)
+    ids = prompt_ids("short")
+    with tempfile.TemporaryDirectory() as d:
+        cf, xf = os.path.join(d, "ref_codes.txt"), os.path.join(d, "xvec.txt")
+        np.savetxt(cf, codes, fmt="%d")
+        np.savetxt(xf, sv[None], fmt="%.9g")
+        cmd = [qtts.CLI_PATH, "-d", tiny_dir, "-t", ",".join(map(str, ids)), "-l", "english", "-o",
+               os.path.join(d, "cli.wav"), "--fixed-codec-tokens", "5", "--seed", "42", "--ref-codes", cf,
+               "--ref-text", ",".join(map(str, REF_IDS)), "--xvector", xf] + (["--non-streaming"] if ns else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        tts_tiny.set_params(max_tokens=4096, fixed=5, seed=42)
+        a = tts_tiny.generate_voice_clone(ids, REF_IDS, codes, sv, "english", ns)
+        api = os.path.join(d, "api.wav")
+        assert qtts.lib().qwen_tts_write_wav(api.encode(), a.ctypes.data_as(qtts._fp), len(a), 24000) == 0
+        assert open(os.path.join(d, "cli.wav"), "rb").read() == open(api, "rb").read()
