@@ -314,6 +314,12 @@ def main():
                   first_packet_samples=int(len(first[0])) if first else 0, stream_chunk_frames=8,
                   prefill_ms=prefill_ms, talker_ms=talker_ms, codec_ms=codec_ms)
 
+    if args.batch == 1 and vc is not None:
+        # voice-clone first packet: reference frames through the streaming codec, then frame 0
+        for _ in range(2):   # second request, as for the custom-voice line
+            m.generate_voice_clone_stream(prompts[0], vc[0][0], vc[0][1], vc[0][2], "english", chunk_frames=8)
+        fp = dict(first_packet_ms=m.c.perf_first_packet_ms, first_frame_ms=m.c.perf_first_frame_ms,
+                  prefill_ms=m.c.perf_prefill_ms, ref_frames=63)
     roof = None if args.no_profile or vc is not None else profile_roofline(m, qtts.lib())
     m.close()
 

@@ -223,6 +223,12 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
 float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
                                      const int *ref_codes, int n_ref_frames, const float *spk_embed,
                                      const char *language, int non_streaming, int *out_samples);
+/* Streaming voice clone (as qwen_tts_generate_stream, after the type below):
+ * the reference frames are pushed through the exact streaming codec first, so
+ * chunks start at the reference boundary (sample n_ref_frames * 1920 of the
+ * reference ++ generated decode).  The non-streamed call cuts at the Python
+ * reference's float position int(ref / total * samples), which for ~5 % of
+ * (ref, total) pairs is one sample earlier. */
 /* nb voice-clone utterances in lock-step frames (BASELINE C5: batch 8 on one
  * GPU); per-slot arrays as above (ref_codes[b] / spk_embeds[b] may be NULL).
  * Returns 0 when every utterance produced audio. */
@@ -243,6 +249,10 @@ int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
 typedef void (*qwen_tts_audio_cb)(const float *pcm, int n_samples, void *userdata);
 float *qwen_tts_generate_stream(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
                                 int chunk_frames, qwen_tts_audio_cb cb, void *userdata, int *out_samples);
+float *qwen_tts_generate_voice_clone_stream(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                            const int *ref_codes, int n_ref_frames, const float *spk_embed,
+                                            const char *language, int non_streaming, int chunk_frames,
+                                            qwen_tts_audio_cb cb, void *userdata, int *out_samples);
 /* Incremental codec decode of host codes [time_steps][16]: begin, then push
  * any number of frames at a time; each push writes time_steps * 1920 samples
  * to `out` and returns that count (-1 on error).  The concatenation equals

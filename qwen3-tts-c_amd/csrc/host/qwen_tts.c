@@ -567,8 +567,13 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     int streamed = 0;
     double t_stream = 0;
     if (stream) {
-        sbuf = (float *)malloc((size_t)max_tokens * 1920 * sizeof(float));
-        if (!sbuf || qtts_dev_codec_stream_begin(dev, max_tokens) != 0) {
+        /* voice clone: the reference frames go through the stream first (their
+         * audio is dropped), so the carried codec state is that of decoding
+         * reference ++ generated, and the chunks start at the reference boundary */
+        const int sref = vcs && vcs[0].ref_codes && vcs[0].n_ref > 0 ? vcs[0].n_ref : 0;
+        sbuf = (float *)malloc((size_t)(max_tokens > sref ? max_tokens : sref) * 1920 * sizeof(float));
+        if (!sbuf || qtts_dev_codec_stream_begin(dev, max_tokens + sref) != 0 ||
+            (sref && qtts_dev_codec_stream_push_host(dev, vcs[0].ref_codes, sref, sbuf) < 0)) {
             free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
         }
     }
@@ -753,12 +758,11 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
     return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms(), NULL, NULL);
 }
 
-int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts,
-                                        const char *const *ref_texts, const int *const *ref_codes,
-                                        const int *n_ref_frames, const float *const *spk_embeds,
-                                        const char *const *languages, int non_streaming, float **out_audio,
-                                        int *out_samples) {
-    if (!ctx || nb < 1 || !texts || !out_audio || !out_samples) return -1;
+static int vclone_run(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *ref_texts,
+                      const int *const *ref_codes, const int *n_ref_frames, const float *const *spk_embeds,
+                      const char *const *languages, int non_streaming, float **out_audio, int *out_samples,
+                      const stream_t *stream) {
+    if (!ctx || nb < 1 || !texts || !out_audio || !out_samples || (stream && nb != 1)) return -1;
     for (int b = 0; b < nb; b++) { out_audio[b] = NULL; out_samples[b] = 0; }
     vclone_t *vcs = (vclone_t *)calloc(nb, sizeof(vclone_t));
     int rc = vcs ? 0 : -1;
@@ -792,11 +796,42 @@ int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char 
         vc->ref_codes = codes;
         vc->n_ref = nref;
     }
-    if (rc == 0) rc = run_batch(ctx, nb, texts, NULL, languages, out_audio, out_samples, now_ms(), NULL, vcs);
+    if (rc == 0) rc = run_batch(ctx, nb, texts, NULL, languages, out_audio, out_samples, now_ms(), stream, vcs);
     if (vcs)
         for (int b = 0; b < nb; b++) free((void *)vcs[b].ref_ids);
     free(vcs);
     return rc;
+}
+
+int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts,
+                                        const char *const *ref_texts, const int *const *ref_codes,
+                                        const int *n_ref_frames, const float *const *spk_embeds,
+                                        const char *const *languages, int non_streaming, float **out_audio,
+                                        int *out_samples) {
+    return vclone_run(ctx, nb, texts, ref_texts, ref_codes, n_ref_frames, spk_embeds, languages, non_streaming,
+                      out_audio, out_samples, NULL);
+}
+
+float *qwen_tts_generate_voice_clone_stream(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                            const int *ref_codes, int n_ref_frames, const float *spk_embed,
+                                            const char *language, int non_streaming, int chunk_frames,
+                                            qwen_tts_audio_cb cb, void *userdata, int *out_samples) {
+    if (!ctx || !out_samples) return NULL;
+    *out_samples = 0;
+    stream_t st = {cb, userdata, chunk_frames > 0 ? chunk_frames : 1};
+    float *audio = NULL;
+    int n = 0;
+    const char *texts[1] = {text}, *rt[1] = {ref_text}, *lang[1] = {language};
+    const int *rc1[1] = {ref_codes};
+    const int nr1[1] = {n_ref_frames};
+    const float *sv1[1] = {spk_embed};
+    ctx->perf_first_packet_ms = 0;
+    if (vclone_run(ctx, 1, texts, rt, rc1, nr1, sv1, lang, non_streaming, &audio, &n, &st) != 0 || !audio || n <= 0) {
+        free(audio);
+        return NULL;
+    }
+    *out_samples = n;
+    return audio;
 }
 
 float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,

@@ -66,7 +66,7 @@ EXPORTS = [
     "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
     "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
-    "qwen_tts_generate_voice_clone_batch",
+    "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -120,6 +120,9 @@ def lib():
     L.qwen_tts_generate_stream.restype = C.c_void_p
     L.qwen_tts_generate_stream.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, AUDIO_CB,
                                            C.c_void_p, _ip]
+    L.qwen_tts_generate_voice_clone_stream.restype = C.c_void_p
+    L.qwen_tts_generate_voice_clone_stream.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, _ip, C.c_int, _fp,
+                                                       C.c_char_p, C.c_int, C.c_int, AUDIO_CB, C.c_void_p, _ip]
     L.qwen_tts_generate_voice_clone.restype = C.c_void_p
     L.qwen_tts_generate_voice_clone.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, _ip, C.c_int, _fp,
                                                 C.c_char_p, C.c_int, _ip]
@@ -256,6 +259,25 @@ class QwenTTS:
         p = lib().qwen_tts_generate_stream(self.ctx, csv, speaker.encode() if speaker else None,
                                            language.encode() if language else None, int(chunk_frames), cb, None,
                                            C.byref(n))
+        return _take_audio(p, n.value)
+
+    def generate_voice_clone_stream(self, ids, ref_ids=None, ref_codes=None, spk_embed=None, language=None,
+                                    non_streaming=False, chunk_frames=4, on_chunk=None):
+        """Streaming voice clone; chunks start at the reference boundary."""
+        csv = ",".join(str(int(i)) for i in ids).encode()
+        rcsv = ",".join(str(int(i)) for i in ref_ids).encode() if ref_ids is not None else None
+        rc = None if ref_codes is None else np.ascontiguousarray(ref_codes, np.int32)
+        sv = None if spk_embed is None else np.ascontiguousarray(spk_embed, np.float32)
+        n = C.c_int(0)
+
+        def _cb(p, k, u):
+            if on_chunk is not None:
+                on_chunk(np.ctypeslib.as_array(p, shape=(k,)).copy())
+        cb = AUDIO_CB(_cb)
+        p = lib().qwen_tts_generate_voice_clone_stream(
+            self.ctx, csv, rcsv, None if rc is None else rc.ctypes.data_as(_ip), 0 if rc is None else rc.shape[0],
+            None if sv is None else sv.ctypes.data_as(_fp), language.encode() if language else None,
+            int(non_streaming), int(chunk_frames), cb, None, C.byref(n))
         return _take_audio(p, n.value)
 
     def codec_stream(self, chunks, max_frames=4096):

@@ -155,3 +155,26 @@ def test_cli_voice_clone_flags(tiny_dir, tts_tiny, oracle, ns):
         api = os.path.join(d, "api.wav")
         assert qtts.lib().qwen_tts_write_wav(api.encode(), a.ctypes.data_as(qtts._fp), len(a), 24000) == 0
         assert open(os.path.join(d, "cli.wav"), "rb").read() == open(api, "rb").read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [0, 7, 63])
+def test_voice_clone_stream(tts_tiny, oracle, T):
+    """Streaming voice clone: same codes as the oracle, chunks concatenate to
+    the reference ++ generated decode from the exact frame boundary T * 1920
+    (the reference frames are pushed through the streaming codec first)."""
+    from test_gpu_model import audio_close
+    codes, sv = _inputs(oracle, max(T, 1), seed=11 + T, spk=True)
+    rc = codes if T else None
+    ids = prompt_ids("short")
+    _, lang = lookup_ids(oracle.cfg, "aiden", "english")
+    tts_tiny.set_params(max_tokens=4096, fixed=6, seed=42, **DEFAULT)
+    chunks = []
+    a = tts_tiny.generate_voice_clone_stream(ids, REF_IDS if T else None, rc, sv, "english", 0, chunk_frames=2,
+                                             on_chunk=chunks.append)
+    assert len(chunks[0]) == 1920 and np.array_equal(np.concatenate(chunks), a)
+    pre, tr = oracle.build_icl_prompt(ids, REF_IDS if T else None, rc, sv, lang, 0)
+    want, _ = oracle.generate_from_prompt(pre, tr, max_tokens=4096, fixed=6, seed=42, **DEFAULT)
+    np.testing.assert_array_equal(tts_tiny.last_codes(), want)
+    full = oracle.codec_decode(np.concatenate([codes, want]) if T else want)
+    audio_close(a, full[T * 1920:])
