@@ -157,9 +157,21 @@ def test_cli_voice_clone_flags(tiny_dir, tts_tiny, oracle, ns):
         assert open(os.path.join(d, "cli.wav"), "rb").read() == open(api, "rb").read()
 
 
+@pytest.fixture(scope="module")
+def tts_stream(gpu, tiny_dir):
+    # own ctx, as test_gpu_model's streaming tests: a streaming generate on a
+    # ctx whose codec stream was driven directly (qwen_tts_codec_stream_*,
+    # test_codec_stream_equals_full_decode) delivers no chunks -- open issue,
+    # DESIGN.md §7
+    import qtts
+    m = qtts.QwenTTS(tiny_dir)
+    yield m
+    m.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("T", [0, 7, 63])
-def test_voice_clone_stream(tts_tiny, oracle, T):
+def test_voice_clone_stream(tts_stream, oracle, T):
     """Streaming voice clone: same codes as the oracle, chunks concatenate to
     the reference ++ generated decode from the exact frame boundary T * 1920
     (the reference frames are pushed through the streaming codec first)."""
@@ -168,10 +180,12 @@ def test_voice_clone_stream(tts_tiny, oracle, T):
     rc = codes if T else None
     ids = prompt_ids("short")
     _, lang = lookup_ids(oracle.cfg, "aiden", "english")
+    tts_tiny = tts_stream
     tts_tiny.set_params(max_tokens=4096, fixed=6, seed=42, **DEFAULT)
     chunks = []
     a = tts_tiny.generate_voice_clone_stream(ids, REF_IDS if T else None, rc, sv, "english", 0, chunk_frames=2,
                                              on_chunk=chunks.append)
+    assert a is not None and chunks, "no audio / no chunks"
     assert len(chunks[0]) == 1920 and np.array_equal(np.concatenate(chunks), a)
     pre, tr = oracle.build_icl_prompt(ids, REF_IDS if T else None, rc, sv, lang, 0)
     want, _ = oracle.generate_from_prompt(pre, tr, max_tokens=4096, fixed=6, seed=42, **DEFAULT)
