@@ -171,7 +171,8 @@ def profile_roofline(m, lib):
     cnt, tot_ms, tot_b = gemv[dom]
     avg_ms, avg_bytes = tot_ms / cnt, tot_b / cnt
     rp_us, traffic, src = _rocprof_lookup(dom)
-    return dict(kernel=dom, launches_per_frame=cnt, avg_bytes=avg_bytes, avg_ms=avg_ms,
+    kind_of = {nm[i]: int(k[i]) for i in range(n)}
+    return dict(kernel=dom, kind=kind_of[dom], launches_per_frame=cnt, avg_bytes=avg_bytes, avg_ms=avg_ms,
                 achieved_GBs=avg_bytes / (avg_ms * 1e-3) / 1e9, rocprof_avg_us=rp_us, traffic=traffic,
                 profile_src=src, frame_kernel_ms=float(t.sum()), share_ms=share, n_kernels=n,
                 kernels={x: {"launches": e[0], "ms": round(e[1], 4), "GBs": round(e[2] / (e[1] * 1e-3) / 1e9, 1)
@@ -180,28 +181,100 @@ def profile_roofline(m, lib):
                 gemv_ms_per_frame=float(t[(k == 0) | (k == 1)].sum()))
 
 
-def cpu_baseline(md, frames, ids, threads):
+def physical_cores():
+    """Physical cores of this host from lscpu (sockets x cores per socket)."""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = dict(l.split(":", 1) for l in out.splitlines() if ":" in l)
+        return int(kv["Socket(s)"].strip()) * int(kv["Core(s) per socket"].strip())
+    except Exception:
+        return None
+
+
+def cpu_threads_default():
+    """Threads for the reference CPU baseline: the physical cores this process
+    may use (affinity and OMP_NUM_THREADS bound it: the GPU box gives one GPU's
+    job a 16-CPU share and exports OMP_NUM_THREADS=16)."""
+    n = len(os.sched_getaffinity(0))
+    pc = physical_cores()
+    if pc:
+        n = min(n, pc)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128, speaker="aiden", timeout=900):
+    """The reference c/ CLI (oracle/_ref/qwen-tts, built unmodified by
+    oracle/Makefile) timed as BASELINE.md §2 plans: --benchmark-warmup /
+    --benchmark-runs with the [persistent] lines parsed (c/main.c:262-271).
+    The bounded sample decodes `frames` frames per run; the 128-frame
+    workload is extrapolated from it: fixed part (prompt + prefill) + talker
+    ms/frame x 128 + codec ms/frame x 128 (the reference's decode loop and
+    codec are linear in frames)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "qwen-tts")
     if not os.path.exists(exe):
         return None
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    cmd = [exe, "-d", md, "-t", ",".join(map(str, ids)), "-s", "aiden", "-l", "english", "-o", "/tmp/qtts_cpu.wav",
-           "--fixed-codec-tokens", str(frames), "-v"]
+    cmd = [exe, "-d", md, "-t", ",".join(map(str, ids)), "-s", speaker, "-l", "english", "-o", "/tmp/qtts_cpu.wav",
+           "--fixed-codec-tokens", str(frames), "--benchmark-warmup", str(warmup), "--benchmark-runs", str(runs), "-v"]
     t = time.time()
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     wall = time.time() - t
-    m = re.search(r"Total: ([0-9.]+) ms \(([0-9.]+) s audio", r.stderr)
-    g = re.search(r"Generated (\d+) codec tokens in ([0-9.]+) ms \(([0-9.]+) ms/token\)", r.stderr)
-    if r.returncode != 0 or not m:
+    pr = re.findall(r"\[persistent\] run (\d+)/(\d+): elapsed=([0-9.]+) ms, audio=([0-9.]+)s, talker=([0-9.]+) ms, "
+                    r"codec=([0-9.]+) ms, total=([0-9.]+) ms, tokens=(\d+)", r.stderr)
+    if r.returncode != 0 or len(pr) != runs:
         log("[bench] cpu baseline failed:", r.stderr[-400:])
         return None
-    total_s = float(m.group(1)) / 1e3
-    audio_s = float(m.group(2))
-    return dict(value=audio_s / total_s, unit="audio-s/s", cores=threads, kind="reference",
-                sample=(f"reference c/ (oracle/_ref/qwen-tts, scalar GEMV + OpenMP {threads} threads, no BLAS in image) "
-                        f"on the same 1.7B synthetic model, same prompt, {frames} frames ({audio_s:.2f} s audio): "
-                        f"generate {total_s:.1f} s (talker {float(g.group(3)) if g else -1:.0f} ms/frame), "
-                        f"process wall incl. load {wall:.1f} s"))
+    runs_ = [dict(elapsed_ms=float(p[2]), audio_s=float(p[3]), talker_ms=float(p[4]), codec_ms=float(p[5]),
+                  total_ms=float(p[6]), tokens=int(p[7])) for p in pr]
+    med = sorted(runs_, key=lambda x: x["total_ms"])[len(runs_) // 2]
+    n = med["tokens"]
+    fixed_ms = med["total_ms"] - med["talker_ms"] - med["codec_ms"]
+    ext_ms = fixed_ms + (med["talker_ms"] + med["codec_ms"]) / n * target_frames
+    audio_s = target_frames * 0.08
+    return dict(value=audio_s / (ext_ms / 1e3), unit="audio-s/s", cores=threads, kind="reference",
+                physical_cores=physical_cores(),
+                runs=runs_,
+                sample=(f"reference c/ (oracle/_ref/qwen-tts: unmodified c/ sources, scalar GEMV + OpenMP, no BLAS in "
+                        f"the image) on the same synthetic model and prompt, {threads} OpenMP threads, "
+                        f"--fixed-codec-tokens {frames} --benchmark-warmup {warmup} --benchmark-runs {runs} "
+                        f"([persistent] lines); the {target_frames}-frame workload is extrapolated from the median run: "
+                        f"fixed {fixed_ms:.0f} ms (prompt + prefill) + talker {med['talker_ms'] / n:.0f} ms/frame + codec "
+                        f"{med['codec_ms'] / n:.0f} ms/frame -> {ext_ms / 1e3:.1f} s for {audio_s:.2f} s of audio; "
+                        f"process wall incl. load {wall:.0f} s"))
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per
+    GPU) through torch.distributed.run as a CHILD process and return its exit
+    code.  Runs before anything in this process touches the GPU."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
+
+
+def gather_ranks(ws, rec):
+    """Per-rank records {rank, device, utterances, samples, frames, wall_ms} to
+    every rank (the only exchange is this gather)."""
+    if ws == 1:
+        return [rec]
+    import torch.distributed as dist
+    out = [None] * ws
+    dist.all_gather_object(out, rec)
+    return out
+
+
+# SURVEY.md §8(d): algorithmic bytes per frame at batch 1 = unique weights +
+# talker KV at 2 B/element (bf16) per position
+FRAME_WEIGHT_BYTES = {"1.7b": 3.056e9, "0.6b": 1.107e9}
+KV_BYTES_PER_POS = 114688
 
 
 def main():
@@ -212,17 +285,28 @@ def main():
     ap.add_argument("--preset", default="1.7b")
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU per step (lock-step batch)")
-    ap.add_argument("--cpu-frames", type=int, default=2)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-frames", type=int, default=8, help="frames per run of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the physical cores this process may use")
+    ap.add_argument("--cpu-1thread", action="store_true", help="also time the reference with 1 thread (slow)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--model-dir", default=None)
     ap.add_argument("--voice-clone", action="store_true",
                     help="BASELINE C5: ICL voice clone (63 synthetic reference frames + reference text + x-vector "
                          "per utterance; the audio encoders are out of scope), decode of reference ++ generated")
+    ap.add_argument("--c1", action="store_true",
+                    help="BASELINE C1 only: the reference c/ CLI on the 0.6B synthetic model, short prompt "
+                         "(test/tokens_great_power.txt), on the host cores; no GPU")
     args = ap.parse_args()
 
+    if args.c1:
+        return c1_line(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+
     ws, rank, local = dist_setup()
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     import torch
     # one process per GPU; QTTS_BENCH_BACKEND=gloo rehearses N ranks on fewer
     # GPUs (ranks share devices round-robin), RCCL ("nccl") otherwise
@@ -293,6 +377,8 @@ def main():
     audio_total = reduce_sum(ws, samples / 24000.0)
     value = audio_total / el_max
     ms_per_step = el_max / args.steps * 1e3
+    ranks = gather_ranks(ws, dict(rank=rank, device=dev, utterances=args.batch * args.steps, samples=samples,
+                                  frames=args.batch * args.steps * args.frames, wall_ms=round(el * 1e3, 2)))
 
     # ---- first packet (BASELINE.json metric, configs[2]): streaming generation,
     # wall time from the call to the first audio chunk (frame 0 decoded by the
@@ -325,7 +411,12 @@ def main():
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(md, args.cpu_frames, prompts[0], args.cpu_threads)
+        thr = args.cpu_threads or cpu_threads_default()
+        cpu = cpu_baseline(md, prompts[0], thr, frames=args.cpu_frames, target_frames=args.frames)
+        if cpu and args.cpu_1thread:
+            one = cpu_baseline(md, prompts[0], 1, frames=2, warmup=0, runs=2, target_frames=args.frames, timeout=3000)
+            if one:
+                cpu["one_thread"] = {k: one[k] for k in ("value", "unit", "cores", "sample")}
 
     if rank == 0:
         out = {
@@ -351,8 +442,29 @@ def main():
         if fp:
             out["first_packet_ms"] = round(fp["first_packet_ms"], 2)
             out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in fp.items()}
+        out["ranks"] = ranks
+        fw = FRAME_WEIGHT_BYTES.get(args.preset)
+        if fw and vc is None:
+            # §8(d) headline: utterance-frames per second x algorithmic bytes per
+            # frame (weights once per lock-step step + B x KV) over 8 TB/s; the
+            # mean talker position is prefill (10 rows: 3 role + 7 codec-prefix
+            # rows, speaker and language set) + the frames before it
+            pos = 10 + (args.frames - 1) / 2.0
+            fps = value / 0.08                                  # 12.5 frames per audio second
+            steps_ps = fps / args.batch
+            ach = (steps_ps * fw + fps * KV_BYTES_PER_POS * pos) / 1e9
+            ach32 = (steps_ps * fw + fps * 2 * KV_BYTES_PER_POS * pos) / 1e9
+            out["roofline_frame"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(ach / HBM_PEAK_GBS, 4), "frames_per_s": round(fps, 1),
+                                     "bytes_per_frame": int(fw + KV_BYTES_PER_POS * pos * args.batch) // args.batch,
+                                     "mean_kv_pos": pos,
+                                     "achieved_fp32_kv": round(ach32, 1),
+                                     "note": "SURVEY.md 8(d): frames/s x (W + 114688 B x pos) / 8 TB/s, KV at 2 B/elem; "
+                                             "this build keeps the reference's fp32 KV (achieved_fp32_kv counts it); "
+                                             "whole utterance wall (prefill + codec included)"}
         if roof:
-            out["roofline"] = {"bound": "hbm", "achieved": round(roof["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
+            bound = "mall/latency" if roof["kind"] == 1 else "hbm"
+            out["roofline"] = {"bound": bound, "achieved": round(roof["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(roof["achieved_GBs"] / HBM_PEAK_GBS, 4),
                                "traffic": None if roof["traffic"] is None else int(roof["traffic"]),
                                "kernel": roof["kernel"],
@@ -373,6 +485,27 @@ def main():
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def c1_line(args):
+    """BASELINE C1: 0.6B, single short prompt, the reference c/ BLAS+OpenMP
+    path (here: scalar + OpenMP, no BLAS in the image), host cores only."""
+    from synth_model import ensure_model, prompt_ids
+    md = args.model_dir or os.path.join(os.environ.get("QTTS_TEST_MODELS", "/tmp/qtts_test_models"), "0.6b")
+    ensure_model(md, "0.6b", seed=0)
+    thr = args.cpu_threads or cpu_threads_default()
+    rows = {}
+    for t in ([thr, 1] if args.cpu_1thread else [thr]):
+        r = cpu_baseline(md, prompt_ids("short"), t, frames=args.cpu_frames, warmup=1 if t > 1 else 0, runs=2,
+                         target_frames=args.cpu_frames, timeout=3000)
+        rows[str(t)] = r
+    out = {"metric": "audio-sec/wall-sec (RTF^-1), reference c/ CPU path (BASELINE C1)", "unit": "audio-s/s",
+           "value": rows[str(thr)]["value"] if rows.get(str(thr)) else None, "higher_is_better": True,
+           "config": {"workload": f"Qwen3-TTS-0.6b synthetic, short prompt (test/tokens_great_power.txt), "
+                                  f"fixed {args.cpu_frames} frames, default sampling"},
+           "data": "synthetic (seeded random-init weights of the 0.6B architecture, tools/synth_model.py)",
+           "rows": rows}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -234,32 +234,6 @@ __global__ __launch_bounds__(256) void k_qk_prep_w(AttnArgs a) {
 // (agent-scope acq_rel ticket) merges them in split order and resets the
 // ticket.  Grid size is fixed at graph capture (nsplit from the cache
 // capacity); splits past the live length exit at once.
-// Prefetch workgroup of k_attn_dec: workgroup i of np reads its share of the
-// two byte ranges in 4 KB rows (16 B per lane, 8 loads in flight) and folds
-// them into one word that is stored only on an impossible match.
-__device__ __forceinline__ void attn_prefetch(const AttnArgs &a) {
-    const int np = gridDim.x * gridDim.y * a.pf_z;
-    const int i = ((blockIdx.z - a.nrows) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    const size_t tot = a.pf0_bytes + a.pf1_bytes;
-    const size_t per = ((tot + np - 1) / np + 4095) / 4096 * 4096;
-    size_t b0 = (size_t)i * per, b1 = b0 + per < tot ? b0 + per : tot;
-    uint32_t x = 0;
-    for (size_t off = b0 + (size_t)threadIdx.x * 16; off < b1; off += 8 * 4096) {
-        v4u v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const size_t o = off + (size_t)u * 4096;
-            const size_t oc = o < b1 ? o : b0 + threadIdx.x * 16;
-            const unsigned char *src = oc < a.pf0_bytes ? (const unsigned char *)a.pf0 + oc
-                                                        : (const unsigned char *)a.pf1 + (oc - a.pf0_bytes);
-            v[u] = *reinterpret_cast<const v4u *>(src);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    }
-    if (x == 0x9E3779B9u && a.pf_sink) *a.pf_sink = x;
-}
-
 template <int HD, int GPH>
 __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     constexpr int LPK = HD >= 32 ? HD / 32 : 1;   // lanes per key
@@ -277,10 +251,6 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     __shared__ int last;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if ((int)blockIdx.z >= a.nrows) {   // weight prefetch workgroup (AttnArgs::pf*)
-        attn_prefetch(a);
-        return;
-    }
     const int kvh = blockIdx.x, split = blockIdx.y, r = blockIdx.z;
     const int KVD = a.KV * HD;
     const int p = a.pos ? a.pos[r] : a.pos_const;
@@ -532,185 +502,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     if (sub == 0 && row < R) part[((size_t)kvh * gridDim.z + b) * R + row] = acc;
 }
 
-// Talker decode attention + O projection by kv head (batch 1, GQA 2), for
-// sessions whose key capacity is small enough that recomputing a head pair's
-// attention in every row-block workgroup is cheaper than a separate split
-// attention launch (the runtime gates on S).  Workgroup (rb, kvh):
-//   1. issues its W_o fragment loads (RPS rows per slot x 2*HD columns),
-//   2. q0 | q1 | k | v of the token: per-head RMSNorm (T.c:158-170) + RoPE,
-//      rb == 0 stores k / v into the cache (T.c:171-189),
-//   3. online softmax over 64-key chunks (scores q.k / sqrt(HD), T.c:190-224;
-//      the exact max / sum order of kernel_softmax is replaced by the
-//      flash-style rescaling, the same reassociation as the split kernel's
-//      merge), P.V one (head, dim) output per thread,
-//   4. part[kvh][row] = W_o[row, 2 HD kvh ..) . attn (the next GEMV adds the
-//      KV partials to the residual, GemvArgs::xadd).
-template <int HD, int RPS>
-__global__ __launch_bounds__(256) void k_attn_o_dec(AttnArgs t, const bf16_t *Wo, int R, float *part) {
-    constexpr int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, NJ = W2 / (8 * LPS), SLOTS = 256 / LPS;
-    constexpr int D4 = HD / 4, CH = 64, LPK = 256 / CH, DPL = HD / LPK;
-    __shared__ __attribute__((aligned(16))) float lq[4 * HD];   // rotated q0 | q1 | k, raw v
-    __shared__ __attribute__((aligned(16))) float att[W2];
-    __shared__ float sc[2][CH];
-    __shared__ float alpha[2], lsum[2];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, kvh = blockIdx.y, rb = blockIdx.x;
-    const int KVD = t.KV * HD, AD = t.NH * HD;
-    const int p = t.pos ? t.pos[0] : t.pos_const, n = p + 1;
-    // 1. the weight fragment first
-    const int slot = tid / LPS, sub = tid - slot * LPS;
-    v4u wv[RPS][NJ];
-#pragma unroll
-    for (int i = 0; i < RPS; ++i) {
-        const int row = (rb * RPS + i) * SLOTS + slot, rowc = row < R ? row : R - 1;
-        const bf16_t *wr = Wo + (size_t)rowc * AD + W2 * kvh + 8 * sub;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) wv[i][j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
-    }
-    // 2. the token's q0 | q1 | k | v -> norm + RoPE -> LDS; cache store by rb == 0
-    {
-        const int seg = tid / D4, l = tid - seg * D4;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float *row = t.qkv;
-        if (seg < 4) {
-            const float *src = seg < 2 ? row + (2 * kvh + seg) * HD
-                                       : row + (seg == 2 ? t.NH * HD : (t.NH + t.KV) * HD) + kvh * HD;
-            x = reinterpret_cast<const float4 *>(src)[l];
-        }
-        float ss = x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
-#pragma unroll
-        for (int o = D4 / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
-        if (seg < 3) {
-            const float iv = rms_inv(ss, HD, t.eps);
-            const float4 wn = reinterpret_cast<const float4 *>(seg < 2 ? t.qn_w : t.kn_w)[l];
-            x.x = x.x * iv * wn.x; x.y = x.y * iv * wn.y; x.z = x.z * iv * wn.z; x.w = x.w * iv * wn.w;
-        }
-        float4 o4;
-        o4.x = __shfl_xor(x.x, D4 / 2, 64); o4.y = __shfl_xor(x.y, D4 / 2, 64);
-        o4.z = __shfl_xor(x.z, D4 / 2, 64); o4.w = __shfl_xor(x.w, D4 / 2, 64);
-        if (seg < 4) {
-            float4 y = x;
-            if (seg < 3) {
-                const float4 c4 = reinterpret_cast<const float4 *>(t.rope_cos + (size_t)p * HD)[l];
-                const float4 s4 = reinterpret_cast<const float4 *>(t.rope_sin + (size_t)p * HD)[l];
-                if (l < D4 / 2) {
-                    y.x = x.x * c4.x - o4.x * s4.x; y.y = x.y * c4.y - o4.y * s4.y;
-                    y.z = x.z * c4.z - o4.z * s4.z; y.w = x.w * c4.w - o4.w * s4.w;
-                } else {
-                    y.x = x.x * c4.x + o4.x * s4.x; y.y = x.y * c4.y + o4.y * s4.y;
-                    y.z = x.z * c4.z + o4.z * s4.z; y.w = x.w * c4.w + o4.w * s4.w;
-                }
-            }
-            reinterpret_cast<float4 *>(lq)[tid] = y;
-            if (seg >= 2 && rb == 0 && !(t.skip && t.skip[0])) {
-                float *dst = (seg == 2 ? t.kc : t.vc) + (size_t)p * KVD + kvh * HD;
-                reinterpret_cast<float4 *>(dst)[l] = y;
-            }
-        }
-    }
-    __syncthreads();
-    // 3. online softmax over 64-key chunks
-    const float *Kc = t.kc + kvh * HD, *Vc = t.vc + kvh * HD;
-    const float scale = div_rn(1.0f, sqrt_rn((float)HD));
-    const int kk = tid / LPK, ks = tid - kk * LPK;       // scores: key kk of the chunk, dims ks*DPL..
-    const int oh = tid / HD, od = tid - oh * HD;         // P.V: output (head oh, dim od)
-    float acc = 0.f, m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
-    for (int c0 = 0; c0 < n; c0 += CH) {
-        const int key = c0 + kk;
-        float d0 = 0.f, d1 = 0.f;
-        if (key < n) {
-            const float4 *k4 = key == p ? reinterpret_cast<const float4 *>(lq + 2 * HD + ks * DPL)
-                                        : reinterpret_cast<const float4 *>(Kc + (size_t)key * KVD + ks * DPL);
-            const float4 *q0 = reinterpret_cast<const float4 *>(lq + ks * DPL);
-            const float4 *q1 = reinterpret_cast<const float4 *>(lq + HD + ks * DPL);
-#pragma unroll
-            for (int j = 0; j < DPL / 4; ++j) {
-                const float4 kv = k4[j], a0 = q0[j], a1 = q1[j];
-                d0 += a0.x * kv.x + a0.y * kv.y + a0.z * kv.z + a0.w * kv.w;
-                d1 += a1.x * kv.x + a1.y * kv.y + a1.z * kv.z + a1.w * kv.w;
-            }
-        }
-#pragma unroll
-        for (int o = LPK / 2; o >= 1; o >>= 1) { d0 += __shfl_xor(d0, o, 64); d1 += __shfl_xor(d1, o, 64); }
-        if (ks == 0) {
-            sc[0][kk] = key < n ? d0 * scale : -INFINITY;
-            sc[1][kk] = key < n ? d1 * scale : -INFINITY;
-        }
-        __syncthreads();
-        if (w < 2) {   // wave h: this chunk's max, rescale, probabilities
-            const float sv = sc[w][lane];
-            const float mc = wave_max(sv);
-            const float mn = fmaxf(m_run[w], mc);
-            const float e = c0 + lane < n ? expf(sv - mn) : 0.f;
-            const float ls = wave_sum(e);
-            sc[w][lane] = e;
-            if (lane == 0) {
-                const float al = m_run[w] == -INFINITY ? 0.f : expf(m_run[w] - mn);
-                alpha[w] = al;
-                lsum[w] = l_run[w] * al + ls;
-            }
-            m_run[w] = mn;
-        }
-        __syncthreads();
-        if (oh < 2) {
-            float sacc = 0.f;
-            const int kn = n - c0 < CH ? n - c0 : CH;
-            for (int k = 0; k < kn; ++k) {
-                const int kt = c0 + k;
-                const float v = kt == p ? lq[3 * HD + od] : Vc[(size_t)kt * KVD + od];
-                sacc += sc[oh][k] * v;
-            }
-            acc = acc * alpha[oh] + sacc;
-        }
-        l_run[0] = lsum[0];
-        l_run[1] = lsum[1];
-        __syncthreads();
-    }
-    if (oh < 2) att[oh * HD + od] = acc * div_rn(1.0f, l_run[oh]);
-    __syncthreads();
-    // 4. the O fragment against this head pair's attention output
-#pragma unroll
-    for (int i = 0; i < RPS; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            float f[8];
-            unpack8(wv[i][j], f);
-            const float *xp = att + 8 * (sub + LPS * j);
-            const float4 x0 = *reinterpret_cast<const float4 *>(xp);
-            const float4 x1 = *reinterpret_cast<const float4 *>(xp + 4);
-            a = fmaf(f[0], x0.x, a); a = fmaf(f[1], x0.y, a); a = fmaf(f[2], x0.z, a); a = fmaf(f[3], x0.w, a);
-            a = fmaf(f[4], x1.x, a); a = fmaf(f[5], x1.y, a); a = fmaf(f[6], x1.z, a); a = fmaf(f[7], x1.w, a);
-        }
-#pragma unroll
-        for (int o = LPS / 2; o >= 1; o >>= 1) a += __shfl_xor(a, o, 64);
-        const int row = (rb * RPS + i) * SLOTS + slot;
-        if (sub == 0 && row < R) part[(size_t)kvh * R + row] = a;
-    }
-}
-
 }  // namespace
-
-// Talker attention + O projection by kv head (batch 1); 1 = not covered.
-// rps: W_o rows per 8-lane slot (1, 2, 4).
-int qtts_attn_o_dec(const AttnArgs &a, const bf16_t *Wo, int R, float *part, int rps, hipStream_t st) {
-    const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
-    if (!(a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.nrows == 1 &&
-          ((uintptr_t)Wo & 15) == 0 && (a.NH * a.HD) % 8 == 0 && (rps == 1 || rps == 2 || rps == 4)))
-        return 1;
-    const int W2 = 2 * a.HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS * rps;
-    const dim3 grid((R + RPW - 1) / RPW, a.KV);
-#define QTTS_AOD(H, P)                                                                                     \
-    if (a.HD == H && rps == P) {                                                                           \
-        hipLaunchKernelGGL((k_attn_o_dec<H, P>), grid, dim3(256), 0, st, a, Wo, R, part);                  \
-        qtts_last_kernel = "k_attn_o_dec<" #H ", " #P ">";                                                 \
-    }
-    QTTS_AOD(128, 1) QTTS_AOD(128, 2) QTTS_AOD(128, 4)
-    QTTS_AOD(64, 1) QTTS_AOD(64, 2) QTTS_AOD(64, 4)
-    QTTS_AOD(32, 1) QTTS_AOD(32, 2) QTTS_AOD(32, 4)
-    QTTS_AOD(16, 1) QTTS_AOD(16, 2) QTTS_AOD(16, 4)
-#undef QTTS_AOD
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 // Sub-talker attention + O projection by kv head, rows b < nrows (grid z):
 // part[(kvh * nrows + b) * R + row]; 1 = not covered.
@@ -739,7 +531,7 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
     }
     const int gph = a.NH / a.KV;
     const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
-    if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok && a.S <= 16 && !getenv("QTTS_HIP_NO_SHORT_ATTN")) {
+    if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok && a.S <= 16) {
         const dim3 grid(a.KV, a.nrows);
         switch (a.HD) {
             case 128: hipLaunchKernelGGL((k_attn_short<128>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_short<128>"; break;
@@ -756,7 +548,7 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
             fprintf(stderr, "qtts_attention: split scratch missing (need %d splits)\n", nsplit);
             return -1;
         }
-        const dim3 grid(a.KV, nsplit, a.nrows + (a.pf0_bytes + a.pf1_bytes ? a.pf_z : 0));
+        const dim3 grid(a.KV, nsplit, a.nrows);
         switch (a.HD) {
             case 128: hipLaunchKernelGGL((k_attn_dec<128, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<128, 2>"; break;
             case 64: hipLaunchKernelGGL((k_attn_dec<64, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<64, 2>"; break;
@@ -776,8 +568,7 @@ int qtts_qk_prep(const AttnArgs &a, hipStream_t st) {
         fprintf(stderr, "qtts_qk_prep: (NH+KV)*HD=%d exceeds 4096\n", (a.NH + a.KV) * a.HD);
         return -1;
     }
-    static const bool old_prep = getenv("QTTS_HIP_QK_PREP_BLOCK") != nullptr;
-    if (!old_prep && (a.HD == 128 || (a.HD <= 64 && (a.HD & (a.HD - 1)) == 0))) {
+    if ((a.HD == 128 || (a.HD <= 64 && (a.HD & (a.HD - 1)) == 0))) {
         const dim3 grid(a.nrows, (a.NH + 2 * a.KV + 3) / 4);
         hipLaunchKernelGGL(k_qk_prep_w, grid, dim3(256), 0, st, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;

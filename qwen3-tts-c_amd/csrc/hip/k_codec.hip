@@ -715,27 +715,22 @@ __global__ void k_iota(int *p, int n, int zero) {
 
 // k_conv covers the conv when its re-laid weights are given, the channels
 // come in whole stages, the window halo fits and the output fills the chip
-// (small first-packet decodes keep the split-K GEMM).  QTTS_HIP_CONV=0 / 1
-// disables / forces it (tests).
+// (small first-packet decodes keep the split-K GEMM).
 static int conv_splits(const XGemm &g);
 static bool conv_ok(const XGemm &g) {
-    static const char *f = getenv("QTTS_HIP_CONV");
-    if (f && !atoi(f)) return false;
-    static const char *ft = getenv("QTTS_HIP_CONV_TILES");
-    static const int min_tiles = ft ? atoi(ft) : 96;
+    constexpr int min_tiles = 96;
     if (!g.wt || g.bmode != XB_CONV || g.amode != XA_ROWS ||
         !(g.Kw == 1 || g.Kw == 2 || g.Kw == 3 || g.Kw == 7) || (g.K / g.Kw) % CV_BC ||
         (g.Kw - 1) * g.dil > CV_HALO || ((uintptr_t)g.wt & 15))
         return false;
     const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM) * (g.stride > 1 ? g.stride : 1);
-    return (f && atoi(f)) || tiles >= min_tiles || (g.part && conv_splits(g) > 1);
+    return tiles >= min_tiles || (g.part && conv_splits(g) > 1);
 }
 
 // input-channel splits for a grid that would not fill the chip: up to 1024
-// workgroups, >= 2 channel stages each (QTTS_HIP_CONV_SPLIT=0 disables)
+// workgroups, >= 2 channel stages each
 static int conv_splits(const XGemm &g) {
-    static const char *f = getenv("QTTS_HIP_CONV_SPLIT");
-    if ((f && !atoi(f)) || !g.part) return 1;
+    if (!g.part) return 1;
     const int nph = g.stride > 1 ? g.stride : 1;
     const int tiles = ((g.N + CV_BN - 1) / CV_BN) * ((g.M + CV_BM - 1) / CV_BM) * nph;
     const int ci = g.K / g.Kw;
@@ -750,16 +745,13 @@ static int conv_launch(const XGemm &gin, int nph, hipStream_t st) {
     XGemm g = gin;
     g.kz = conv_splits(g);
     const dim3 cg((g.N + CV_BN - 1) / CV_BN, (g.M + CV_BM - 1) / CV_BM, nph * g.kz);
-    static const char *fb = getenv("QTTS_HIP_CONV_BF");
-    static const bool bf_on = !fb || atoi(fb);
-    const bool bf = bf_on && (!g.sa || g.K / g.Kw / (g.kz > 1 ? g.kz : 1) <= CB_SNAKE_MAX);
+    // bf16 3-plane MFMA path, except a SnakeBeta prologue over more input
+    // channels than its staging covers (then the fp32 MFMA k_conv)
+    const bool bf = !g.sa || g.K / g.Kw / (g.kz > 1 ? g.kz : 1) <= CB_SNAKE_MAX;
     if (bf) {
         // 256-column tiles where the grid still holds >= 2 workgroups per CU
-        // (QTTS_HIP_CONV_WN=2 keeps 128)
-        static const char *fw = getenv("QTTS_HIP_CONV_WN");
-        static const int wn_max = fw ? atoi(fw) : 4;
         const int tiles4 = ((g.N + 255) / 256) * cg.y * cg.z;
-        if (wn_max >= 4 && tiles4 >= 512) {
+        if (tiles4 >= 512) {
             const dim3 c4((g.N + 255) / 256, cg.y, cg.z);
             switch (g.Kw) {
                 case 7: hipLaunchKernelGGL((k_convb<7, 4>), c4, dim3(512), 0, st, g); break;
@@ -790,10 +782,8 @@ static int conv_launch(const XGemm &gin, int nph, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// k_xgemv covers a linear at <= 4 rows (QTTS_HIP_XGEMV=0 disables)
+// k_xgemv covers a linear at <= 4 rows
 static bool xgemv_ok(const XGemm &g) {
-    static const char *f = getenv("QTTS_HIP_XGEMV");
-    if (f && !atoi(f)) return false;
     return g.M <= 4 && g.bmode == XB_WT && (g.amode == XA_ROWS || g.amode == XA_TRANS) && g.K % 256 == 0 &&
            g.ldb % 4 == 0 && ((uintptr_t)g.B & 15) == 0 && (size_t)4 * g.K * 4 + 512 <= 64 * 1024;
 }
@@ -869,6 +859,13 @@ void codec_free_state(CodecModel *m) {
     m->t_cap = 0;
     m->rope_cap = 0;
     m->bufA = m->bufB = m->bufC = m->bufD = nullptr;
+    m->tq = m->tx = m->txn = m->tatt = m->tg = m->tu = nullptr;
+    m->rope_cos = m->rope_sin = nullptr;
+    m->codes_tmp = nullptr;
+    // the split-K workspace lives in `scratch` too: a stream that outlives this
+    // state (codec_stream_begin's reuse path) must re-create it, never reuse it
+    m->xg_part = nullptr;
+    m->xg_part_elems = 0;
 }
 
 void codec_destroy(CodecModel *m) {
@@ -1007,7 +1004,13 @@ int codec_finalize(CodecModel *m) {
 
 static void *scratch_alloc(CodecModel *m, size_t bytes) {
     void *p = nullptr;
-    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    const hipError_t prior = hipPeekAtLastError();
+    const hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+        fprintf(stderr, "qtts codec: hipMalloc(%zu) failed: %s (last error before it: %s)\n", bytes,
+                hipGetErrorName(e), hipGetErrorName(prior));
+        return nullptr;
+    }
     m->scratch.push_back(p);
     m->scratch_bytes += bytes;
     return p;
@@ -1074,7 +1077,7 @@ static int ensure_codec_state(CodecModel *m, int T) {
 
 // codec GEMMs get the split-K workspace
 static int xgm(CodecModel *m, XGemm g, hipStream_t st) {
-    g.part = m->xg_part;
+    g.part = m->xg_part;   // nullptr (kernel-level entries' stateless model): no split
     g.part_elems = m->xg_part_elems;
     return qtts_xgemm(g, st);
 }
@@ -1358,7 +1361,13 @@ constexpr int kStreamChunk = 16;   // frames per internal chunk
 
 void *salloc(CodecStream &S, size_t bytes) {
     void *p = nullptr;
-    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    const hipError_t prior = hipPeekAtLastError();
+    const hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+        fprintf(stderr, "qtts codec stream: hipMalloc(%zu) failed: %s (last error before it: %s)\n", bytes,
+                hipGetErrorName(e), hipGetErrorName(prior));
+        return nullptr;
+    }
     hipMemset(p, 0, bytes ? bytes : 16);
     S.allocs.push_back(p);
     return p;
@@ -1502,6 +1511,10 @@ void codec_stream_free(CodecModel *m) {
 int codec_stream_begin(CodecModel *m, int max_frames) {
     const qtts_dims_t &d = m->d;
     CodecStream &S0 = m->cs;
+    // the codec GEMMs' split-K workspace belongs to the (non-streaming) codec
+    // state, which the decode state's re-allocation frees (free_state ->
+    // codec_free_state): re-create it before a stream reuses its own buffers
+    if (ensure_codec_state(m, 1)) return -1;
     if (S0.active && max_frames + S0.tc <= S0.rope_cap) {
         // reuse the buffers: only the carried state restarts (zero histories =
         // the causal left padding, no K/V rows, position 0), on the codec stream
@@ -1514,7 +1527,7 @@ int codec_stream_begin(CodecModel *m, int max_frames) {
         return 0;
     }
     codec_stream_free(m);
-    if (ensure_codec_state(m, 1)) return -1;   // split-K workspace
+    // (ensure_codec_state ran above: the split-K workspace exists)
     CodecStream &S = m->cs;
     S.tc = kStreamChunk;
     const int hm = S.hm, tc = S.tc;
@@ -1600,6 +1613,10 @@ int codec_stream_push_to(CodecModel *m, const int *codes, int ldc_codes, int Tto
     CodecStream &S = m->cs;
     const qtts_dims_t &d = m->d;
     if (!S.active || ldc_codes != d.cq) return -1;
+    if (!m->xg_part) {   // freed with the codec state and not re-created (codec_stream_begin re-creates it)
+        fprintf(stderr, "qtts codec stream: split-K workspace missing (stream not begun after a state re-allocation)\n");
+        return -1;
+    }
     if (S.pos0 + Ttot > S.rope_cap - S.tc) {
         fprintf(stderr, "qtts codec stream: %d frames exceed the stream capacity\n", S.pos0 + Ttot);
         return -1;

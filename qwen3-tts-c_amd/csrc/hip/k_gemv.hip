@@ -8,8 +8,6 @@
 //          - optional RMSNorm (c/qwen_tts_kernels.c:27-39) with the full-row
 //            statistics computed per workgroup
 //          - optional copy-out (raw or normalised) by workgroup 0
-//          - or (k_gemv1_att) the short-context decode attention of the token,
-//            computed from its q|k|v row (qtts_attn_pro.h)
 //   epilogue: store / +bias / +bias then SiLU / residual add (x += acc) /
 //             SwiGLU over interleaved gate|up row quads.
 //
@@ -24,78 +22,10 @@
 // combine through LDS.  KSPLIT is chosen on the host so the grid fills the 256
 // CUs.  Weight loads for the first block group are issued before the prologue
 // so HBM latency overlaps the norm.  Accumulation is fp32 (exact bf16->f32).
-#include "qtts_attn_dev.h"
-#include "qtts_attn_pro.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
-#include "qtts_sample_dev.h"
 
 namespace {
-
-// Optional tail work of the batch-1 GEMV (TAIL = 1: decode attention of the
-// kv head whose q/k/v rows this grid just produced; TAIL = 2: the sampler).
-template <int TAIL> struct TailA { int unused; };
-template <> struct TailA<1> { AttnArgs at; };
-template <> struct TailA<2> { SampArgs sa; int *cnt; };
-
-// Tail hand-off (cdna_hip_programming.md Guideline 16, R1 counter form): the
-// GEMV epilogue stores the rows the tail reads with write-through (sc1)
-// stores; every wave drains vmcnt, the workgroup barriers, lane 0 takes a
-// relaxed agent-scope ticket; the last arriver reads the rows with sc1 loads
-// (no release / acquire fences: a per-workgroup __threadfence() here cost
-// ~10x the kernel).  The last arriver resets the ticket (zeroed at alloc).
-// `flag` is an LDS word of the DYNAMIC region (see k_gemv1).
-
-// The last workgroup of the logit-head GEMV draws the token (qtts_sample_dev.h),
-// so sampling costs no kernel of its own.
-__device__ __forceinline__ void gemv_sample_tail(const SampArgs &sa, int *cnt, int *flag, float *pool) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = (old == (int)gridDim.x - 1);
-    }
-    __syncthreads();
-    if (!*flag) return;
-    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    qtts_samp::sample_row<true>(sa, 0, reinterpret_cast<unsigned char *>(pool));
-}
-
-// The last workgroup to finish the q/k/v rows of a kv head runs that head's
-// attention (one ticket per kv head).
-__device__ __forceinline__ void gemv_attn_tail(const AttnArgs &t, int row0, int RPW, int *flag, float *pool) {
-    const int HD = t.HD, NH = t.NH, KV = t.KV, gph = NH / KV;
-    int kvg;
-    if (row0 < NH * HD) kvg = (row0 / HD) / gph;
-    else if (row0 < (NH + KV) * HD) kvg = (row0 - NH * HD) / HD;
-    else kvg = (row0 - (NH + KV) * HD) / HD;
-    const int need = (gph + 2) * HD / RPW;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(t.cnt + kvg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = (old == need - 1);
-    }
-    __syncthreads();
-    if (!*flag) return;
-    if (t.S <= 16) {   // short context (the sub-talker): the lean single-workgroup body
-        switch (HD) {
-            case 128: attn_short_wg<128, true>(t, kvg, 0, pool, pool + 4 * 128); break;
-            case 64: attn_short_wg<64, true>(t, kvg, 0, pool, pool + 4 * 64); break;
-            case 32: attn_short_wg<32, true>(t, kvg, 0, pool, pool + 4 * 32); break;
-            default: attn_short_wg<16, true>(t, kvg, 0, pool, pool + 4 * 16); break;
-        }
-        if (threadIdx.x == 0) __hip_atomic_store(t.cnt + kvg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    switch (HD) {
-        case 128: attn_full_wg<128, 2, true>(t, kvg, 0, pool); break;
-        case 64: attn_full_wg<64, 2, true>(t, kvg, 0, pool); break;
-        case 32: attn_full_wg<32, 2, true>(t, kvg, 0, pool); break;
-        default: attn_full_wg<16, 2, true>(t, kvg, 0, pool); break;
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(t.cnt + kvg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 constexpr int U = 8;  // blocks per load group (16 B each per lane)
 
@@ -257,7 +187,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// Batch-1 weight stream shared by k_gemv1 and k_gemv1_att: the 8-lane slot of
+// Batch-1 weight stream of k_gemv1: the 8-lane slot of
 // row `row` streams its KSPLIT share of the row's 64-column blocks in groups of
 // U1 x 16 B per lane, double-buffered in registers (the first group is issued
 // by the caller before its prologue).
@@ -335,9 +265,7 @@ struct G1Stream {
 };
 
 // Batch-1 epilogue: KSPLIT partials through LDS `red` [32], one barrier, then
-// one thread per output row applies the epilogue.  SC1: plain stores become
-// write-through (the rows are handed to a tail of the same launch).
-template <bool SC1>
+// one thread per output row applies the epilogue.
 __device__ __forceinline__ void g1_epilogue(const GemvArgs &a, float acc, float *red, int row0, int RPW, int ksn,
                                             int ks, int rloc, int sub) {
     const int tid = threadIdx.x;
@@ -349,10 +277,7 @@ __device__ __forceinline__ void g1_epilogue(const GemvArgs &a, float acc, float 
             float v = red[tid];
             for (int k = 1; k < ksn; ++k) v += red[k * RPW + tid];
             switch (a.epi) {
-                case EPI_STORE:
-                    if constexpr (SC1) st_sc1(a.y + r, v);
-                    else a.y[r] = v;
-                    break;
+                case EPI_STORE: a.y[r] = v; break;
                 case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
                 case EPI_BIAS_SILU: {
                     const float z = v + a.bias[r];
@@ -379,16 +304,16 @@ __device__ __forceinline__ void g1_epilogue(const GemvArgs &a, float acc, float 
 // already in flight.  One barrier in the epilogue: each output thread sums
 // the KSPLIT partials it needs (for SwiGLU also its up row's) straight from
 // LDS.
-// Dynamic LDS: [flag: 4 words][xs: C][red: 32][bred: 4].  The tails' ticket
-// flag lives in the dynamic region on purpose: a static __shared__ is placed
-// in front of it and shifts every float4 LDS access off its 16-B alignment
-// (replayed at 64 cycles each, cdna_hip_programming.md Guideline 17).
-constexpr int G1_HEAD = 4;   // floats in front of xs
+// Dynamic LDS: [xs: C][red: nslot][bred: nthr/64], all of it in the dynamic
+// region (a static __shared__ would shift every float4 LDS access off its
+// 16-B alignment: replayed at 64 cycles each, cdna_hip_programming.md
+// Guideline 17).
+constexpr int G1_HEAD = 0;   // floats in front of xs
 
-// Block size: 256 threads (the tails), or up to 1024 ("wide": one workgroup
-// per CU streaming R/256 rows, qtts_gemv) -- nslot = blockDim/8 slots.
-template <int U1, int XV, bool NT, int TAIL>
-__global__ __launch_bounds__(TAIL == 0 ? 1024 : 256) void k_gemv1(GemvArgs a, TailA<TAIL> ta) {
+// Block size: 256 threads, or up to 1024 ("wide": one workgroup per CU
+// streaming R/256 rows, qtts_gemv) -- nslot = blockDim/8 slots.
+template <int U1, int XV, bool NT>
+__global__ __launch_bounds__(1024) void k_gemv1(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7, nthr = blockDim.x, nslot = nthr >> 3;
     const int ksn = a.ksplit, RPW = nslot / ksn;
@@ -468,33 +393,7 @@ __global__ __launch_bounds__(TAIL == 0 ? 1024 : 256) void k_gemv1(GemvArgs a, Ta
 
     // ---- stream the weights, then the epilogue (and the tail) ----
     const float acc = ws.run(xs);
-    g1_epilogue<TAIL != 0>(a, acc, red, row0, RPW, ksn, ks, rloc, sub);
-    int *flag = reinterpret_cast<int *>(smem);
-    if constexpr (TAIL == 1) gemv_attn_tail(ta.at, row0, RPW, flag, smem + G1_HEAD);
-    if constexpr (TAIL == 2) gemv_sample_tail(ta.sa, ta.cnt, flag, smem + G1_HEAD);
-}
-
-// ---------------------------------------------------------------------------
-// Batch-1 O projection with the decode attention as its prologue
-// (qtts_attn_pro.h): x = attention(q|k|v row, K/V cache) computed in every
-// workgroup into LDS, then the weight stream and the epilogue of k_gemv1.
-// Dynamic LDS: [xs: C][red: 32][lq: (NH+2KV)*HD][sc: NH*ATT_NMAX].
-template <int U1, bool NT, int HD>
-__global__ __launch_bounds__(256) void k_gemv1_att(GemvArgs a, AttnArgs t) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int tid = threadIdx.x, slot = tid >> 3, sub = tid & 7;
-    const int ksn = a.ksplit, RPW = 32 / ksn;
-    const int rloc = slot % RPW, ks = slot / RPW;
-    const int row0 = blockIdx.x * RPW, row = row0 + rloc;
-    float *xs = smem;                        // [C] attention output = this GEMV's input
-    float *red = xs + a.C;                   // [32]
-    float *lq = red + 32;                    // [(NH+2KV)*HD] rotated q|k, raw v
-    float *sc = lq + (t.NH + 2 * t.KV) * HD; // [NH][ATT_NMAX] scores / probabilities
-    G1Stream<U1, NT> ws(a, row, ks, ksn, sub);
-    ws.load(0);
-    att_prologue<HD>(t, xs, lq, sc, blockIdx.x == 0);
-    const float acc = ws.run(xs);
-    g1_epilogue<false>(a, acc, red, row0, RPW, ksn, ks, rloc, sub);
+    g1_epilogue(a, acc, red, row0, RPW, ksn, ks, rloc, sub);
 }
 
 }  // namespace
@@ -514,18 +413,10 @@ static int pick_ksplit(int R, int C, int epi, int target) {
     return ks;
 }
 
-// "Wide" batch-1 configuration: about one workgroup per CU (grid ~ 256),
-// each streaming ceil(R / 256) rows with up to 1024 threads, so the grid runs
-// in one round and x is staged 256 times instead of once per 32-row block.
-// QTTS_HIP_GEMV_WIDE = 0 / 1 / 2: off / talker (non-temporal) weights only /
-// every batch-1 GEMV.
-static bool gemv_wide(int nt) {
-    static const int mode = [] {
-        const char *e = getenv("QTTS_HIP_GEMV_WIDE");
-        return e ? atoi(e) : 1;
-    }();
-    return mode == 2 || (mode == 1 && nt);
-}
+// "Wide" batch-1 configuration for the talker's (non-temporal) weights:
+// about one workgroup per CU (grid ~ 256), each streaming ceil(R / 256) rows
+// with up to 1024 threads, so the grid runs in one round and x is staged 256
+// times instead of once per 32-row block.
 static void wide_config(int R, int C, int epi, int &ks_out, int &nthr_out) {
     const int nb64 = C / 64, quad = epi == EPI_SWIGLU ? 8 : 1;
     int rows = (R + 255) / 256;
@@ -555,7 +446,7 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         int nthr = 256;
         // (one CU's share >= 96 KB: below that the 256-thread grid measured faster,
         // profiles/r01x_mb_gemv_wide_u16.txt)
-        if (a.ksplit <= 0 && gemv_wide(a.nt) && (size_t)a.R * a.C * 2 / 256 >= 96 * 1024) {
+        if (a.ksplit <= 0 && a.nt && (size_t)a.R * a.C * 2 / 256 >= 96 * 1024) {
             wide_config(a.R, a.C, a.epi, a.ksplit, nthr);
         }
         if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
@@ -565,14 +456,13 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         const int xq = (a.C + 4 * nthr - 1) / (4 * nthr);
         const int xv = xq <= 1 ? 1 : xq <= 2 ? 2 : xq <= 4 ? 4 : 8;
         const size_t smem = (size_t)(G1_HEAD + a.C + nthr / 8 + 16) * sizeof(float);
-        const TailA<0> t0{0};
 #define QTTS_G1(U, X)                                                                                 \
         if (a.nt) {                                                                                   \
-            hipLaunchKernelGGL((k_gemv1<U, X, true, 0>), dim3(grid), dim3(nthr), smem, st, a, t0);    \
-            qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 0>";                                    \
+            hipLaunchKernelGGL((k_gemv1<U, X, true>), dim3(grid), dim3(nthr), smem, st, a);           \
+            qtts_last_kernel = "k_gemv1<" #U ", " #X ", true>";                                       \
         } else {                                                                                      \
-            hipLaunchKernelGGL((k_gemv1<U, X, false, 0>), dim3(grid), dim3(nthr), smem, st, a, t0);   \
-            qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 0>";                                   \
+            hipLaunchKernelGGL((k_gemv1<U, X, false>), dim3(grid), dim3(nthr), smem, st, a);          \
+            qtts_last_kernel = "k_gemv1<" #U ", " #X ", false>";                                      \
         }
         if (nthr != 256 && nblk > 8 && nblk <= 16) {   // wide: every weight load of a lane in one group
             switch (xv) { case 1: QTTS_G1(16, 1) break; case 2: QTTS_G1(16, 2) break;
@@ -620,111 +510,5 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         QTTS_GEMV_CASE(16)
     }
 #undef QTTS_GEMV_CASE
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// QKV GEMV with the decode attention fused as its tail (batch 1).  Returns 1
-// when the configuration is not covered (the caller launches the two
-// kernels), 0 on success, -1 on a launch error.
-int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st) {
-    const int HD = t.HD;
-    const bool hd_ok = HD == 128 || HD == 64 || HD == 32 || HD == 16;
-    if (!(a.nb == 1 && t.nrows == 1 && a.C <= 2048 && a.ldx_ok1() && hd_ok && t.KV > 0 && t.NH == 2 * t.KV &&
-          t.mode == 0 && t.win == 0 && t.cnt && a.epi == EPI_STORE && a.R == (t.NH + 2 * t.KV) * HD))
-        return 1;
-    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
-    while (32 / a.ksplit > HD && a.ksplit < a.C / 64) a.ksplit *= 2;   // one kv head per workgroup
-    if (32 / a.ksplit > HD || (a.C / 64) % a.ksplit) return 1;
-    const int rpw = 32 / a.ksplit;
-    const int grid = a.R / rpw;
-    const int nblk = a.C / 64 / a.ksplit;
-    int pool = 0;
-    switch (HD) {
-        case 128: pool = AttnWG<128, 2>::POOL; break;
-        case 64: pool = AttnWG<64, 2>::POOL; break;
-        case 32: pool = AttnWG<32, 2>::POOL; break;
-        default: pool = AttnWG<16, 2>::POOL; break;
-    }
-    const size_t smem = (size_t)(G1_HEAD + (a.C + 36 > pool ? a.C + 36 : pool)) * sizeof(float);
-    const TailA<1> ta{t};
-#define QTTS_GT(U, X)                                                                                 \
-    if (a.nt) {                                                                                       \
-        hipLaunchKernelGGL((k_gemv1<U, X, true, 1>), dim3(grid), dim3(256), smem, st, a, ta);         \
-        qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 1>";                                        \
-    } else {                                                                                          \
-        hipLaunchKernelGGL((k_gemv1<U, X, false, 1>), dim3(grid), dim3(256), smem, st, a, ta);        \
-        qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 1>";                                       \
-    }
-    if (nblk >= 8) {
-        if (a.C <= 1024) { QTTS_GT(8, 1) } else { QTTS_GT(8, 2) }
-    } else {
-        if (a.C <= 1024) { QTTS_GT(4, 1) } else { QTTS_GT(4, 2) }
-    }
-#undef QTTS_GT
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// Logit-head GEMV with the sampler fused as its tail (batch 1).  Returns 1
-// when not covered (the caller launches the sampler), 0 ok, -1 error.
-int qtts_gemv_sample(GemvArgs a, const SampArgs &sa, int *cnt, hipStream_t st) {
-    if (!(a.nb == 1 && sa.nb == 1 && a.C <= 8192 && a.ldx_ok1() && cnt && a.epi == EPI_STORE && sa.n == a.R &&
-          qtts_samp::fast_path(sa) && sa.logits == a.y))
-        return 1;
-    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, 512);
-    const int rpw = 32 / a.ksplit;
-    const int grid = (a.R + rpw - 1) / rpw;
-    const int nblk = a.C / 64 / a.ksplit;
-    const int xv = a.C <= 1024 ? 1 : a.C <= 2048 ? 2 : a.C <= 4096 ? 4 : 8;
-    size_t smem = (size_t)(a.C + 36) * sizeof(float);
-    if (smem < sizeof(qtts_samp::FastSmem)) smem = sizeof(qtts_samp::FastSmem);
-    smem += G1_HEAD * sizeof(float);
-    TailA<2> ta;
-    ta.sa = sa;
-    ta.cnt = cnt;
-#define QTTS_GS(U, X)                                                                                 \
-    if (a.nt) {                                                                                       \
-        hipLaunchKernelGGL((k_gemv1<U, X, true, 2>), dim3(grid), dim3(256), smem, st, a, ta);         \
-        qtts_last_kernel = "k_gemv1<" #U ", " #X ", true, 2>";                                        \
-    } else {                                                                                          \
-        hipLaunchKernelGGL((k_gemv1<U, X, false, 2>), dim3(grid), dim3(256), smem, st, a, ta);        \
-        qtts_last_kernel = "k_gemv1<" #U ", " #X ", false, 2>";                                       \
-    }
-    if (nblk >= 8) {
-        switch (xv) { case 1: QTTS_GS(8, 1) break; case 2: QTTS_GS(8, 2) break;
-                      case 4: QTTS_GS(8, 4) break; default: QTTS_GS(8, 8) break; }
-    } else {
-        switch (xv) { case 1: QTTS_GS(4, 1) break; case 2: QTTS_GS(4, 2) break;
-                      case 4: QTTS_GS(4, 4) break; default: QTTS_GS(4, 8) break; }
-    }
-#undef QTTS_GS
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// O-projection GEMV with the decode attention as its prologue (batch 1,
-// short context: the sub-talker).  `target_wg` sizes the grid: every
-// workgroup recomputes the attention, so fewer, fuller workgroups trade
-// weight-stream parallelism for less redundant K/V traffic.  Returns 1 when
-// not covered (the caller launches attention + GEMV), 0 ok, -1 error.
-int qtts_gemv_att(GemvArgs a, const AttnArgs &t, int target_wg, hipStream_t st) {
-    if (!(a.nb == 1 && a.C <= 8192 && a.C % 64 == 0 && a.epi != EPI_SWIGLU && att_pro_ok(t, a.C))) return 1;
-    if (a.ksplit <= 0) a.ksplit = pick_ksplit(a.R, a.C, a.epi, target_wg > 0 ? target_wg : 256);
-    const int rpw = 32 / a.ksplit;
-    const int grid = (a.R + rpw - 1) / rpw;
-    const int nblk = a.C / 64 / a.ksplit;
-    const size_t smem = (size_t)(a.C + 32 + att_pro_lds_floats(t.NH, t.KV, t.HD)) * sizeof(float);
-#define QTTS_GA(U, H)                                                                                 \
-    if (a.nt) {                                                                                       \
-        hipLaunchKernelGGL((k_gemv1_att<U, true, H>), dim3(grid), dim3(256), smem, st, a, t);         \
-        qtts_last_kernel = "k_gemv1_att<" #U ", true, " #H ">";                                       \
-    } else {                                                                                          \
-        hipLaunchKernelGGL((k_gemv1_att<U, false, H>), dim3(grid), dim3(256), smem, st, a, t);        \
-        qtts_last_kernel = "k_gemv1_att<" #U ", false, " #H ">";                                      \
-    }
-#define QTTS_GA_HD(U)                                                                                 \
-    switch (t.HD) { case 128: QTTS_GA(U, 128) break; case 64: QTTS_GA(U, 64) break;                   \
-                    case 32: QTTS_GA(U, 32) break; default: QTTS_GA(U, 16) break; }
-    if (nblk >= 8) { QTTS_GA_HD(8) } else { QTTS_GA_HD(4) }
-#undef QTTS_GA_HD
-#undef QTTS_GA
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -308,8 +308,6 @@ static int gm_planes(int nb, int cch) { return 3 * nb * (cch + 8) * 2; }
 // Returns 1 when the shape is not covered (the caller uses k_gemv), 0 ok,
 // -1 launch error.
 int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
-    static const char *off = getenv("QTTS_HIP_GEMVM");
-    if (off && !atoi(off)) return 1;
     GemvArgs a = in;
     if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32) return 1;
     if (a.table) {

@@ -81,26 +81,11 @@ struct AttnArgs {
     float *part = nullptr;
     int *cnt = nullptr;
     int nsplit = 0;
-    // talker decode only: extra workgroups (grid z >= nrows, pf_z per (kv, split))
-    // read the next GEMVs' weights [pf0, +pf0_bytes) and [pf1, +pf1_bytes) while
-    // the latency-bound attention leaves HBM idle, so those GEMVs find them in
-    // the Infinity Cache; pf_sink: a scratch word that keeps the reads live
-    const void *pf0 = nullptr, *pf1 = nullptr;
-    size_t pf0_bytes = 0, pf1_bytes = 0;
-    int pf_z = 0;
-    unsigned *pf_sink = nullptr;
 };
 int qtts_attn_keys_per_split(int HD);
-int qtts_gemv_qkv_attn(GemvArgs a, const AttnArgs &t, hipStream_t st);
-// O projection with the short-context decode attention as its prologue
-// (qtts_attn_pro.h); 1 = not covered
-int qtts_gemv_att(GemvArgs a, const AttnArgs &t, int target_wg, hipStream_t st);
 // sub-talker attention + O projection split by kv head: part [KV][nrows][R]
 // (GQA 2, <= 16 keys); 1 = not covered
 int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st);
-// talker decode attention (any key count, 64-key online-softmax chunks) + O
-// projection by kv head (batch 1, GQA 2); rps W_o rows per slot; 1 = not covered
-int qtts_attn_o_dec(const AttnArgs &a, const bf16_t *Wo, int R, float *part, int rps, hipStream_t st);
 
 // Name of the kernel instantiation the last launcher on this thread chose
 // (diagnostics: per-kernel profile rows match rocprofv3's kernel names).
@@ -129,7 +114,6 @@ struct SampArgs {
     int codes_bstride = 0, G = 16, g = 0;
     int *out_tok = nullptr;        // optional plain output [b]
 };
-int qtts_gemv_sample(GemvArgs a, const SampArgs &sa, int *cnt, hipStream_t st);
 int qtts_sample(const SampArgs &a, hipStream_t st);
 
 struct EmbedSumArgs {

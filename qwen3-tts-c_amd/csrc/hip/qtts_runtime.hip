@@ -26,7 +26,6 @@
 #include <string>
 #include <vector>
 
-#include "qtts_attn_pro.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 #include "qtts_codec.h"
@@ -111,7 +110,6 @@ struct qtts_dev {
     int *stop_step = nullptr, *kv_len = nullptr, *n_trailing = nullptr;
     float *att_part = nullptr;   // split-K decode attention partials (talker)
     int *att_cnt = nullptr, att_nsplit = 0;
-    int *samp_cnt = nullptr;     // ticket of the GEMV + sampler fusion
     uint32_t *rng = nullptr, *st_rng = nullptr;
     float *trailing = nullptr, *prefill = nullptr, *pad_emb = nullptr;
     // prefill / prompt scratch
@@ -130,31 +128,17 @@ struct qtts_dev {
     // codec overlapped with the decode (qtts_dev_codec_async_*): its own stream,
     // ordered after the frames it decodes by an event; output stays on device
     hipStream_t cst = nullptr;
-    int codec_cus = 0, cu_mask_style = 0;   // QTTS_HIP_CODEC_CUS / QTTS_HIP_CU_MASK_STYLE
     hipEvent_t cev = nullptr;
     float *cwav = nullptr;
     size_t cwav_cap = 0;
+    // host codes staged for qtts_dev_codec_stream_push_host (grown on demand)
+    int *push_codes = nullptr;
+    size_t push_cap = 0;
     // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
     bool profiling = false;
-    bool fuse_attn = false;  // QTTS_HIP_FUSE=1: GEMV-tail fusions (talker attention, samplers)
-    bool fuse_st = false;    // QTTS_HIP_FUSE_ST=1: sub-talker attention as the QKV GEMV's tail
-    bool use_mfma = true;    // QTTS_HIP_NO_MFMA=1: multi-row projections on the GEMV path
-    bool att_pro = false;    // QTTS_HIP_ATT_PRO=1: sub-talker attention as the O GEMV's prologue
-                             // (measured slower: profiles/r01d_envsweep.txt)
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
-    int attn_o_tmax = 0;     // QTTS_HIP_ATTN_O_TALKER=S: talker attention + O fused while the key
-                             // capacity <= S (opt-in: 30 vs 17 us per layer at S ~150,
-                             // profiles/r01aj_envsweep_attn_o_talker.txt)
-    int attn_o_rps = 2;      // QTTS_HIP_ATTN_O_RPS: W_o rows per slot of the fused talker kernel
-    // talker attention prefetch (AttnArgs::pf*): the O weights (QTTS_HIP_PF_O) and
-    // the first QTTS_HIP_PF_GU MB of gate|up, by about QTTS_HIP_PF_WG workgroups.
-    // Opt-in: the attention launch grows by more than the GEMVs gain (23.9 vs
-    // 22.8 audio-s/s with O + 24 MB, profiles/r01am_envsweep_prefetch_inline.txt)
-    int pf_o = 1, pf_gu_mb = 24, pf_wg = 0;
-    unsigned *pf_sink = nullptr;
-    int att_pro_wg = 256;    // QTTS_HIP_ATT_PRO_WG: grid target of the attention-prologue O GEMV
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
     int pinv_cap = 0;
 
@@ -166,8 +150,11 @@ struct qtts_dev {
 static void *dalloc(qtts_dev *dv, size_t n, bool weight) {
     void *p = nullptr;
     if (n == 0) n = 16;
-    if (hipMalloc(&p, n) != hipSuccess) {
-        fprintf(stderr, "qtts: hipMalloc(%zu) failed\n", n);
+    const hipError_t prior = hipPeekAtLastError();
+    const hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+        fprintf(stderr, "qtts: hipMalloc(%zu) failed: %s (last error before it: %s)\n", n, hipGetErrorName(e),
+                hipGetErrorName(prior));
         return nullptr;
     }
     if (weight) { dv->wallocs.push_back(p); dv->wbytes += n; }
@@ -336,19 +323,6 @@ extern "C" int qtts_dev_put_tensor(qtts_dev_t *dv, const char *cname, const void
     return 0;
 }
 
-// CU masks of the decode (codec = false) and codec streams: style 0 gives the
-// codec the top codec_cus CU indices, style 1 every (ncu / codec_cus)-th CU.
-static void cu_masks(const qtts_dev *dv, bool codec, std::vector<uint32_t> &m) {
-    int ncu = 256;
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv->device);
-    const int n = std::min(dv->codec_cus, ncu - 1), stride = std::max(1, ncu / std::max(1, n));
-    m.assign((ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i) {
-        const bool c = dv->cu_mask_style == 1 ? (i % stride == stride - 1 && i / stride < n) : i >= ncu - n;
-        if (c == codec) m[i >> 5] |= 1u << (i & 31);
-    }
-}
-
 extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     if (hipSetDevice(device) != hipSuccess) {
         fprintf(stderr, "qtts: cannot select HIP device %d\n", device);
@@ -357,52 +331,19 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     qtts_dev *dv = new qtts_dev();
     dv->d = *dims;
     dv->device = device;
-    // QTTS_HIP_CODEC_CUS=N (opt-in, with the overlapped codec): the decode
-    // stream and the codec stream get disjoint CU masks (N CUs for the codec),
-    // so a long codec workgroup never holds a CU a decode kernel waits for.
-    {
-        const char *cc = getenv("QTTS_HIP_CODEC_CUS");
-        const char *cs = getenv("QTTS_HIP_CU_MASK_STYLE");
-        dv->codec_cus = cc ? atoi(cc) : 0;
-        dv->cu_mask_style = cs ? atoi(cs) : 0;
-    }
-    if (dv->codec_cus > 0) {
-        std::vector<uint32_t> m;
-        cu_masks(dv, false, m);
-        if (hipExtStreamCreateWithCUMask(&dv->st, (uint32_t)m.size(), m.data()) != hipSuccess) {
-            delete dv;
-            return nullptr;
-        }
-    } else if (hipStreamCreateWithFlags(&dv->st, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&dv->st, hipStreamNonBlocking) != hipSuccess) {
         delete dv;
         return nullptr;
     }
     dv->tl.resize(dims->L);
     dv->sl.resize(dims->Ls);
-    // GEMV-tail fusions (attention into QKV, sampler into the logit head) are
-    // correct but measured slower than separate kernels on MI355X (the per-kv-
-    // head ticket serialises 64 cross-XCD atomics; profiles/r01g): opt-in.
-    const char *nf = getenv("QTTS_HIP_FUSE");
-    dv->fuse_attn = nf && atoi(nf);
-    const char *ns = getenv("QTTS_HIP_FUSE_ST");
-    dv->fuse_st = ns && atoi(ns);
-    const char *nm = getenv("QTTS_HIP_NO_MFMA");
-    dv->use_mfma = !(nm && atoi(nm));
-    const char *ap = getenv("QTTS_HIP_ATT_PRO");
-    dv->att_pro = ap && atoi(ap);
+    // debug switches: QTTS_HIP_BSPLIT=0 batch O / down
+    // projections without split-K; QTTS_HIP_ATTN_O=0 sub-talker attention and
+    // O projection as two kernels
     const char *bs = getenv("QTTS_HIP_BSPLIT");
     dv->bsplit = !(bs && !atoi(bs));
-    if (const char *e = getenv("QTTS_HIP_PF_O")) dv->pf_o = atoi(e);
-    if (const char *e = getenv("QTTS_HIP_PF_GU")) dv->pf_gu_mb = atoi(e);
-    if (const char *e = getenv("QTTS_HIP_PF_WG")) dv->pf_wg = atoi(e);
-    const char *aot = getenv("QTTS_HIP_ATTN_O_TALKER");
-    if (aot) dv->attn_o_tmax = atoi(aot);
-    const char *aor = getenv("QTTS_HIP_ATTN_O_RPS");
-    if (aor) dv->attn_o_rps = atoi(aor);
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
-    const char *aw = getenv("QTTS_HIP_ATT_PRO_WG");
-    if (aw && atoi(aw) > 0) dv->att_pro_wg = atoi(aw);
     codec_init(&dv->codec, dims, dv->st);
     return dv;
 }
@@ -415,6 +356,7 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
     codec_destroy(&dv->codec);
     if (dv->cst) hipStreamSynchronize(dv->cst);
     if (dv->cwav) hipFree(dv->cwav);
+    if (dv->push_codes) hipFree(dv->push_codes);
     if (dv->cev) hipEventDestroy(dv->cev);
     if (dv->cst) hipStreamDestroy(dv->cst);
     for (void *p : dv->wallocs) hipFree(p);
@@ -512,7 +454,6 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(x_st, float, B * d.Hs);
     A(x_st2, float, B * d.Hs);
     A(x_tk2, float, B * d.H);
-    A(pf_sink, unsigned, 16);
     A(bpo, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(bpd, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(opart, float, (size_t)B * ((size_t)d.KVs * d.Hs > (size_t)d.KV * d.H ? (size_t)d.KVs * d.Hs : (size_t)d.KV * d.H));
@@ -555,8 +496,6 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         A(att_part, float, B * d.KV * dv->att_nsplit * (gph * d.HD + 2 * gph));
         const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
         A(att_cnt, int, B * kvmax);
-        A(samp_cnt, int, 16);
-        CK(hipMemsetAsync(dv->samp_cnt, 0, 16 * sizeof(int), dv->st));
         CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
     }
 #undef A
@@ -634,19 +573,13 @@ static int pgemv(qtts_dev *dv, const GemvArgs &a, int kind) {
     ProfScope ps(dv, kind, gemv_bytes(a));
     return qtts_gemv(a, dv->st);
 }
-// O projection with the sub-talker attention as its prologue (k_gemv.hip):
-// algorithmic bytes add the K / V rows of the live positions once.
-static int pgemv_att(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
-    ProfScope ps(dv, kind, gemv_bytes(a) + 2.0 * (t.pos_const + 1) * t.KV * t.HD * 4);
-    return qtts_gemv_att(a, t, dv->att_pro_wg, dv->st) == 0 ? 0 : -1;
-}
 // Multi-row projection over `rows` activation rows (prefill, text
 // projection): > 64 rows in one matrix-core launch (64-row chunks on its
 // grid.y), else the matrix-core kernel / batch GEMV / GEMV in chunks of 64 /
 // 16.  Row r of x / y / ids is at r*ldx / r*ldy / r*ids_bstride.
 static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
     const int xs = a.ldx, ys = a.ldy;
-    if (rows > 64 && dv->use_mfma && (!a.norm_w || rows <= dv->pinv_cap)) {
+    if (rows > 64 && (!a.norm_w || rows <= dv->pinv_cap)) {
         GemvArgs c = a;
         c.nb = rows;
         const int rc = qtts_mgemm(c, dv->pinv, dv->st);
@@ -663,8 +596,8 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
         // <= 16 rows (a custom-voice prompt): the batch decode kernel (k_gemvm,
         // x split once per workgroup, ~1 round over the CUs) streams the
         // weights faster than the 64-row prefill GEMM
-        if (nr >= 2 && nr <= 16 && dv->use_mfma) rc = qtts_gemvm(c, dv->st);
-        if (rc == 1 && nr >= 2 && dv->use_mfma) rc = qtts_mgemm(c, dv->pinv, dv->st);
+        if (nr >= 2 && nr <= 16) rc = qtts_gemvm(c, dv->st);
+        if (rc == 1 && nr >= 2) rc = qtts_mgemm(c, dv->pinv, dv->st);
         if (rc < 0) return -1;
         if (rc == 1) {
             nr = nr < 16 ? nr : 16;
@@ -705,18 +638,8 @@ static int build_proj_tables(qtts_dev *dv) {
     return 0;
 }
 
-// QKV projection + decode attention: one fused kernel at batch 1 (the
-// attention runs as the GEMV's tail, k_gemv.hip), else two launches.
+// QKV projection, then the decode attention
 static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
-    if (dv->nrun == 1 && (t.S <= 16 ? dv->fuse_st : dv->fuse_attn)) {
-        int rc;
-        {
-            ProfScope ps(dv, kind, gemv_bytes(a));
-            rc = qtts_gemv_qkv_attn(a, t, dv->st);
-            if (rc == 1) ps.cancel();
-        }
-        if (rc != 1) return rc;
-    }
     CKI(pgemv(dv, a, kind));
     ProfScope ps(dv, PK_ATTN, 0);
     return qtts_attention(t, dv->st);
@@ -766,46 +689,16 @@ static int talker_layers(qtts_dev *dv) {
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
         t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
-        {   // next GEMVs' weights into the Infinity Cache while attention runs
-            const size_t gu = (size_t)2 * d.I * d.H * 2, gpf = (size_t)dv->pf_gu_mb << 20;
-            t.pf0 = ly.wo; t.pf0_bytes = dv->pf_o ? (size_t)d.H * AD * 2 : 0;
-            t.pf1 = ly.wgu; t.pf1_bytes = gpf < gu ? gpf : gu;
-            const int ch = qtts_attn_keys_per_split(d.HD), ns = (dv->S + ch - 1) / ch;
-            t.pf_z = (dv->pf_wg + d.KV * ns - 1) / (d.KV * ns);
-            t.pf_sink = dv->pf_sink;
-        }
-        // batch 1, small key capacity: attention + O by kv head in one launch
-        // (k_attn_o_dec), per-head partials summed in the gate|up prologue
-        bool fused_o = false;
-        if (nb == 1 && dv->S <= dv->attn_o_tmax && !dv->fuse_attn) {
-            CKI(pgemv(dv, a, PK_GEMV_TALKER));
-            ProfScope ps(dv, PK_ATTN, (double)d.H * AD * 2);
-            const int rc = qtts_attn_o_dec(t, ly.wo, d.H, dv->opart, dv->attn_o_rps, st);
-            if (rc < 0) return -1;
-            if (rc == 1) {
-                ps.cancel();
-                { ProfScope pa(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
-                CKI(pgemv(dv, gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID), PK_GEMV_TALKER));
-            } else {
-                fused_o = true;
-            }
-        } else {
-            CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
-            if (pend) { std::swap(xa, xb); pend = nullptr; }
-            GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
-            if (kzo) split_out(dv, o, dv->bpo, kzo);
-            CKI(pgemv(dv, o, PK_GEMV_TALKER));
-        }
+        CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
+        if (pend) { std::swap(xa, xb); pend = nullptr; }
+        GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
+        if (kzo) split_out(dv, o, dv->bpo, kzo);
+        CKI(pgemv(dv, o, PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
-        if (fused_o) {
-            a.xadd = dv->opart; a.n_xadd = d.KV; a.ld_xadd = d.H;
-            a.xcopy = xb; a.ldxc = d.H; a.xcopy_normed = 0;
-        } else if (kzo) {
-            add_in(a, dv->bpo, kzo, d.H, nb, xb);
-        }
+        if (kzo) add_in(a, dv->bpo, kzo, d.H, nb, xb);
         CKI(pgemv(dv, a, PK_GEMV_TALKER));
-        if (fused_o || kzo) std::swap(xa, xb);
+        if (kzo) std::swap(xa, xb);
         GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
         if (kzd) { split_out(dv, dn, dv->bpd, kzd); pend = dv->bpd; npend = kzd; }
         CKI(pgemv(dv, dn, PK_GEMV_TALKER));
@@ -814,19 +707,8 @@ static int talker_layers(qtts_dev *dv) {
     return 0;
 }
 
-// Logit head + sampler: one fused kernel at batch 1 when the sampling
-// parameters take the register fast path (the draw runs as the GEMV's tail),
-// else two launches.
+// logit head, then the sampler
 static int head_sample(qtts_dev *dv, const GemvArgs &a, const SampArgs &s, int kind) {
-    if (dv->nrun == 1 && dv->fuse_attn) {
-        int rc;
-        {
-            ProfScope ps(dv, kind, gemv_bytes(a));
-            rc = qtts_gemv_sample(a, s, dv->samp_cnt, dv->st);
-            if (rc == 1) ps.cancel();
-        }
-        if (rc != 1) return rc;
-    }
     CKI(pgemv(dv, a, kind));
     ProfScope ps(dv, PK_SAMPLE, 0);
     return qtts_sample(s, dv->st);
@@ -921,7 +803,7 @@ static int subtalker(qtts_dev *dv) {
             // (batch 1 only: at batch 8 / 16 the per-row recompute measured slower than
             // the separate attention + split-K O projection, 98 vs 107 / 132 vs 155
             // audio-s/s, profiles/r01av_bench_batch_attn_o.txt)
-            if (dv->attn_o && nb == 1 && !dv->att_pro && !dv->fuse_st) {
+            if (dv->attn_o && nb == 1) {
                 CKI(pgemv(dv, a, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 ProfScope ps(dv, PK_ATTN, (double)d.Hs * AD * 2);
@@ -936,10 +818,6 @@ static int subtalker(qtts_dev *dv) {
                 } else {
                     fused_o = true;
                 }
-            } else if (dv->att_pro && nb == 1 && att_pro_ok(t, AD)) {
-                // q|k|v rows, then attention (as the prologue) + O projection + residual
-                CKI(pgemv(dv, a, PK_GEMV_SUB));
-                CKI(pgemv_att(dv, o, t, PK_GEMV_SUB));
             } else {
                 CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
@@ -1246,15 +1124,22 @@ extern "C" int qtts_dev_codec_stream_push_slot(qtts_dev_t *dv, int b, int frame0
 }
 
 extern "C" int qtts_dev_codec_stream_push_host(qtts_dev_t *dv, const int *codes, int T, float *host_out) {
-    if (!dv || T < 1) return -1;
+    if (!dv || !codes || T < 1) return -1;
     hipSetDevice(dv->device);
-    int *dc = nullptr;
-    if (hipMalloc(&dc, (size_t)T * dv->d.cq * 4) != hipSuccess) return -1;
-    int r = -1;
-    if (hipMemcpy(dc, codes, (size_t)T * dv->d.cq * 4, hipMemcpyHostToDevice) == hipSuccess)
-        r = codec_stream_push(&dv->codec, dc, dv->d.cq, T, host_out);
-    hipFree(dc);
-    return r;
+    const size_t n = (size_t)T * dv->d.cq;
+    if (n > dv->push_cap) {   // persistent staging buffer: no allocation per push
+        CK(hipStreamSynchronize(dv->st));
+        if (dv->push_codes) CK(hipFree(dv->push_codes));
+        dv->push_codes = nullptr;
+        dv->push_cap = 0;
+        const size_t cap = n < 4096 ? 4096 : n;
+        CK(hipMalloc(&dv->push_codes, cap * 4));
+        dv->push_cap = cap;
+    }
+    // ordered on the codec's stream before the push reads it; the synchronous
+    // push waits for the stream before returning, so the host buffer may be reused
+    CK(hipMemcpyAsync(dv->push_codes, codes, n * 4, hipMemcpyHostToDevice, dv->codec.st));
+    return codec_stream_push(&dv->codec, dv->push_codes, dv->d.cq, T, host_out);
 }
 
 // ----------------------------------------------------------------- codec overlapped with the decode
@@ -1268,13 +1153,7 @@ extern "C" int qtts_dev_codec_async_begin(qtts_dev_t *dv, int max_frames) {
     if (!dv->cst) {
         int lo = 0, hi = 0;
         CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        if (dv->codec_cus > 0) {
-            std::vector<uint32_t> m;
-            cu_masks(dv, true, m);
-            CK(hipExtStreamCreateWithCUMask(&dv->cst, (uint32_t)m.size(), m.data()));
-        } else {
-            CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
-        }
+        CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
         CK(hipEventCreateWithFlags(&dv->cev, hipEventDisableTiming));
     }
     const size_t need = (size_t)max_frames * 1920;

@@ -577,29 +577,11 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
         }
     }
-    /* QWEN_TTS_HIP_OVERLAP=1 (one utterance, not streamed): decode the codec
-     * chunk by chunk on a second stream while the frames continue (exact
-     * streaming decode).  Off by default: sharing the CUs slowed the latency-
-     * bound decode by more than the codec time it hides (profiles/r01g_envsweep.txt). */
-    const char *ov_env = getenv("QWEN_TTS_HIP_OVERLAP");
-    const int overlap = !stream && !vcs && nb == 1 && ov_env && atoi(ov_env);
-    const int ov_chunk = 16;
-    int ov_done = 0;
-    if (overlap && qtts_dev_codec_async_begin(dev, max_tokens) != 0) {
-        free(stopped); free(ngen); free(sstep); goto out;
-    }
     double t_gen = now_ms();
     const int poll_every = fixed > 0 ? 0 : 8;
     int step = 0;
     for (; step < max_tokens; step++) {
         if (qtts_dev_frame(dev, step) != 0) { free(sbuf); free(stopped); free(ngen); free(sstep); goto out; }
-        /* fixed length: every enqueued frame stores a code row */
-        if (overlap && fixed > 0 && step + 1 - ov_done >= ov_chunk) {
-            if (qtts_dev_codec_async_push(dev, 0, ov_done, step + 1 - ov_done) < 0) {
-                free(stopped); free(ngen); free(sstep); goto out;
-            }
-            ov_done = step + 1;
-        }
         if (step == 0) {
             qtts_dev_poll(dev, NULL, NULL, NULL);
             ctx->perf_first_frame_ms = now_ms() - t_start;
@@ -618,13 +600,6 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
                 if (streamed == 0) ctx->perf_first_packet_ms = now_ms() - t_start;
                 streamed = ngen[0];
             }
-            /* EOS mode: the polled count is what exists */
-            if (overlap && fixed == 0 && ngen[0] - ov_done >= ov_chunk) {
-                if (qtts_dev_codec_async_push(dev, 0, ov_done, ngen[0] - ov_done) < 0) {
-                    free(stopped); free(ngen); free(sstep); goto out;
-                }
-                ov_done = ngen[0];
-            }
             int all = 1;
             for (int b = 0; b < nb; b++) all &= stopped[b];
             if (qwen_tts_verbose >= 1 && ngen[0] > 0 && ngen[0] % 10 < poll_every)
@@ -642,12 +617,6 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
         if (stream->cb) stream->cb(sbuf + (size_t)streamed * 1920, n, stream->user);
         if (streamed == 0) ctx->perf_first_packet_ms = now_ms() - t_start;
         streamed = ngen[0];
-    }
-    if (overlap && ngen[0] > ov_done) {
-        if (qtts_dev_codec_async_push(dev, 0, ov_done, ngen[0] - ov_done) < 0) {
-            free(stopped); free(ngen); free(sstep); goto out;
-        }
-        ov_done = ngen[0];
     }
     double t_gen_done = now_ms();
     ctx->perf_talker_ms = t_gen_done - t_gen - t_stream;
@@ -677,18 +646,6 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
         samples[0] = streamed * 1920;
         if (streamed <= 0) { free(sbuf); audio[0] = NULL; rc = -1; }
         ctx->perf_codec_ms = t_stream;
-    } else if (overlap) {   /* only the tail of the overlapped codec is left to wait for */
-        audio[0] = NULL;
-        samples[0] = 0;
-        if (ngen[0] > 0 && (audio[0] = (float *)malloc((size_t)ngen[0] * 1920 * sizeof(float))) != NULL)
-            samples[0] = qtts_dev_codec_async_end(dev, audio[0], ngen[0]);
-        if (!audio[0] || samples[0] <= 0) {
-            free(audio[0]);
-            audio[0] = NULL;
-            samples[0] = 0;
-            rc = -1;
-        }
-        ctx->perf_codec_ms = now_ms() - t_codec;
     } else {
         for (int b = 0; b < nb; b++) {
             audio[b] = NULL;

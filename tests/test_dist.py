@@ -56,3 +56,74 @@ def test_partition_and_reductions_gloo(ws):
 def test_single_rank_is_identity():
     assert bench.reduce_max(1, 3.5) == 3.5 and bench.reduce_sum(1, 2.0) == 2.0
     assert bench.rank_prompt_seeds(0, 2) == [1234, 1235]
+
+
+def _gen_worker(rank, ws, port, tiny_dir, q):
+    """One rank of the data-parallel bench on CPU: its own prompts (bench's
+    static partition), decoded by the oracle (the CPU checker stands in for
+    the HIP path, which needs the GPU), then bench's per-rank gather."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from oracle_py import Oracle, GREEDY
+    from qtts_io import lookup_ids
+    from synth_model import prompt_ids
+    w, r, _ = bench.dist_setup()
+    o = Oracle(tiny_dir)
+    s, l = lookup_ids(o.cfg, "aiden", "english")
+    codes = []
+    for sd in bench.rank_prompt_seeds(r, 2):
+        c, _ = o.generate_codes(prompt_ids("p128", seed=sd), s, l, max_tokens=4096, fixed=2, seed=42, **GREEDY)
+        codes.append(c.tolist())
+    o.close()
+    recs = bench.gather_ranks(w, dict(rank=r, samples=2 * 2 * 1920, frames=4, wall_ms=10.0 * (r + 1), codes=codes))
+    q.put((r, recs))
+    dist.destroy_process_group()
+
+
+def test_two_rank_generate_gather_gloo(tiny_dir):
+    """world_size 2 on gloo: each rank decodes its own utterances, bench's
+    gather gives every rank every record, and each rank's codes equal a
+    single-process decode of the same prompts (ranks share nothing)."""
+    from oracle_py import Oracle, GREEDY
+    from qtts_io import lookup_ids
+    from synth_model import prompt_ids
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gen_worker, args=(r, ws, port, tiny_dir, q)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(ws))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1] and [x["rank"] for x in res[0]] == [0, 1]
+    o = Oracle(tiny_dir)
+    s, l = lookup_ids(o.cfg, "aiden", "english")
+    for rec in res[0]:
+        for sd, got in zip(bench.rank_prompt_seeds(rec["rank"], 2), rec["codes"]):
+            want, _ = o.generate_codes(prompt_ids("p128", seed=sd), s, l, max_tokens=4096, fixed=2, seed=42, **GREEDY)
+            assert got == want.tolist()
+    o.close()
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_self_launch(gpu):
+    """`bench.py --gpus 2` starts its own 2 ranks (no external launcher); on a
+    one-GPU box both share it over gloo.  The line reports n_gpus 2 and one
+    record per rank."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QTTS_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--preset", "tiny",
+                        "--frames", "4", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-profile"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 2
+    assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
+    assert all(x["samples"] == 4 * 1920 for x in line["ranks"])

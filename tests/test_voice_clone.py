@@ -157,30 +157,19 @@ def test_cli_voice_clone_flags(tiny_dir, tts_tiny, oracle, ns):
         assert open(os.path.join(d, "cli.wav"), "rb").read() == open(api, "rb").read()
 
 
-@pytest.fixture(scope="module")
-def tts_stream(gpu, tiny_dir):
-    # own ctx, as test_gpu_model's streaming tests: a streaming generate on a
-    # ctx whose codec stream was driven directly (qwen_tts_codec_stream_*,
-    # test_codec_stream_equals_full_decode) delivers no chunks -- open issue,
-    # DESIGN.md §7
-    import qtts
-    m = qtts.QwenTTS(tiny_dir)
-    yield m
-    m.close()
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("T", [0, 7, 63])
-def test_voice_clone_stream(tts_stream, oracle, T):
+def test_voice_clone_stream(tts_tiny, oracle, T):
     """Streaming voice clone: same codes as the oracle, chunks concatenate to
     the reference ++ generated decode from the exact frame boundary T * 1920
-    (the reference frames are pushed through the streaming codec first)."""
+    (the reference frames are pushed through the streaming codec first).
+    Runs on the session ctx after test_gpu_model's direct codec_stream_* use
+    and the batch tests above (which re-allocate the decode state)."""
     from test_gpu_model import audio_close
     codes, sv = _inputs(oracle, max(T, 1), seed=11 + T, spk=True)
     rc = codes if T else None
     ids = prompt_ids("short")
     _, lang = lookup_ids(oracle.cfg, "aiden", "english")
-    tts_tiny = tts_stream
     tts_tiny.set_params(max_tokens=4096, fixed=6, seed=42, **DEFAULT)
     chunks = []
     a = tts_tiny.generate_voice_clone_stream(ids, REF_IDS if T else None, rc, sv, "english", 0, chunk_frames=2,
@@ -192,3 +181,46 @@ def test_voice_clone_stream(tts_stream, oracle, T):
     np.testing.assert_array_equal(tts_tiny.last_codes(), want)
     full = oracle.codec_decode(np.concatenate([codes, want]) if T else want)
     audio_close(a, full[T * 1920:])
+    # the non-streamed call cuts where the Python reference does,
+    # int(T / tot * samples) (qwen3_tts_model.py:612-630), which is one sample
+    # before the frame boundary for some (T, tot): the streamed chunks start at
+    # T * 1920 because tot is unknown while streaming
+    b = tts_tiny.generate_voice_clone(ids, REF_IDS if T else None, rc, sv, "english", 0)
+    tot = T + len(want)
+    off = T * 1920 - int(T / tot * (tot * 1920))   # the C host's (double) ref / tot * samples
+    assert off in (0, 1) and len(b) == len(a) + off
+    audio_close(b[off:], a)
+
+
+@pytest.mark.gpu
+def test_stream_after_state_realloc_same_ctx(tts_tiny, tiny_dir, oracle):
+    """Regression (round-1 use-after-free): a codec stream is started, then a
+    batch call re-allocates the decode state (and with it the codec GEMMs'
+    split-K workspace), then a streaming voice clone reuses the stream's
+    buffers on the same ctx.  Its chunks must be there and bit-equal to the
+    same call on a fresh ctx."""
+    import qtts
+    codes, sv = _inputs(oracle, 7, seed=21, spk=True)
+    ids = prompt_ids("short")
+    tts_tiny.codec_stream([codes[:3], codes[3:]])                       # stream begun directly
+    tts_tiny.set_params(max_tokens=4096, fixed=4, seed=42, **DEFAULT)
+    rc, _ = tts_tiny.generate_voice_clone_batch([ids, ids], [REF_IDS, REF_IDS], [codes, codes], [sv, sv],
+                                                ["english"] * 2)      # nb = 2: state re-allocated
+    assert rc == 0
+
+    def run(m):
+        m.set_params(max_tokens=4096, fixed=6, seed=42, **DEFAULT)
+        ch = []
+        a = m.generate_voice_clone_stream(ids, REF_IDS, codes, sv, "english", 0, chunk_frames=2,
+                                          on_chunk=ch.append)
+        return a, ch, m.last_codes()
+
+    a, ch, c = run(tts_tiny)
+    assert a is not None and ch and np.array_equal(np.concatenate(ch), a)
+    fresh = qtts.QwenTTS(tiny_dir)
+    try:
+        a2, ch2, c2 = run(fresh)
+    finally:
+        fresh.close()
+    np.testing.assert_array_equal(c, c2)
+    np.testing.assert_array_equal(a, a2)

@@ -1,0 +1,254 @@
+// mb_persist.hip - micro-benchmark (development tool, not product code): the
+// sub-talker layer chain (1.7B / 0.6B shapes: Hs 1024, q|k|v 4096, attention
+// 2048, gate|up 6144 -> 3072, down 1024; bf16 weights resident in the
+// Infinity Cache) as
+//   (a) a HIP graph of one weight-streaming GEMV kernel per op, and
+//   (b) ONE persistent launch (one workgroup per CU) whose ops hand their
+//       output vectors to every workgroup through 8-byte {epoch, value}
+//       granules (cdna_hip_programming.md Guideline 16, R2), each workgroup
+//       issuing its next weight slice into registers BEFORE it waits for the
+//       vector (the prefetch a kernel boundary cannot give).
+// Also the boundary floor: a graph of empty kernels, and of kernels that only
+// read a 4 KB vector (the r01c "3.48 us per kernel" probe's body).
+//
+//   hipcc -O3 --offload-arch=gfx950 tools/mb_persist.hip -o tools/mb_persist && tools/mb_persist
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s failed: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+struct Op { const uint16_t *W; int R, C; int in, out; };   // in/out: vector buffer ids
+constexpr int NBUF = 3, VMAX = 8192;
+
+__device__ __forceinline__ float dot8(const v4u &w, const float *x) {
+    float s = 0.f;
+    s = fmaf(__uint_as_float(w.x << 16), x[0], s); s = fmaf(__uint_as_float(w.x & 0xFFFF0000u), x[1], s);
+    s = fmaf(__uint_as_float(w.y << 16), x[2], s); s = fmaf(__uint_as_float(w.y & 0xFFFF0000u), x[3], s);
+    s = fmaf(__uint_as_float(w.z << 16), x[4], s); s = fmaf(__uint_as_float(w.z & 0xFFFF0000u), x[5], s);
+    s = fmaf(__uint_as_float(w.w << 16), x[6], s); s = fmaf(__uint_as_float(w.w & 0xFFFF0000u), x[7], s);
+    return s;
+}
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// rows of workgroup `wg` for op o: [wg*rpw, +rpw); wave w takes rows w, w+4, ..
+template <int RW, int NV>
+__device__ __forceinline__ void load_w(const Op &o, int wg, v4u (&w)[24]) {
+    const int rpw = o.R / gridDim.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const int r = wg * rpw + wv + 4 * i;
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            w[i * NV + k] = *(reinterpret_cast<const v4u *>(o.W + (size_t)r * o.C) + lane + 64 * k);
+    }
+}
+template <int RW, int NV>
+__device__ __forceinline__ void compute(const Op &o, int wg, const v4u (&w)[24], const float *xs, float *outv,
+                                        uint64_t *outg, unsigned ep) {
+    const int rpw = o.R / gridDim.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) s += dot8(w[i * NV + k], xs + 8 * (lane + 64 * k));
+        s = wsum(s);
+        const int r = wg * rpw + wv + 4 * i;
+        if (lane == 0) {
+            if (outg) __hip_atomic_store(outg + r, ((uint64_t)ep << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            else outv[r] = s;
+        }
+    }
+}
+#define DISPATCH(o, FN, ...)                                                                              \
+    do {                                                                                                  \
+        const int rw_ = (o).R / gridDim.x / 4, nv_ = (o).C / 512;                                          \
+        if (rw_ == 4 && nv_ == 2) FN<4, 2>(__VA_ARGS__);                                                   \
+        else if (rw_ == 1 && nv_ == 4) FN<1, 4>(__VA_ARGS__);                                              \
+        else if (rw_ == 6 && nv_ == 2) FN<6, 2>(__VA_ARGS__);                                              \
+        else if (rw_ == 1 && nv_ == 6) FN<1, 6>(__VA_ARGS__);                                              \
+        else if (rw_ == 2 && nv_ == 2) FN<2, 2>(__VA_ARGS__);                                              \
+        else if (rw_ == 3 && nv_ == 2) FN<3, 2>(__VA_ARGS__);                                              \
+        else if (rw_ == 2 && nv_ == 4) FN<2, 4>(__VA_ARGS__);                                              \
+        else if (rw_ == 2 && nv_ == 6) FN<2, 6>(__VA_ARGS__);                                              \
+        else if (rw_ == 8 && nv_ == 2) FN<8, 2>(__VA_ARGS__);                                              \
+        else if (rw_ == 12 && nv_ == 2) FN<12, 2>(__VA_ARGS__);                                            \
+    } while (0)
+
+// (a) one op per kernel: the input vector read once per workgroup into LDS
+__global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out) {
+    __shared__ __attribute__((aligned(16))) float xs[VMAX];
+    v4u w[24];
+    DISPATCH(o, load_w, o, blockIdx.x, w);
+    for (int c = 4 * threadIdx.x; c < o.C; c += 1024)
+        *reinterpret_cast<float4 *>(xs + c) = *reinterpret_cast<const float4 *>(in + c);
+    __syncthreads();
+    DISPATCH(o, compute, o, blockIdx.x, w, xs, out, nullptr, 0u);
+}
+
+// (b) persistent chain
+__global__ __launch_bounds__(256) void k_chain(const Op *ops, int nops, const float *x0, uint64_t *gbuf,
+                                               unsigned base, unsigned *err) {
+    __shared__ __attribute__((aligned(16))) float xs[VMAX];
+    __shared__ int bad;
+    v4u w[24];
+    for (int c = threadIdx.x; c < ops[0].C; c += 256) xs[c] = x0[c];
+    __syncthreads();
+    for (int i = 0; i < nops; ++i) {
+        const Op o = ops[i];
+        DISPATCH(o, load_w, o, blockIdx.x, w);      // next weights in flight before the wait
+        if (i > 0) {
+            const uint64_t *g = gbuf + (size_t)o.in * VMAX;
+            const unsigned ep = base + i;           // epoch of op i-1's output
+            if (threadIdx.x == 0) bad = 0;
+            for (int c = threadIdx.x; c < o.C; c += 256) {
+                uint64_t v;
+                unsigned spins = 0;
+                while (((v = __hip_atomic_load(g + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != ep) {
+                    if (++spins > (1u << 22)) { bad = 1; break; }
+                }
+                xs[c] = __uint_as_float((unsigned)v);
+            }
+            __syncthreads();
+            if (bad) { if (threadIdx.x == 0) atomicAdd(err, 1u); return; }
+        }
+        DISPATCH(o, compute, o, blockIdx.x, w, xs, nullptr, gbuf + (size_t)o.out * VMAX, base + i + 1);
+        __syncthreads();
+    }
+}
+
+__global__ void k_empty(int) {}
+__global__ __launch_bounds__(256) void k_read4k(const float *in, float *out) {
+    __shared__ float red[4];
+    float4 v = reinterpret_cast<const float4 *>(in)[threadIdx.x];
+    float s = wsum(v.x + v.y + v.z + v.w);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+struct Big { float p[56]; };   // a 224-B kernarg, about GemvArgs' size
+__global__ void k_bigarg(Big b) { if (b.p[0] == 12345.f) b.p[1] = 0; }
+
+int main() {
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timed_graph = [&](auto rec, int reps) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        rec();
+        CK(hipStreamEndCapture(st, &g));
+        CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        CK(hipGraphLaunch(ge, st));
+        CK(hipStreamSynchronize(st));
+        CK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, st));
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipGraphExecDestroy(ge));
+        CK(hipGraphDestroy(g));
+        return ms / reps;
+    };
+    float *va, *vb;
+    CK(hipMalloc(&va, VMAX * 4 * NBUF));
+    CK(hipMalloc(&vb, VMAX * 4 * NBUF));
+    CK(hipMemset(va, 0, VMAX * 4 * NBUF));
+    CK(hipMemset(vb, 0, VMAX * 4 * NBUF));
+    // ---- boundary floor ----
+    for (int grid : {256, 512}) {
+        float t = timed_graph([&] { for (int i = 0; i < 200; ++i) hipLaunchKernelGGL(k_empty, dim3(grid), dim3(256), 0, st, i); }, 10);
+        printf("graph of empty kernels, grid %d: %.2f us per kernel\n", grid, t * 1e3 / 200);
+        Big b{};
+        t = timed_graph([&] { for (int i = 0; i < 200; ++i) hipLaunchKernelGGL(k_bigarg, dim3(grid), dim3(256), 0, st, b); }, 10);
+        printf("graph of empty kernels with a 224-B kernarg, grid %d: %.2f us per kernel\n", grid, t * 1e3 / 200);
+        t = timed_graph([&] { for (int i = 0; i < 200; ++i) hipLaunchKernelGGL(k_read4k, dim3(grid), dim3(256), 0, st, (i & 1) ? vb : va, (i & 1) ? va : vb); }, 10);
+        printf("graph of 4-KB-read kernels (dependent), grid %d: %.2f us per kernel\n", grid, t * 1e3 / 200);
+    }
+    // ---- sub-talker layer chain ----
+    const int Hs = 1024, QKV = 4096, AD = 2048, I = 3072, L = 5;
+    std::vector<Op> ops;
+    size_t wtot = 0;
+    std::vector<uint16_t *> ws;
+    auto W = [&](int R, int C) {
+        uint16_t *p;
+        CK(hipMalloc(&p, (size_t)R * C * 2));
+        std::vector<uint16_t> h((size_t)R * C);
+        for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3c00 + (uint16_t)(i * 2654435761u >> 28);   // ~1/256.. values
+        CK(hipMemcpy(p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+        wtot += h.size() * 2;
+        ws.push_back(p);
+        return p;
+    };
+    for (int l = 0; l < L; ++l) {
+        ops.push_back({W(QKV, Hs), QKV, Hs, 0, 1});      // x -> q|k|v
+        ops.push_back({W(Hs, AD), Hs, AD, 1, 2});        // attention (first 2048 of q|k|v) -> O
+        ops.push_back({W(2 * I, Hs), 2 * I, Hs, 2, 1});  // x -> gate|up
+        ops.push_back({W(Hs, I), Hs, I, 1, 0});          // h -> down
+    }
+    printf("sub-talker chain: %d ops, %.1f MB of weights (Infinity-Cache resident)\n", (int)ops.size(), wtot / 1e6);
+    const int passes = 16;
+    for (int grid : {ncu, ncu / 2}) {
+        bool ok = true;
+        for (auto &o : ops) ok &= o.R % (grid * 4) == 0;
+        if (!ok) continue;
+        float *bufs[NBUF] = {va, va + VMAX, va + 2 * VMAX};
+        float t = timed_graph([&] {
+            for (int p = 0; p < passes; ++p)
+                for (auto &o : ops)
+                    hipLaunchKernelGGL(k_op, dim3(grid), dim3(256), 0, st, o, bufs[o.in], bufs[o.out]);
+        }, 20);
+        printf("graph, grid %d: %.2f us per layer (%.2f us per op kernel)\n", grid, t * 1e3 / (passes * L),
+               t * 1e3 / (passes * L * 4));
+        // persistent
+        std::vector<Op> all;
+        for (int p = 0; p < passes; ++p) all.insert(all.end(), ops.begin(), ops.end());
+        Op *dops;
+        uint64_t *gb;
+        unsigned *err;
+        CK(hipMalloc(&dops, all.size() * sizeof(Op)));
+        CK(hipMemcpy(dops, all.data(), all.size() * sizeof(Op), hipMemcpyHostToDevice));
+        CK(hipMalloc(&gb, (size_t)NBUF * VMAX * 8));
+        CK(hipMemset(gb, 0, (size_t)NBUF * VMAX * 8));
+        CK(hipMalloc(&err, 4));
+        CK(hipMemset(err, 0, 4));
+        unsigned base = 0;
+        const int nops = (int)all.size();
+        for (int r = 0; r < 3; ++r, base += nops + 2)
+            hipLaunchKernelGGL(k_chain, dim3(grid), dim3(256), 0, st, dops, nops, va, gb, base, err);
+        CK(hipStreamSynchronize(st));
+        const int reps = 20;
+        CK(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; ++r, base += nops + 2)
+            hipLaunchKernelGGL(k_chain, dim3(grid), dim3(256), 0, st, dops, nops, va, gb, base, err);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned herr = 0;
+        CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+        printf("persistent, grid %d: %.2f us per layer (%.2f us per op hand-off)%s\n", grid,
+               ms * 1e3 / reps / (passes * L), ms * 1e3 / reps / (passes * L * 4), herr ? "  [TIMEOUTS!]" : "");
+        CK(hipFree(dops));
+        CK(hipFree(gb));
+        CK(hipFree(err));
+    }
+    for (auto p : ws) CK(hipFree(p));
+    return 0;
+}
