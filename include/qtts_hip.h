@@ -147,6 +147,12 @@ int qtts_hip_rmsnorm_matvec_bf16(float *out_dev, const uint16_t *A_dev, const fl
  * (c/qwen_tts_kernels.c:27 + :95 per row) */
 int qtts_hip_decode_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_dev, const float *w_dev,
                                 float eps, int rows, int cols, int batch, void *stream);
+/* the batch-1 GEMV of the sub-talker chain (weights resident in the Infinity
+ * Cache, default cache policy): w_dev NULL: no norm; epi 0 store, 3 residual
+ * (out += A x), 4 SwiGLU over interleaved gate|up row quads (rows/2 outputs)
+ * (c/qwen_tts_kernels.c:27 + :95 + :213) */
+int qtts_hip_resident_matvec_bf16(float *out_dev, const uint16_t *A_dev, const float *x_dev, const float *w_dev,
+                                  float eps, int rows, int cols, int epi, void *stream);
 /* kernel_sample_top_k (c/qwen_tts_kernels.c:407) on `batch` logit rows; rng_bits
  * holds the float-bit xorshift state per row (updated in place). */
 int qtts_hip_sample_top_k(int *out_dev, const float *logits_dev, int vocab, int top_k, float top_p,

@@ -477,12 +477,15 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     const int slot = tid / LPS, sub = tid - slot * LPS;
     const int row = rb * RPW + slot, rowc = row < R ? row : R - 1;
     const int AD = t.NH * HD;
-    // the weight fragment first: row `row`, columns W2*kvh + 8*(sub + LPS*j)
+    // the weight fragment (row `row`, columns W2*kvh + 8*(sub + LPS*j)) is
+    // issued right behind the attention's own loads
     v4u wv[NJ];
     const bf16_t *wr = Wo + (size_t)rowc * AD + W2 * kvh + 8 * sub;
+    auto issue = [&]() {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
-    attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0);
+        for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
+    };
+    attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0, issue);
     __syncthreads();
     float acc = 0.f;
 #pragma unroll

@@ -324,9 +324,10 @@ __global__ __launch_bounds__(1024) void k_gemv1(GemvArgs a) {
     float *red = xs + C;          // [nslot]
     float *bred = red + nslot;    // [nthr / 64]
     G1Stream<U1, NT> ws(a, row, ks, ksn, sub);
-    ws.load(0);
 
-    // ---- prologue: x (fp32 row or gathered bf16 row) -> optional RMSNorm -> LDS
+    // ---- prologue: x (fp32 row or gathered bf16 row) -> optional RMSNorm -> LDS.
+    // The x and norm-weight loads go out BEFORE the first weight group: loads
+    // retire in issue order, so x behind U1 weight loads would wait for them.
     const bf16_t *trow = nullptr;
     const float *xrow = a.x;
     if (a.table || a.table_f32) {
@@ -337,33 +338,37 @@ __global__ __launch_bounds__(1024) void k_gemv1(GemvArgs a) {
         else xrow = a.table_f32 + off;
     }
     float4 xv[XV], wn[XV];
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int c = 4 * (tid + nthr * i);
+        const int cc = c < C ? c : C - 4;
+        if (trow) {
+            const uint2 t = *reinterpret_cast<const uint2 *>(trow + cc);
+            xv[i] = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
+                                __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
+        } else {
+            xv[i] = *reinterpret_cast<const float4 *>(xrow + cc);
+        }
+        if (a.norm_w) wn[i] = *reinterpret_cast<const float4 *>(a.norm_w + cc);
+    }
+    ws.load(0);
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const int c = 4 * (tid + nthr * i);
         const int cc = c < C ? c : C - 4;
-        float4 v;
-        if (trow) {
-            const uint2 t = *reinterpret_cast<const uint2 *>(trow + cc);
-            v = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
-                            __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
-        } else {
-            v = *reinterpret_cast<const float4 *>(xrow + cc);
-            if (a.xadd) {   // residual + the O projection's per-head partials, summed in head order
-                float4 sacc = *reinterpret_cast<const float4 *>(a.xadd + cc);
-                for (int p = 1; p < a.n_xadd; ++p) {
-                    const float4 t = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + cc);
-                    sacc.x += t.x; sacc.y += t.y; sacc.z += t.z; sacc.w += t.w;
-                }
-                v.x += sacc.x; v.y += sacc.y; v.z += sacc.z; v.w += sacc.w;
+        float4 v = xv[i];
+        if (!trow && a.xadd) {   // residual + the O projection's per-head partials, summed in head order
+            float4 sacc = *reinterpret_cast<const float4 *>(a.xadd + cc);
+            for (int p = 1; p < a.n_xadd; ++p) {
+                const float4 t = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + cc);
+                sacc.x += t.x; sacc.y += t.y; sacc.z += t.z; sacc.w += t.w;
             }
+            v.x += sacc.x; v.y += sacc.y; v.z += sacc.z; v.w += sacc.w;
         }
         if (c >= C) v = make_float4(0.f, 0.f, 0.f, 0.f);
         xv[i] = v;
-        if (a.norm_w) {
-            wn[i] = *reinterpret_cast<const float4 *>(a.norm_w + cc);
-            ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-        }
+        if (a.norm_w) ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
     float inv = 1.f;
     if (a.norm_w) {
@@ -441,6 +446,13 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     if (a.xadd && a.nb == 1 && !(a.C <= 8192 && a.ldx_ok1())) {
         fprintf(stderr, "qtts_gemv: xadd needs the batch-1 fast path (R=%d C=%d)\n", a.R, a.C);
         return -1;
+    }
+    if (a.nb == 1 && a.ksplit <= 0) {
+        static const int lean = [] { const char *e = getenv("QTTS_HIP_GEMVW"); return e ? atoi(e) : 1; }();
+        if (lean == 2 || (lean == 1 && !a.nt)) {
+            const int rc = qtts_gemvw(a, st);
+            if (rc != 1) return rc;
+        }
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
         int nthr = 256;

@@ -1,0 +1,204 @@
+// k_gemvw.hip - batch-1 GEMV for the latency-bound sub-talker chain (gfx950).
+//
+// y[r] = epilogue( sum_c W[r, c] * xin[c] ),  the role of kernel_matvec_bf16 /
+// kernel_swiglu_matvec_bf16 (K.c:95-149, :213-233) with the rms_norm and
+// residual passes around them (T.c:142-247), for matrices that stay resident
+// in the Infinity Cache (the sub-talker's 224 MB, read 16 times per frame).
+//
+// Why a second batch-1 GEMV: each sub-talker op moves only 4-12.6 MB, so its
+// time is the kernel boundary plus one dependent read of x plus the weight
+// latency, not bandwidth.  profiles/r02a_mb_persist.txt measures the floor:
+// an empty kernel 1.6 us, a kernel that only reads a 4 KB vector 2.0 us, and
+// this kernel's shape (whole weight slice in flight before x is read, one
+// wave per row, no LDS reduction) 4.2 us per op over the sub-talker chain,
+// against ~6 us for k_gemv1 (two workgroups per CU, KSPLIT partials through
+// LDS and a third barrier).  A persistent launch with 8-byte granule
+// hand-offs between the ops measured 5.1 us per op in the same benchmark:
+// the all-to-all vector exchange costs more than the boundary it removes.
+//
+// Mapping: one 256-thread workgroup per 4*RW rows (grid ~256 = one per CU);
+// wave w owns rows row0 + w + 4i (i < RW); lane l covers the 8-column chunks
+// l + 64k (k < NV), so C = 512 NV and every wave load is 1 KB contiguous.
+// The x loads are issued first, then all RW*NV 16-B weight loads of a lane;
+// the prologue (x or a gathered table row, + the O projection's per-head
+// partials, RMSNorm) overlaps the weights; one barrier publishes the
+// normalised x in LDS; each row is a dot of the lane's chunks in order + a
+// 6-step xor-shuffle sum.
+// SwiGLU rows come as interleaved gate|up quads (qtts_runtime.hip layout):
+// with 4 | row0 / 8 even RW, a wave's rows i = 2j, 2j+1 are the gate row and
+// its up row (r + 4), so the product is formed in registers.
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ float dot8w(const v4u &w, const float *x) {
+    const float4 x0 = *reinterpret_cast<const float4 *>(x);
+    const float4 x1 = *reinterpret_cast<const float4 *>(x + 4);
+    float s = 0.f;
+    s = fmaf(__uint_as_float(w.x << 16), x0.x, s); s = fmaf(__uint_as_float(w.x & 0xFFFF0000u), x0.y, s);
+    s = fmaf(__uint_as_float(w.y << 16), x0.z, s); s = fmaf(__uint_as_float(w.y & 0xFFFF0000u), x0.w, s);
+    s = fmaf(__uint_as_float(w.z << 16), x1.x, s); s = fmaf(__uint_as_float(w.z & 0xFFFF0000u), x1.y, s);
+    s = fmaf(__uint_as_float(w.w << 16), x1.z, s); s = fmaf(__uint_as_float(w.w & 0xFFFF0000u), x1.w, s);
+    return s;
+}
+
+// Dynamic LDS: [xs: C floats][red: 4 floats] (16-B aligned, Guideline 17).
+template <int RW, int NV, bool NT>
+__global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int C = 512 * NV, XQ = C / 1024 > 0 ? (C + 1023) / 1024 : 1;   // float4 of x per thread
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int row0 = blockIdx.x * 4 * RW;
+    float *xs = smem, *red = smem + C;
+
+    // 1. x (and the partials it adds) first: the weight loads issued after
+    //    them do not hold back the prologue (vmcnt retires loads in issue
+    //    order, so x issued behind 12 weight loads would wait for all of them)
+    const bf16_t *trow = nullptr;
+    const float *xrow = a.x;
+    if (a.table || a.table_f32) {
+        const int *ip = a.ids + a.ids_off;
+        if (a.row_sel) ip += (size_t)a.row_sel[0] * a.ids_rstride;
+        const size_t off = (size_t)(*ip) * C;
+        if (a.table) trow = a.table + off;
+        else xrow = a.table_f32 + off;
+    }
+    constexpr int PMAX = 8;   // partials held in registers (more: summed from memory below)
+    float4 xv[XQ], pv[XQ][PMAX], nwv[XQ];
+    const int np = a.xadd ? a.n_xadd : 0;
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+        const int c = 4 * (tid + 256 * q);
+        const int cc = c < C ? c : 0;
+        if (trow) {
+            const uint2 t = *reinterpret_cast<const uint2 *>(trow + cc);
+            xv[q] = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
+                                __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
+        } else {
+            xv[q] = *reinterpret_cast<const float4 *>(xrow + cc);
+        }
+#pragma unroll
+        for (int p = 0; p < PMAX; ++p)
+            if (p < np) pv[q][p] = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + cc);
+        if (a.norm_w) nwv[q] = *reinterpret_cast<const float4 *>(a.norm_w + cc);
+    }
+
+    // 2. the whole weight slice of this lane in flight
+    v4u wv[RW][NV];
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const v4u *p = reinterpret_cast<const v4u *>(a.W + (size_t)(row0 + w + 4 * i) * C) + lane;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            if constexpr (NT) wv[i][k] = __builtin_nontemporal_load(p + 64 * k);
+            else wv[i][k] = p[64 * k];
+        }
+    }
+
+    // 3. residual + partials summed in partial order, RMS statistic
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+        const int c = 4 * (tid + 256 * q);
+        float4 v = xv[q];
+        if (np > 0) {
+            float4 s = pv[q][0];
+#pragma unroll
+            for (int p = 1; p < PMAX; ++p)
+                if (p < np) { s.x += pv[q][p].x; s.y += pv[q][p].y; s.z += pv[q][p].z; s.w += pv[q][p].w; }
+            for (int p = PMAX; p < np; ++p) {
+                const float4 t = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + c);
+                s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+            }
+            v.x += s.x; v.y += s.y; v.z += s.z; v.w += s.w;
+        }
+        if (c >= C) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.norm_w) ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        xv[q] = v;
+    }
+    float inv = 1.f;
+    if (a.norm_w) {
+        ss = wave_sum(ss);
+        if (lane == 0) red[w] = ss;
+        __syncthreads();
+        inv = rms_inv(red[0] + red[1] + red[2] + red[3], C, a.eps);
+    }
+    const bool cp = a.xcopy && blockIdx.x == 0;
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+        const int c = 4 * (tid + 256 * q);
+        if (c < C) {
+            float4 v = xv[q];
+            if (cp && !a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + c) = v;
+            if (a.norm_w) {
+                const float4 nw = nwv[q];
+                v.x = v.x * inv * nw.x; v.y = v.y * inv * nw.y; v.z = v.z * inv * nw.z; v.w = v.w * inv * nw.w;
+            }
+            if (cp && a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + c) = v;
+            *reinterpret_cast<float4 *>(xs + c) = v;
+        }
+    }
+    __syncthreads();
+
+    // 4. one wave per row: the lane's chunks in order, then the wave sum
+    float acc[RW];
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) s += dot8w(wv[i][k], xs + 8 * (lane + 64 * k));
+        acc[i] = wave_sum(s);
+    }
+    if (lane != 0) return;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const int r = row0 + w + 4 * i;
+        const float v = acc[i];
+        switch (a.epi) {
+            case EPI_STORE: a.y[r] = v; break;
+            case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
+            case EPI_BIAS_SILU: {
+                const float z = v + a.bias[r];
+                a.y[r] = z / (1.0f + expf(-z));
+                break;
+            }
+            case EPI_RESID: a.y[r] += v; break;
+            case EPI_SWIGLU:
+                if ((i & 1) == 0 && i + 1 < RW) a.y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * acc[i + 1];
+                break;
+        }
+    }
+}
+
+}  // namespace
+
+// Returns 1 when the shape is not covered (the caller uses k_gemv1), 0 ok,
+// -1 on a launch error.  Covers nb == 1, C in {512, 1024, ..., 3072},
+// R a multiple of 1024 (RW = R / 1024 rows per wave, grid R / (4 RW) = 256
+// workgroups), RW * NV <= 16 registers' worth of loads per lane.
+int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
+    if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart || !a.ldx_ok1()) return 1;
+    const int NV = a.C / 512, RW = a.R / 1024;
+    if (NV > 6 || RW * NV > 16 || (a.epi == EPI_SWIGLU && (RW & 1))) return 1;
+    if (a.xcopy && ((uintptr_t)a.xcopy & 15)) return 1;
+    const dim3 grid(a.R / (4 * RW));
+    const size_t smem = (size_t)(a.C + 4) * sizeof(float);
+#define QTTS_GW(RW_, NV_)                                                                              \
+    if (RW == RW_ && NV == NV_) {                                                                      \
+        if (a.nt) {                                                                                    \
+            hipLaunchKernelGGL((k_gemvw<RW_, NV_, true>), grid, dim3(256), smem, st, a);               \
+            qtts_last_kernel = "k_gemvw<" #RW_ ", " #NV_ ", true>";                                    \
+        } else {                                                                                       \
+            hipLaunchKernelGGL((k_gemvw<RW_, NV_, false>), grid, dim3(256), smem, st, a);              \
+            qtts_last_kernel = "k_gemvw<" #RW_ ", " #NV_ ", false>";                                   \
+        }                                                                                              \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                               \
+    }
+    // sub-talker (Hs 1024): q|k|v 4096x1024, gate|up 6144x1024, down 1024x3072,
+    // lm heads 2048x1024, O 1024x2048; talker 0.6B (H 1024) alike
+    QTTS_GW(4, 2) QTTS_GW(6, 2) QTTS_GW(1, 6) QTTS_GW(2, 2) QTTS_GW(1, 4) QTTS_GW(1, 2) QTTS_GW(3, 2)
+    QTTS_GW(2, 4) QTTS_GW(4, 4)
+#undef QTTS_GW
+    return 1;
+}

@@ -229,9 +229,13 @@ __device__ __forceinline__ void attn_full_wg(const AttnArgs &a, int kvh, int r, 
 // lout != nullptr: the 2*HD outputs go to LDS lout (the caller barriers);
 // wcache = false: the token's k / v are used but not stored (another
 // workgroup of the launch stores them).
-template <int HD, bool SC1>
+struct NoIssue { __device__ __forceinline__ void operator()() const {} };
+// `issue` runs right after the attention's own loads are issued (k_attn_o
+// issues its O-weight fragment there: loads retire in issue order, so the
+// attention's inputs must not queue behind the weights)
+template <int HD, bool SC1, class Issue = NoIssue>
 __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r, float *lq, float *scs,
-                                              float *lout = nullptr, bool wcache = true) {
+                                              float *lout = nullptr, bool wcache = true, Issue issue = Issue()) {
     constexpr int D4 = HD / 4, LPK = HD / 16, NK = 16;
     float (*sc)[NK] = reinterpret_cast<float (*)[NK]>(scs);
     const int tid = threadIdx.x;
@@ -262,6 +266,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
     float vr[NK];
 #pragma unroll
     for (int t = 0; t < NK; ++t) vr[t] = (go < 2 && t < p) ? Vc[(size_t)t * KVD + dd] : 0.f;
+    issue();
 
     // ---- per-head RMSNorm (T.c:646-649) + RoPE (T.c:650-653) -> LDS; k, v -> cache (T.c:654-655)
     float ss = x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;

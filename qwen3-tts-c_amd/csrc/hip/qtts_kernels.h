@@ -54,6 +54,8 @@ struct GemvArgs {
     }
 };
 int qtts_gemv(const GemvArgs &a, hipStream_t st);
+// batch-1 wave-per-row GEMV for Infinity-Cache-resident weights (k_gemvw.hip); 1 = not covered
+int qtts_gemvw(const GemvArgs &a, hipStream_t st);
 // lock-step batch (2..16 rows) on the bf16 matrix cores (k_gemvm.hip); 1 = not covered
 int qtts_gemvm(const GemvArgs &a, hipStream_t st);
 // multi-row (2..64) projection on the bf16 matrix cores (k_mgemm.hip); 1 = not covered

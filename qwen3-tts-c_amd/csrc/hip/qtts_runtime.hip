@@ -1322,6 +1322,14 @@ extern "C" int qtts_hip_decode_matvec_bf16(float *out, const uint16_t *A, const 
     return qtts_gemv(a, (hipStream_t)stream);
 }
 
+extern "C" int qtts_hip_resident_matvec_bf16(float *out, const uint16_t *A, const float *x, const float *w, float eps,
+                                             int rows, int cols, int epi, void *stream) {
+    if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_SWIGLU) return -1;
+    GemvArgs a = gv(A, rows, cols, x, cols, out, epi == EPI_SWIGLU ? rows / 2 : rows, 1, epi);
+    a.norm_w = w; a.eps = eps; a.nt = 0;
+    return qtts_gemv(a, (hipStream_t)stream);
+}
+
 extern "C" int qtts_hip_sample_top_k(int *out, const float *logits, int vocab, int top_k, float top_p, float temp,
                                      uint32_t *rng_bits, int batch, void *stream) {
     SampArgs s;

@@ -71,7 +71,7 @@ EXPORTS = [
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
     "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
-    "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_decode_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
+    "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_decode_matvec_bf16", "qtts_hip_resident_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
     "qtts_hip_transposed_conv1d", "qtts_hip_snake_beta", "qtts_hip_expf_glibc", "qtts_hip_sync",
     "qtts_dev_profile_frame", "qtts_dev_codec_stream_begin", "qtts_dev_codec_stream_push_slot",
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
@@ -137,6 +137,7 @@ def lib():
     L.qtts_hip_matvec_bf16.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
     L.qtts_hip_rmsnorm_matvec_bf16.argtypes = [vp, vp, vp, vp, C.c_float, C.c_int, C.c_int, C.c_int, vp]
     L.qtts_hip_decode_matvec_bf16.argtypes = [vp, vp, vp, vp, C.c_float, C.c_int, C.c_int, C.c_int, vp]
+    L.qtts_hip_resident_matvec_bf16.argtypes = [vp, vp, vp, vp, C.c_float, C.c_int, C.c_int, C.c_int, vp]
     L.qtts_hip_sample_top_k.argtypes = [vp, vp, C.c_int, C.c_int, C.c_float, C.c_float, vp, C.c_int, vp]
     L.qtts_hip_causal_conv1d.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
     L.qtts_hip_transposed_conv1d.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp]
@@ -362,6 +363,11 @@ class Kernels:
     def decode_matvec_bf16(out, A_u16, x, w, eps, rows, cols, batch=1):
         _ok(lib().qtts_hip_decode_matvec_bf16(_ptr(out), _ptr(A_u16), _ptr(x), _ptr(w) if w is not None else None,
                                               eps, rows, cols, batch, _stream()), "decode_matvec")
+
+    @staticmethod
+    def resident_matvec_bf16(out, A_u16, x, w, eps, rows, cols, epi=0):
+        _ok(lib().qtts_hip_resident_matvec_bf16(_ptr(out), _ptr(A_u16), _ptr(x), _ptr(w) if w is not None else None,
+                                                eps, rows, cols, epi, _stream()), "resident_matvec")
 
     @staticmethod
     def sample_top_k(out_i32, logits, vocab, top_k, top_p, temperature, rng_u32, batch=1):

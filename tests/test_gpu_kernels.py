@@ -117,6 +117,45 @@ def test_decode_matvec_batch(gpu, R, Cc, B, norm):
     assert np.all(np.abs(got - ref) <= gemv_bound(A, xn) + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
 
 
+# the sub-talker chain's batch-1 GEMV (k_gemvw: Infinity-Cache-resident weights)
+# at the 1.7B / 0.6B sub-talker shapes, every epilogue, + shapes it leaves to k_gemv1
+RESIDENT = [(4096, 1024, 0, True), (6144, 1024, 4, True), (1024, 3072, 3, False), (2048, 1024, 0, True),
+            (1024, 2048, 3, False), (3072, 1024, 0, True), (2048, 2048, 0, True), (4096, 2048, 0, False),
+            (1024, 1024, 3, True), (6144, 2048, 4, True), (96, 64, 0, True), (200, 1024, 3, False)]
+
+
+@pytest.mark.parametrize("R,Cc,epi,norm", RESIDENT)
+def test_resident_matvec(gpu, R, Cc, epi, norm):
+    import torch
+    rng = np.random.default_rng(R + 5 * Cc + epi)
+    A = f32_to_bf16((rng.standard_normal((R, Cc)) / np.sqrt(Cc)).astype(np.float32))
+    x = (rng.standard_normal((1, Cc)) * 2).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(Cc)).astype(np.float32)
+    nout = R // 2 if epi == 4 else R
+    y0 = rng.standard_normal(nout).astype(np.float32) if epi == 3 else np.zeros(nout, np.float32)
+    out = T(y0.copy(), gpu)
+    qtts.Kernels.resident_matvec_bf16(out, T(A, gpu, torch.int16), T(x, gpu), T(w, gpu) if norm else None, 1e-6,
+                                      R, Cc, epi)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    xn = x.astype(np.float64)
+    if norm:
+        xn = x / np.sqrt((x.astype(np.float64) ** 2).mean(1, keepdims=True) + 1e-6) * w
+    acc = (xn @ bf16_f64(A).T)[0]
+    bound = gemv_bound(A, xn)[0] + 1e-5 * np.abs(acc)
+    if epi == 0:
+        ref = acc
+    elif epi == 3:
+        ref = y0 + acc
+    else:   # SwiGLU over gate|up quads: rows 8q..8q+3 gate, 8q+4..8q+7 up
+        q = acc.reshape(-1, 2, 4)
+        g, u = q[:, 0, :].reshape(-1), q[:, 1, :].reshape(-1)
+        ref = g / (1 + np.exp(-g)) * u
+        bound = (bound.reshape(-1, 2, 4)[:, 0, :].reshape(-1) + bound.reshape(-1, 2, 4)[:, 1, :].reshape(-1)) * \
+            (np.abs(u) + np.abs(g) + 1)
+    assert np.all(np.abs(got - ref) <= bound), np.abs(got - ref).max()
+
+
 def sample_gpu(dev, lg, V, k, tp, temp, rng_bits):
     import torch
     B = lg.shape[0]

@@ -100,7 +100,6 @@ __global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out) {
 __global__ __launch_bounds__(256) void k_chain(const Op *ops, int nops, const float *x0, uint64_t *gbuf,
                                                unsigned base, unsigned *err) {
     __shared__ __attribute__((aligned(16))) float xs[VMAX];
-    __shared__ int bad;
     v4u w[24];
     for (int c = threadIdx.x; c < ops[0].C; c += 256) xs[c] = x0[c];
     __syncthreads();
@@ -108,19 +107,28 @@ __global__ __launch_bounds__(256) void k_chain(const Op *ops, int nops, const fl
         const Op o = ops[i];
         DISPATCH(o, load_w, o, blockIdx.x, w);      // next weights in flight before the wait
         if (i > 0) {
+            // sweep: every granule of this thread's share loaded at once per
+            // pass (N / 256 <= 16 loads in flight), re-swept until all tags match
             const uint64_t *g = gbuf + (size_t)o.in * VMAX;
             const unsigned ep = base + i;           // epoch of op i-1's output
-            if (threadIdx.x == 0) bad = 0;
-            for (int c = threadIdx.x; c < o.C; c += 256) {
-                uint64_t v;
-                unsigned spins = 0;
-                while (((v = __hip_atomic_load(g + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != ep) {
-                    if (++spins > (1u << 22)) { bad = 1; break; }
-                }
-                xs[c] = __uint_as_float((unsigned)v);
+            const int n = o.C / 256;
+            uint64_t v[16];
+            unsigned spins = 0;
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (k < n) {
+                        v[k] = __hip_atomic_load(g + threadIdx.x + 256 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok &= (unsigned)(v[k] >> 32) == ep;
+                    }
+                if (__syncthreads_and(ok)) break;
+                if (++spins > (1u << 20)) { if (threadIdx.x == 0) atomicAdd(err, 1u); return; }
             }
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < n) xs[threadIdx.x + 256 * k] = __uint_as_float((unsigned)v[k]);
             __syncthreads();
-            if (bad) { if (threadIdx.x == 0) atomicAdd(err, 1u); return; }
         }
         DISPATCH(o, compute, o, blockIdx.x, w, xs, nullptr, gbuf + (size_t)o.out * VMAX, base + i + 1);
         __syncthreads();
@@ -128,6 +136,15 @@ __global__ __launch_bounds__(256) void k_chain(const Op *ops, int nops, const fl
 }
 
 __global__ void k_empty(int) {}
+// the talker's per-frame weight stream (2.8 GB, non-temporal loads, as k_gemv1<.., true>)
+__global__ __launch_bounds__(256) void k_stream(const v4u *p, size_t n, unsigned *sink) {
+    unsigned x = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const v4u v = __builtin_nontemporal_load(p + i);
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x9E3779B9u) *sink = x;
+}
 __global__ __launch_bounds__(256) void k_read4k(const float *in, float *out) {
     __shared__ float red[4];
     float4 v = reinterpret_cast<const float4 *>(in)[threadIdx.x];
@@ -216,6 +233,27 @@ int main() {
         }, 20);
         printf("graph, grid %d: %.2f us per layer (%.2f us per op kernel)\n", grid, t * 1e3 / (passes * L),
                t * 1e3 / (passes * L * 4));
+        if (grid == ncu) {   // a frame: the talker's 2.8 GB HBM stream, then the 16 passes
+            const size_t sb = (size_t)2800 << 20;
+            v4u *big;
+            unsigned *sink;
+            CK(hipMalloc(&big, sb));
+            CK(hipMemset(big, 1, sb));
+            CK(hipMalloc(&sink, 4));
+            const float ts = timed_graph([&] {
+                hipLaunchKernelGGL(k_stream, dim3(4 * ncu), dim3(256), 0, st, big, sb / 16, sink);
+            }, 10);
+            const float tf = timed_graph([&] {
+                hipLaunchKernelGGL(k_stream, dim3(4 * ncu), dim3(256), 0, st, big, sb / 16, sink);
+                for (int p = 0; p < passes; ++p)
+                    for (auto &o : ops)
+                        hipLaunchKernelGGL(k_op, dim3(grid), dim3(256), 0, st, o, bufs[o.in], bufs[o.out]);
+            }, 10);
+            printf("  2.8 GB nt stream alone: %.1f us (%.2f TB/s); stream + 16 passes: %.1f us -> %.2f us per layer "
+                   "after the stream\n", ts * 1e3, sb / (ts * 1e-3) / 1e12, tf * 1e3, (tf - ts) * 1e3 / (passes * L));
+            CK(hipFree(big));
+            CK(hipFree(sink));
+        }
         // persistent
         std::vector<Op> all;
         for (int p = 0; p < passes; ++p) all.insert(all.end(), ops.begin(), ops.end());
