@@ -447,12 +447,9 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         fprintf(stderr, "qtts_gemv: xadd needs the batch-1 fast path (R=%d C=%d)\n", a.R, a.C);
         return -1;
     }
-    if (a.nb == 1 && a.ksplit <= 0) {
-        static const int lean = [] { const char *e = getenv("QTTS_HIP_GEMVW"); return e ? atoi(e) : 1; }();
-        if (lean == 2 || (lean == 1 && !a.nt)) {
-            const int rc = qtts_gemvw(a, st);
-            if (rc != 1) return rc;
-        }
+    if (a.nb == 1 && a.ksplit <= 0) {   // the wave-per-row kernel where it covers the shape (k_gemvw.hip)
+        const int rc = qtts_gemvw(a, st);
+        if (rc != 1) return rc;
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
         int nthr = 256;

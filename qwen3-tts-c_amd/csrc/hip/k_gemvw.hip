@@ -16,7 +16,8 @@
 // hand-offs between the ops measured 5.1 us per op in the same benchmark:
 // the all-to-all vector exchange costs more than the boundary it removes.
 //
-// Mapping: one 256-thread workgroup per 4*RW rows (grid ~256 = one per CU);
+// Mapping: one 256-thread workgroup per 4*RW rows (grid 256 = one per CU, or
+// 512 for the 1.7B talker's gate|up and down);
 // wave w owns rows row0 + w + 4i (i < RW); lane l covers the 8-column chunks
 // l + 64k (k < NV), so C = 512 NV and every wave load is 1 KB contiguous.
 // The x loads are issued first, then all RW*NV 16-B weight loads of a lane;
@@ -64,8 +65,10 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
         if (a.table) trow = a.table + off;
         else xrow = a.table_f32 + off;
     }
-    constexpr int PMAX = 8;   // partials held in registers (more: summed from memory below)
-    float4 xv[XQ], pv[XQ][PMAX], nwv[XQ];
+    // partials held in registers (the sub-talker's 8 per-head O partials at
+    // C = 1024); wider rows sum them from memory below
+    constexpr int PMAX = XQ == 1 ? 8 : 0;
+    float4 xv[XQ], pv[XQ][PMAX > 0 ? PMAX : 1], nwv[XQ];
     const int np = a.xadd ? a.n_xadd : 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
@@ -174,14 +177,16 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
 }  // namespace
 
 // Returns 1 when the shape is not covered (the caller uses k_gemv1), 0 ok,
-// -1 on a launch error.  Covers nb == 1, C in {512, 1024, ..., 3072},
-// R a multiple of 1024 (RW = R / 1024 rows per wave, grid R / (4 RW) = 256
-// workgroups), RW * NV <= 16 registers' worth of loads per lane.
+// -1 on a launch error.  Covers nb == 1, C = 512 NV, R = 1024 RW (grid 256,
+// one workgroup per CU) or R = 2048 RW (grid 512) where RW * NV loads per
+// lane would not fit one workgroup per CU.
 int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
     if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart || !a.ldx_ok1()) return 1;
-    const int NV = a.C / 512, RW = a.R / 1024;
-    if (NV > 6 || RW * NV > 16 || (a.epi == EPI_SWIGLU && (RW & 1))) return 1;
     if (a.xcopy && ((uintptr_t)a.xcopy & 15)) return 1;
+    const int NV = a.C / 512;
+    int RW = a.R / 1024;
+    if (RW * NV > 16 && a.R % 2048 == 0) RW = a.R / 2048;   // two workgroups per CU
+    if (RW * NV > 24 || (a.epi == EPI_SWIGLU && (RW & 1))) return 1;
     const dim3 grid(a.R / (4 * RW));
     const size_t smem = (size_t)(a.C + 4) * sizeof(float);
 #define QTTS_GW(RW_, NV_)                                                                              \
@@ -195,10 +200,14 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
         }                                                                                              \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                               \
     }
-    // sub-talker (Hs 1024): q|k|v 4096x1024, gate|up 6144x1024, down 1024x3072,
-    // lm heads 2048x1024, O 1024x2048; talker 0.6B (H 1024) alike
+    // sub-talker (Hs 1024) and 0.6B talker (H 1024): q|k|v 4096x1024, gate|up
+    // 6144x1024, down 1024x3072, lm heads 2048x1024, O 1024x2048, codec head
+    // 3072x1024; 1.7B talker (H 2048): q|k|v 4096x2048, O 2048x2048, gate|up
+    // 12288x2048 (grid 512), codec head 3072x2048.  (The talker's down
+    // projection 2048x6144 as RW 1, NV 12 measured 6.8 vs 5.9 us on k_gemv1's
+    // wide config, profiles/r02h_frame_trace_*.txt: left to k_gemv1.)
     QTTS_GW(4, 2) QTTS_GW(6, 2) QTTS_GW(1, 6) QTTS_GW(2, 2) QTTS_GW(1, 4) QTTS_GW(1, 2) QTTS_GW(3, 2)
-    QTTS_GW(2, 4) QTTS_GW(4, 4)
+    QTTS_GW(2, 4) QTTS_GW(4, 4) QTTS_GW(6, 4) QTTS_GW(3, 4)
 #undef QTTS_GW
     return 1;
 }

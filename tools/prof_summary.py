@@ -7,9 +7,16 @@ Looks under <out_dir> for
   prof/**/run_kernel_stats.csv        (--kernel-trace --stats)  -> kernel_stats.csv (copied)
   pmc_fetch/**/*counter_collection.csv (--pmc FETCH_SIZE)        -> pmc.json
   pmc_write/**/*counter_collection.csv (--pmc WRITE_SIZE)
+  pmc_mfma/**/*counter_collection.csv  (--pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE)
 and writes pmc.json: per kernel name {dispatches, FETCH_SIZE_kb_avg,
 WRITE_SIZE_kb_avg, hbm_read_bytes_avg (FETCH_SIZE x 1024 x 2: the gfx950
 half-count correction of MI355X_MICROARCH.md "HBM"), hbm_write_bytes_avg}.
+and mfma.json: per matrix-core kernel {dispatches, the three counters per
+dispatch, mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 256 CUs
+x 4 SIMDs)} -- GRBM_GUI_ACTIVE is summed over the 8 XCDs and
+SQ_VALU_MFMA_BUSY_CYCLES counts 32 cycles per 32x32x16 bf16 MFMA per SIMD
+(MI355X_MICROARCH.md), so mfma_util is the fraction of the chip's matrix-core
+issue cycles the kernel kept busy while it ran.
 The raw traces are deleted afterwards (they do not fit gpurun's 64 MiB).
 """
 import csv
@@ -59,11 +66,24 @@ def main():
             e["hbm_read_bytes_avg"] = e["FETCH_SIZE_kb_avg"] * 1024 * 2
         if "WRITE_SIZE_kb_avg" in e:
             e["hbm_write_bytes_avg"] = e["WRITE_SIZE_kb_avg"] * 1024
-    with open(os.path.join(d, "pmc.json"), "w") as f:
-        json.dump(res, f, indent=1, sort_keys=True)
-    for sub in ("prof", "pmc_fetch", "pmc_write"):
+    if res:   # (a second call after the mfma pass leaves the first call's pmc.json)
+        with open(os.path.join(d, "pmc.json"), "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+    mf = {}
+    for name, e in counters(find(os.path.join(d, "pmc_mfma"), "*counter_collection.csv")).items():
+        busy = e.get("SQ_VALU_MFMA_BUSY_CYCLES_kb_avg", 0.0)
+        if busy <= 0:
+            continue
+        act = e.get("GRBM_GUI_ACTIVE_kb_avg", 0.0)
+        mf[name] = {"dispatches": e["dispatches"], "SQ_VALU_MFMA_BUSY_CYCLES_avg": busy,
+                    "SQ_BUSY_CYCLES_avg": e.get("SQ_BUSY_CYCLES_kb_avg"), "GRBM_GUI_ACTIVE_avg": act,
+                    "mfma_util": busy / (act / 8 * 256 * 4) if act > 0 else None}
+    if mf:
+        with open(os.path.join(d, "mfma.json"), "w") as f:
+            json.dump(mf, f, indent=1, sort_keys=True)
+    for sub in ("prof", "pmc_fetch", "pmc_write", "pmc_mfma"):
         shutil.rmtree(os.path.join(d, sub), ignore_errors=True)
-    print(f"summaries in {d}: kernel_stats.csv, pmc.json ({len(res)} kernels)")
+    print(f"summaries in {d}: kernel_stats.csv, pmc.json ({len(res)} kernels), mfma.json ({len(mf)} kernels)")
 
 
 if __name__ == "__main__":
