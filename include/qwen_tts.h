@@ -175,6 +175,7 @@ typedef struct {
     int last_stop_reason;        /* 1 eos, 2 max_tokens */
     int last_stop_step;
     double perf_first_packet_ms; /* qwen_tts_generate_stream(): entry -> first audio chunk delivered */
+    void *tokenizer;             /* Qwen2 BPE of the model dir, loaded on first text input */
 } qwen_tts_ctx_t;
 
 qwen_tts_ctx_t *qwen_tts_load(const char *model_dir);
@@ -259,6 +260,18 @@ float *qwen_tts_generate_voice_clone_stream(qwen_tts_ctx_t *ctx, const char *tex
  * qwen_tts_codec_decode of all frames at once. */
 int qwen_tts_codec_stream_begin(qwen_tts_ctx_t *ctx, int max_frames);
 int qwen_tts_codec_stream_push(qwen_tts_ctx_t *ctx, const int *codes, int time_steps, float *out);
+
+/* Text input (the reference's TODO at c/qwen_tts.c:1071-1077,
+ * its browser front end tokenizes with @huggingface/transformers,
+ * web/wasm/app.js:241-267): Qwen2 byte-level BPE over the model directory's
+ * vocab.json / merges.txt / tokenizer_config.json.
+ * qwen_tts_tokenize: UTF-8 text (NFC) -> malloc'd ids (caller frees), NULL on
+ * error with *n_ids = 0; needs no GPU.
+ * qwen_tts_text_prompt: the comma-separated ids of the chat template
+ * "<|im_start|>assistant\n{text}<|im_end|>\n<|im_start|>assistant\n" -- the
+ * `text` argument of qwen_tts_generate* -- malloc'd, NULL on error. */
+int *qwen_tts_tokenize(const char *model_dir, const char *text, int *n_ids);
+char *qwen_tts_text_prompt(qwen_tts_ctx_t *ctx, const char *text);
 
 /* sizeof(qwen_tts_ctx_t) as compiled into the library (FFI layout check) */
 size_t qwen_tts_abi_sizeof_ctx(void);

@@ -29,10 +29,12 @@ static double now_ms(void) {
 static void usage(const char *prog) {
     fprintf(stderr,
             "qwen-tts (MI355X / gfx950) - Qwen3-TTS talker + sub-talker decode and codec vocoder on the GPU\n\n"
-            "usage: %s -d <model_dir> (-t <ids> | -f <file>) [options]\n\n"
+            "usage: %s -d <model_dir> (-t <ids> | -f <file> | -T <text>) [options]\n\n"
             "  -d <dir>    model directory (config.json, *.safetensors, speech_tokenizer/)\n"
             "  -t <ids>    comma-separated token ids in the chat template\n"
             "  -f <file>   token ids from a file (comma- or newline-separated)\n"
+            "  -T <text>   text, tokenized with the model dir's vocab.json / merges.txt (Qwen2 BPE)\n"
+            "              inside the chat template; --print-ids prints the ids and exits\n"
             "  -s <name>   speaker (config.json spk_id)      -l <lang>  language or auto\n"
             "  -o <path>   output wav (default output.wav)   -v         verbose (repeatable)\n"
             "  --temperature F (0.9)   --top-k N (50)   --top-p F (1.0)   --repetition-penalty F (1.05)\n"
@@ -104,7 +106,8 @@ static void progress(int step, int total, void *u) {
 int main(int argc, char **argv) {
     const char *dir = NULL, *ids = NULL, *ids_file = NULL, *spk = NULL, *lang = NULL, *out = "output.wav";
     int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1, stream_chunk = 0, non_streaming = 0;
-    const char *ref_codes_file = NULL, *ref_text = NULL, *xvec_file = NULL;
+    const char *ref_codes_file = NULL, *ref_text = NULL, *xvec_file = NULL, *text = NULL;
+    int print_ids = 0;
     float temp = -1, st_temp = -1, top_p = -1, st_top_p = -1, rep = -1;
     int top_k = -1, st_top_k = -1, max_tokens = -1, fixed = -1, seed = -1;
     for (int i = 1; i < argc; i++) {
@@ -114,6 +117,8 @@ int main(int argc, char **argv) {
         if (ARG("-d")) dir = argv[++i];
         else if (ARG("-t")) ids = argv[++i];
         else if (ARG("-f")) ids_file = argv[++i];
+        else if (ARG("-T")) text = argv[++i];
+        else if (!strcmp(a, "--print-ids")) print_ids = 1;
         else if (ARG("-s")) spk = argv[++i];
         else if (ARG("-l")) lang = argv[++i];
         else if (ARG("-o")) out = argv[++i];
@@ -146,7 +151,25 @@ int main(int argc, char **argv) {
 #undef ARG
     }
     if (!dir) { fprintf(stderr, "Error: model directory required (-d)\n\n"); usage(argv[0]); return 1; }
-    if (!ids && !ids_file) { fprintf(stderr, "Error: token IDs required (-t or -f)\n\n"); usage(argv[0]); return 1; }
+    if (!ids && !ids_file && !text) {
+        fprintf(stderr, "Error: token IDs required (-t or -f) or text (-T)\n\n");
+        usage(argv[0]);
+        return 1;
+    }
+    if (text && print_ids) {   /* tokenizer only: no model load, no GPU */
+        int n = 0;
+        static const char pre[] = "<|im_start|>assistant\n", post[] = "<|im_end|>\n<|im_start|>assistant\n";
+        char *chat = (char *)malloc(strlen(text) + sizeof pre + sizeof post);
+        if (!chat) return 1;
+        sprintf(chat, "%s%s%s", pre, text, post);
+        int *tid = qwen_tts_tokenize(dir, chat, &n);
+        free(chat);
+        if (!tid) return 1;
+        for (int k = 0; k < n; k++) printf(k ? ",%d" : "%d", tid[k]);
+        printf("\n");
+        free(tid);
+        return 0;
+    }
     if (runs < 1 || warmup < 0 || batch < 1) {
         fprintf(stderr, "Error: invalid benchmark settings (--benchmark-runs >= 1, --benchmark-warmup >= 0)\n");
         return 1;
@@ -197,6 +220,14 @@ int main(int argc, char **argv) {
         fprintf(stderr, "Error: failed to load model\n");
         free(file_ids);
         return 1;
+    }
+    if (text && !ids) {   /* -T: the chat-template ids of the text (Qwen2 BPE, bpe.c) */
+        if (!(file_ids = qwen_tts_text_prompt(ctx, text))) {
+            fprintf(stderr, "Error: cannot tokenize the text\n");
+            qwen_tts_free(ctx); free(ref_codes); free(xvec);
+            return 1;
+        }
+        ids = file_ids;
     }
     if (xvec && n_xvec != ctx->config.talker_hidden) {
         fprintf(stderr, "Error: --xvector has %d floats, the talker hidden size is %d\n", n_xvec,

@@ -24,6 +24,7 @@
 #include <unistd.h>
 
 #include "../../../include/qtts_hip.h"
+#include "bpe.h"
 #include "qjson.h"
 
 int qwen_tts_verbose = 0;
@@ -324,7 +325,46 @@ void qwen_tts_free(qwen_tts_ctx_t *ctx) {
     free(ctx->config.language_ids);
     free(ctx->last_codes);
     free(ctx->tk_x);
+    qtok_free((qtok_t *)ctx->tokenizer);
     free(ctx);
+}
+
+/* ------------------------------------------------------------------ text input (bpe.c) */
+int *qwen_tts_tokenize(const char *model_dir, const char *text, int *n_ids) {
+    if (n_ids) *n_ids = 0;
+    if (!model_dir || !text || !n_ids) return NULL;
+    qtok_t *t = qtok_load(model_dir);
+    if (!t) return NULL;
+    int *ids = NULL;
+    const int n = qtok_encode(t, text, &ids);
+    qtok_free(t);
+    if (n < 0) return NULL;
+    *n_ids = n;
+    return ids;
+}
+
+char *qwen_tts_text_prompt(qwen_tts_ctx_t *ctx, const char *text) {
+    if (!ctx || !text) return NULL;
+    if (!ctx->tokenizer && !(ctx->tokenizer = qtok_load(ctx->model_dir))) return NULL;
+    static const char pre[] = "<|im_start|>assistant\n", post[] = "<|im_end|>\n<|im_start|>assistant\n";
+    const size_t lt = strlen(text);
+    char *chat = (char *)malloc(sizeof pre + lt + sizeof post);
+    if (!chat) return NULL;
+    memcpy(chat, pre, sizeof pre - 1);
+    memcpy(chat + sizeof pre - 1, text, lt);
+    memcpy(chat + sizeof pre - 1 + lt, post, sizeof post);
+    int *ids = NULL;
+    const int n = qtok_encode((qtok_t *)ctx->tokenizer, chat, &ids);
+    free(chat);
+    if (n < 0) return NULL;
+    char *csv = (char *)malloc((size_t)n * 12 + 1);
+    if (!csv) { free(ids); return NULL; }
+    size_t k = 0;
+    for (int i = 0; i < n; i++) k += (size_t)sprintf(csv + k, i ? ",%d" : "%d", ids[i]);
+    csv[k] = 0;
+    free(ids);
+    if (qwen_tts_verbose >= 1) fprintf(stderr, "Text: %d tokens (chat template)\n", n);
+    return csv;
 }
 
 void qwen_tts_set_progress_callback(qwen_tts_ctx_t *ctx, qwen_tts_progress_cb cb, void *userdata) {

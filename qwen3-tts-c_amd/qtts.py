@@ -56,6 +56,7 @@ class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
         ("perf_codec_tokens", C.c_int), ("perf_prefill_ms", C.c_double), ("perf_first_frame_ms", C.c_double),
         ("last_codes", _ip), ("last_frames", C.c_int), ("last_stop_reason", C.c_int), ("last_stop_step", C.c_int),
         ("perf_first_packet_ms", C.c_double),
+        ("tokenizer", C.c_void_p),
     ]
 
 
@@ -66,7 +67,8 @@ EXPORTS = [
     "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
     "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
-    "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream",
+    "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream", "qwen_tts_tokenize",
+    "qwen_tts_text_prompt",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -79,6 +81,18 @@ EXPORTS = [
 ]
 
 _LIB = None
+
+
+def tokenize(model_dir, text):
+    """Qwen2 BPE ids of `text` (qwen_tts_tokenize: the model dir's vocab.json /
+    merges.txt; no GPU needed).  None on error."""
+    n = C.c_int(0)
+    p = lib().qwen_tts_tokenize(model_dir.encode(), text.encode("utf-8"), C.byref(n))
+    if not p:
+        return None
+    ids = np.ctypeslib.as_array(C.cast(p, _ip), shape=(n.value,)).tolist() if n.value else []
+    _libc.free(C.c_void_p(p))
+    return ids
 
 
 def lib():
@@ -117,6 +131,10 @@ def lib():
     L.qwen_tts_set_progress_callback.argtypes = [C.POINTER(Ctx), PROGRESS_CB, C.c_void_p]
     L.qwen_tts_write_wav.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
     L.qwen_tts_abi_sizeof_ctx.restype = C.c_size_t
+    L.qwen_tts_tokenize.restype = C.c_void_p
+    L.qwen_tts_tokenize.argtypes = [C.c_char_p, C.c_char_p, _ip]
+    L.qwen_tts_text_prompt.restype = C.c_void_p
+    L.qwen_tts_text_prompt.argtypes = [C.POINTER(Ctx), C.c_char_p]
     L.qwen_tts_generate_stream.restype = C.c_void_p
     L.qwen_tts_generate_stream.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, AUDIO_CB,
                                            C.c_void_p, _ip]

@@ -360,11 +360,13 @@ def ensure_model(out, preset="tiny", seed=0, overrides=None):
     """Create the model dir unless an identical one (same preset/seed) exists."""
     stamp = os.path.join(out, ".synth_stamp")
     want = json.dumps({"preset": preset, "seed": seed, "overrides": overrides or {}}, sort_keys=True)
-    if os.path.exists(stamp) and open(stamp).read() == want:
-        return out
-    write_model(out, preset, seed, overrides, quiet=True)
-    with open(stamp, "w") as f:
-        f.write(want)
+    if not (os.path.exists(stamp) and open(stamp).read() == want):
+        write_model(out, preset, seed, overrides, quiet=True)
+        with open(stamp, "w") as f:
+            f.write(want)
+    if not os.path.exists(os.path.join(out, "merges.txt")):   # text input (tools/synth_tokenizer.py)
+        from synth_tokenizer import write as write_tokenizer
+        write_tokenizer(out)
     return out
 
 
