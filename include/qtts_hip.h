@@ -115,6 +115,13 @@ float *qtts_dev_codec_slot(qtts_dev_t *dev, int b, int T, int *out_samples);
  * returns the sample count (< 0 on error).  push_slot reads slot b's generated
  * codes [frame0, frame0 + T) on the device (no host round trip). */
 int qtts_dev_codec_stream_begin(qtts_dev_t *dev, int max_frames);
+/* the same with the internal chunk sized for pushes of up to chunk_frames
+ * frames at once (<= 16: the default 16) */
+int qtts_dev_codec_stream_begin_ex(qtts_dev_t *dev, int max_frames, int chunk_frames);
+/* push T host frames [T][16] through the stream on a second HIP stream without
+ * waiting, audio dropped; every later stream call is ordered after it (the
+ * voice-clone reference frames, overlapped with the prefill) */
+int qtts_dev_codec_stream_prime(qtts_dev_t *dev, const int *codes, int T);
 int qtts_dev_codec_stream_push_slot(qtts_dev_t *dev, int b, int frame0, int T, float *host_out);
 int qtts_dev_codec_stream_push_host(qtts_dev_t *dev, const int *codes, int T, float *host_out);
 

@@ -1357,7 +1357,8 @@ extern "C" int qtts_hip_expf_glibc(float *out, const float *in, int n, void *str
 // saved back.  The transformer keeps the last window-1 K/V rows per layer and
 // continues the absolute positions (RoPE table offset by pos0).
 namespace {
-constexpr int kStreamChunk = 16;   // frames per internal chunk
+constexpr int kStreamChunk = 16;      // frames per internal chunk
+constexpr int kStreamChunkMax = 128;  // largest chunk a begin may ask for
 
 void *salloc(CodecStream &S, size_t bytes) {
     void *p = nullptr;
@@ -1508,14 +1509,18 @@ void codec_stream_free(CodecModel *m) {
     S = CodecStream();
 }
 
-int codec_stream_begin(CodecModel *m, int max_frames) {
+int codec_stream_begin(CodecModel *m, int max_frames, int chunk) {
     const qtts_dims_t &d = m->d;
     CodecStream &S0 = m->cs;
+    // frames per internal chunk: kStreamChunk, or up to kStreamChunkMax when a
+    // caller pushes long runs at once (the voice-clone reference frames: one
+    // chunk of T frames runs ~T/16 times fewer, larger kernels)
+    const int tc_want = chunk > kStreamChunk ? (chunk < kStreamChunkMax ? chunk : kStreamChunkMax) : kStreamChunk;
     // the codec GEMMs' split-K workspace belongs to the (non-streaming) codec
     // state, which the decode state's re-allocation frees (free_state ->
     // codec_free_state): re-create it before a stream reuses its own buffers
     if (ensure_codec_state(m, 1)) return -1;
-    if (S0.active && max_frames + S0.tc <= S0.rope_cap) {
+    if (S0.active && max_frames + S0.tc <= S0.rope_cap && S0.tc >= tc_want) {
         // reuse the buffers: only the carried state restarts (zero histories =
         // the causal left padding, no K/V rows, position 0), on the codec stream
         for (size_t i = 0; i < S0.hist.size(); ++i)
@@ -1529,7 +1534,7 @@ int codec_stream_begin(CodecModel *m, int max_frames) {
     codec_stream_free(m);
     // (ensure_codec_state ran above: the split-K workspace exists)
     CodecStream &S = m->cs;
-    S.tc = kStreamChunk;
+    S.tc = tc_want;
     const int hm = S.hm, tc = S.tc;
     // activation buffers: largest C x (hm + L) over the stages at tc frames
     size_t L = (size_t)tc * d.ratios[0] * d.ratios[1];

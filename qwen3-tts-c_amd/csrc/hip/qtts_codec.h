@@ -69,9 +69,9 @@ int codec_finalize(CodecModel *m);
 // codes: device int32 [T][cq] (time-major).  Returns malloc'd host audio.
 float *codec_decode(CodecModel *m, const int *codes_dev, int T, int *out_samples);
 // streaming decode: begin resets the state (max_frames bounds the absolute
-// position); push decodes T more frames (device codes, rows of stride ldc
+// position; chunk > 16 sizes the internal chunk for long pushes); push decodes T more frames (device codes, rows of stride ldc
 // ints) and writes T * 1920 samples to host_out.  Returns samples or -1.
-int codec_stream_begin(CodecModel *m, int max_frames);
+int codec_stream_begin(CodecModel *m, int max_frames, int chunk = 0);
 int codec_stream_push(CodecModel *m, const int *codes_dev, int ldc, int T, float *host_out);
 // the same into `out` (host memory, synchronous; or device memory: enqueued on
 // m->st only, nothing waited for)

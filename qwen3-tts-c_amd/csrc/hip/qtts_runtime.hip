@@ -131,9 +131,10 @@ struct qtts_dev {
     hipEvent_t cev = nullptr;
     float *cwav = nullptr;
     size_t cwav_cap = 0;
-    // host codes staged for qtts_dev_codec_stream_push_host (grown on demand)
+    // host codes staged for qtts_dev_codec_stream_push_host / _prime (grown on demand)
     int *push_codes = nullptr;
     size_t push_cap = 0;
+    bool prime_pending = false;   // a qtts_dev_codec_stream_prime push runs on cst (cev marks its end)
     // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
@@ -912,7 +913,11 @@ extern "C" int qtts_dev_begin(qtts_dev_t *dv, int nb, int max_frames, int max_pr
     hipSetDevice(dv->device);
     if (max_prefill < 16) max_prefill = 16;
     const bool realloc_ = nb != dv->nb || max_frames > dv->max_frames || max_prefill > dv->p_cap;
-    if (realloc_) CKI(alloc_state(dv, nb, max_frames, max_prefill));
+    if (realloc_) {
+        if (dv->cst) CK(hipStreamSynchronize(dv->cst));   // a prime still reading the codec scratch
+        dv->prime_pending = false;
+        CKI(alloc_state(dv, nb, max_frames, max_prefill));
+    }
     if (!dv->have_par || !same_params(dv->par, *p)) {
         dv->par = *p;
         dv->have_par = true;
@@ -1109,16 +1114,82 @@ extern "C" float *qtts_dev_codec_slot(qtts_dev_t *dv, int b, int T, int *out_sam
 }
 
 // ----------------------------------------------------------------- streaming codec (exact, incremental)
+// a pending prime (below) orders every later use of the stream state after it
+static int join_prime(qtts_dev *dv) {
+    if (!dv->prime_pending) return 0;
+    dv->prime_pending = false;
+    CK(hipStreamWaitEvent(dv->st, dv->cev, 0));
+    return 0;
+}
+
+static int ensure_cst(qtts_dev *dv) {
+    if (dv->cst) return 0;
+    int lo = 0, hi = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
+    CK(hipEventCreateWithFlags(&dv->cev, hipEventDisableTiming));
+    return 0;
+}
+
+static int ensure_push_codes(qtts_dev *dv, size_t n) {
+    if (n <= dv->push_cap) return 0;
+    CK(hipDeviceSynchronize());
+    if (dv->push_codes) CK(hipFree(dv->push_codes));
+    dv->push_codes = nullptr;
+    dv->push_cap = 0;
+    const size_t cap = n < 4096 ? 4096 : n;
+    CK(hipMalloc(&dv->push_codes, cap * 4));
+    dv->push_cap = cap;
+    return 0;
+}
+
 extern "C" int qtts_dev_codec_stream_begin(qtts_dev_t *dv, int max_frames) {
+    return qtts_dev_codec_stream_begin_ex(dv, max_frames, 0);
+}
+
+extern "C" int qtts_dev_codec_stream_begin_ex(qtts_dev_t *dv, int max_frames, int chunk_frames) {
     if (!dv || max_frames < 1) return -1;
     hipSetDevice(dv->device);
+    CKI(join_prime(dv));
     CK(hipStreamSynchronize(dv->st));
-    return codec_stream_begin(&dv->codec, max_frames);
+    return codec_stream_begin(&dv->codec, max_frames, chunk_frames);
+}
+
+// Push T host frames through the stream on the second stream (cst) without
+// waiting: their audio is dropped (device scratch), the carried state is what
+// later pushes continue from.  The voice-clone reference frames go this way
+// while the prefill runs on the context stream (SURVEY.md 8f N1 + N2).
+extern "C" int qtts_dev_codec_stream_prime(qtts_dev_t *dv, const int *codes, int T) {
+    if (!dv || !codes || T < 1) return -1;
+    hipSetDevice(dv->device);
+    CKI(join_prime(dv));
+    CKI(ensure_cst(dv));
+    CKI(ensure_push_codes(dv, (size_t)T * dv->d.cq));
+    const size_t need = (size_t)T * 1920;
+    if (need > dv->cwav_cap) {
+        CK(hipStreamSynchronize(dv->cst));
+        if (dv->cwav) CK(hipFree(dv->cwav));
+        dv->cwav = nullptr;
+        dv->cwav_cap = 0;
+        CK(hipMalloc(&dv->cwav, need * 4));
+        dv->cwav_cap = need;
+    }
+    CK(hipEventRecord(dv->cev, dv->st));          // after the begin's resets on st
+    CK(hipStreamWaitEvent(dv->cst, dv->cev, 0));
+    CK(hipMemcpyAsync(dv->push_codes, codes, (size_t)T * dv->d.cq * 4, hipMemcpyHostToDevice, dv->cst));
+    dv->codec.st = dv->cst;
+    const int n = codec_stream_push_to(&dv->codec, dv->push_codes, dv->d.cq, T, dv->cwav, false);
+    dv->codec.st = dv->st;
+    if (n < 0) return -1;
+    CK(hipEventRecord(dv->cev, dv->cst));
+    dv->prime_pending = true;
+    return 0;
 }
 
 extern "C" int qtts_dev_codec_stream_push_slot(qtts_dev_t *dv, int b, int frame0, int T, float *host_out) {
     if (!dv || b < 0 || b >= dv->nb || T < 1 || frame0 < 0 || frame0 + T > dv->max_frames + 1) return -1;
     hipSetDevice(dv->device);
+    CKI(join_prime(dv));
     const int *codes = dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G + (size_t)frame0 * dv->d.G;
     return codec_stream_push(&dv->codec, codes, dv->d.G, T, host_out);
 }
@@ -1126,16 +1197,9 @@ extern "C" int qtts_dev_codec_stream_push_slot(qtts_dev_t *dv, int b, int frame0
 extern "C" int qtts_dev_codec_stream_push_host(qtts_dev_t *dv, const int *codes, int T, float *host_out) {
     if (!dv || !codes || T < 1) return -1;
     hipSetDevice(dv->device);
+    CKI(join_prime(dv));
     const size_t n = (size_t)T * dv->d.cq;
-    if (n > dv->push_cap) {   // persistent staging buffer: no allocation per push
-        CK(hipStreamSynchronize(dv->st));
-        if (dv->push_codes) CK(hipFree(dv->push_codes));
-        dv->push_codes = nullptr;
-        dv->push_cap = 0;
-        const size_t cap = n < 4096 ? 4096 : n;
-        CK(hipMalloc(&dv->push_codes, cap * 4));
-        dv->push_cap = cap;
-    }
+    CKI(ensure_push_codes(dv, n));   // persistent staging buffer: no allocation per push
     // ordered on the codec's stream before the push reads it; the synchronous
     // push waits for the stream before returning, so the host buffer may be reused
     CK(hipMemcpyAsync(dv->push_codes, codes, n * 4, hipMemcpyHostToDevice, dv->codec.st));
@@ -1150,12 +1214,8 @@ extern "C" int qtts_dev_codec_stream_push_host(qtts_dev_t *dv, const int *codes,
 extern "C" int qtts_dev_codec_async_begin(qtts_dev_t *dv, int max_frames) {
     if (!dv || max_frames < 1) return -1;
     hipSetDevice(dv->device);
-    if (!dv->cst) {
-        int lo = 0, hi = 0;
-        CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        CK(hipStreamCreateWithPriority(&dv->cst, hipStreamNonBlocking, lo));   // lowest: the decode goes first
-        CK(hipEventCreateWithFlags(&dv->cev, hipEventDisableTiming));
-    }
+    CKI(join_prime(dv));
+    CKI(ensure_cst(dv));
     const size_t need = (size_t)max_frames * 1920;
     if (need > dv->cwav_cap) {
         CK(hipStreamSynchronize(dv->cst));

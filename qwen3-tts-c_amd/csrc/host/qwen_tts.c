@@ -592,6 +592,15 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             qtts_dev_prompt(dev, b, pr[b].text, pr[b].n_text, pr[b].plan, pr[b].nplan, pr[b].p_len,
                             pr[b].n_trailing, pr[b].pad_row) != 0)
             goto out;
+    /* streaming voice clone: the reference frames go through the codec stream
+     * first (their audio is dropped), so the carried codec state is that of
+     * decoding reference ++ generated and the chunks start at the reference
+     * boundary.  They run on a second HIP stream in one chunk while the
+     * prefill runs (qtts_dev_codec_stream_prime); later pushes wait for them. */
+    const int sref = stream && vcs && vcs[0].ref_codes && vcs[0].n_ref > 0 ? vcs[0].n_ref : 0;
+    if (stream && (qtts_dev_codec_stream_begin_ex(dev, max_tokens + sref, sref) != 0 ||
+                   (sref && qtts_dev_codec_stream_prime(dev, vcs[0].ref_codes, sref) != 0)))
+        goto out;
     double t_prefill = now_ms();
     if (qtts_dev_prefill(dev) != 0) goto out;
     double t_prefill_done = now_ms();
@@ -607,15 +616,8 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     int streamed = 0;
     double t_stream = 0;
     if (stream) {
-        /* voice clone: the reference frames go through the stream first (their
-         * audio is dropped), so the carried codec state is that of decoding
-         * reference ++ generated, and the chunks start at the reference boundary */
-        const int sref = vcs && vcs[0].ref_codes && vcs[0].n_ref > 0 ? vcs[0].n_ref : 0;
-        sbuf = (float *)malloc((size_t)(max_tokens > sref ? max_tokens : sref) * 1920 * sizeof(float));
-        if (!sbuf || qtts_dev_codec_stream_begin(dev, max_tokens + sref) != 0 ||
-            (sref && qtts_dev_codec_stream_push_host(dev, vcs[0].ref_codes, sref, sbuf) < 0)) {
-            free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
-        }
+        sbuf = (float *)malloc((size_t)max_tokens * 1920 * sizeof(float));
+        if (!sbuf) { free(stopped); free(ngen); free(sstep); goto out; }
     }
     double t_gen = now_ms();
     const int poll_every = fixed > 0 ? 0 : 8;
