@@ -234,9 +234,9 @@ __global__ __launch_bounds__(256) void k_qk_prep_w(AttnArgs a) {
 // (agent-scope acq_rel ticket) merges them in split order and resets the
 // ticket.  Grid size is fixed at graph capture (nsplit from the cache
 // capacity); splits past the live length exit at once.
-template <int HD, int GPH>
+template <int HD, int GPH, int LPK>
 __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
-    constexpr int LPK = HD >= 32 ? HD / 32 : 1;   // lanes per key
+    // LPK lanes per key
     constexpr int DPL = HD / LPK;                  // dims per lane
     constexpr int CH = 256 / LPK;                  // keys per workgroup
     constexpr int D4 = HD / 4;
@@ -525,7 +525,15 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int qtts_attn_keys_per_split(int HD) { return HD >= 32 ? 256 / (HD / 32) : 256; }
+// lanes per key of the talker decode attention: CH = 256 / LPK keys per split
+// workgroup (QTTS_HIP_ATTN_LPK: development A/B switch, read once)
+static int attn_lpk(int HD) {
+    static const int env = [] { const char *e = getenv("QTTS_HIP_ATTN_LPK"); return e ? atoi(e) : 0; }();
+    const int base = HD >= 32 ? HD / 32 : 1;
+    if (env > 0 && env <= 64 && HD % env == 0 && HD / env >= 4 && env >= base) return env;
+    return base;
+}
+int qtts_attn_keys_per_split(int HD) { return 256 / attn_lpk(HD); }
 
 int qtts_attention(const AttnArgs &a, hipStream_t st) {
     if (a.HD > 128 || a.HD < 8 || (a.HD & 7) || a.NH % a.KV) {
@@ -552,12 +560,19 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
             return -1;
         }
         const dim3 grid(a.KV, nsplit, a.nrows);
-        switch (a.HD) {
-            case 128: hipLaunchKernelGGL((k_attn_dec<128, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<128, 2>"; break;
-            case 64: hipLaunchKernelGGL((k_attn_dec<64, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<64, 2>"; break;
-            case 32: hipLaunchKernelGGL((k_attn_dec<32, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<32, 2>"; break;
-            default: hipLaunchKernelGGL((k_attn_dec<16, 2>), grid, dim3(256), 0, st, a); qtts_last_kernel = "k_attn_dec<16, 2>"; break;
+        const int lpk = attn_lpk(a.HD);
+#define QTTS_AD(H, L)                                                                                      \
+        if (a.HD == H && lpk == L) {                                                                       \
+            hipLaunchKernelGGL((k_attn_dec<H, 2, L>), grid, dim3(256), 0, st, a);                         \
+            qtts_last_kernel = "k_attn_dec<" #H ", 2, " #L ">";                                            \
+            return hipGetLastError() == hipSuccess ? 0 : -1;                                               \
         }
+        QTTS_AD(128, 4) QTTS_AD(128, 8) QTTS_AD(128, 16) QTTS_AD(128, 32)
+        QTTS_AD(64, 2) QTTS_AD(64, 4) QTTS_AD(64, 8) QTTS_AD(64, 16)
+        QTTS_AD(32, 1) QTTS_AD(32, 2) QTTS_AD(32, 4) QTTS_AD(32, 8)
+        QTTS_AD(16, 1) QTTS_AD(16, 2) QTTS_AD(16, 4)
+#undef QTTS_AD
+        return -1;
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     size_t smem = (size_t)(128 * 3 + 256 + 8 + 8 * 128 + a.S + 4) * sizeof(float);

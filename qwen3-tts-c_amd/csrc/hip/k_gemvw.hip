@@ -181,7 +181,12 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
 // one workgroup per CU) or R = 2048 RW (grid 512) where RW * NV loads per
 // lane would not fit one workgroup per CU.
 int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
-    if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart || !a.ldx_ok1()) return 1;
+    if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart) return 1;
+    // sources: an fp32 row, a bf16 / fp32 table row (+ per-head partials too:
+    // the sub-talker's layer-0 gate|up reads its residual from the table)
+    if (a.xadd && (((uintptr_t)a.xadd & 15) || a.ld_xadd % 4 || a.n_xadd < 1)) return 1;
+    if (a.norm_w && ((uintptr_t)a.norm_w & 15)) return 1;
+    if (!a.table && ((uintptr_t)(a.table_f32 ? a.table_f32 : a.x) & 15)) return 1;
     if (a.xcopy && ((uintptr_t)a.xcopy & 15)) return 1;
     const int NV = a.C / 512;
     int RW = a.R / 1024;

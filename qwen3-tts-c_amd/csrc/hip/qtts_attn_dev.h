@@ -242,6 +242,11 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
     const int KVD = a.KV * HD;
     const int p = a.pos ? a.pos[r] : a.pos_const, n = p + 1;
     const float *row = a.qkv + (size_t)r * a.ld_qkv;
+    if (a.qkv_tab) {
+        const int *ip = a.tab_ids + (size_t)r * a.tab_bstride + a.tab_off;
+        if (a.tab_row_sel) ip += (size_t)a.tab_row_sel[r] * a.tab_rstride;
+        row = a.qkv_tab + (size_t)(*ip) * a.ld_qkv;
+    }
     const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
     const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -79,6 +79,12 @@ struct AttnArgs {
     int nrows = 0;
     const int *skip = nullptr;     // decode: per-b stop flags (skip the cache write)
     int win = 0;                   // >0: sliding window (keys t > pos - win), c/qwen_tts_codec.c:363-367
+    // decode: the q|k|v row of row r read from a table by id instead of qkv
+    // (the sub-talker's layer-0 projections of every input id, precomputed):
+    // id = tab_ids[r*tab_bstride + tab_row_sel[r]*tab_rstride + tab_off]
+    const float *qkv_tab = nullptr;
+    const int *tab_ids = nullptr, *tab_row_sel = nullptr;
+    int tab_bstride = 0, tab_rstride = 0, tab_off = 0;
     // decode split-K scratch: [rows][KV][nsplit][GPH*HD + 2*GPH] partials, [rows][KV] tickets (zeroed)
     float *part = nullptr;
     int *cnt = nullptr;

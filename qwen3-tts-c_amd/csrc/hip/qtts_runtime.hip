@@ -87,6 +87,11 @@ struct qtts_dev {
     // sub-talker pass g >= 1 can consume (fp32): [V][Hs] of the talker codec
     // embedding (pass 1) and [G-1][Vs][Hs] of the sub-talker ones (passes 2..)
     float *codec_ptab = nullptr, *st_ptab = nullptr;
+    // the sub-talker's layer-0 q|k|v of every row a pass g >= 1 can consume
+    // (its input is a table row chosen by the previous code alone): fp32
+    // [V + (G-2) Vs][QKVs], pass 1 rows first, then pass g at V + (g-2) Vs;
+    // computed once at load by the per-frame GEMV itself (bit-identical)
+    float *qkv0_tab = nullptr;
     // codec
     CodecModel codec;
     // rope
@@ -390,6 +395,7 @@ static int build_rope(qtts_dev *dv, int npos, int hd, float theta, float **cs, f
 }
 
 static int build_proj_tables(qtts_dev *dv);
+static int build_qkv0_table(qtts_dev *dv);
 
 extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
     const qtts_dims_t &d = dv->d;
@@ -425,7 +431,9 @@ extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
         return -1;
     }
     const char *pt = getenv("QTTS_HIP_PTAB");
-    if (dv->st_proj && !(pt && !atoi(pt))) CKI(build_proj_tables(dv));
+    const bool ptab_on = !(pt && !atoi(pt));
+    if (dv->st_proj && ptab_on) CKI(build_proj_tables(dv));
+    if (ptab_on) CKI(build_qkv0_table(dv));
     return codec_finalize(&dv->codec);
 }
 
@@ -651,6 +659,42 @@ static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float
     return a;
 }
 
+// The layer-0 q|k|v table (qtts_dev::qkv0_tab): row r of group g's block is
+// exactly what the per-frame GEMV computes for input id r (same kernel, same
+// arguments but the output row), so reading it is bit-identical.  One
+// batch-1 launch per row at load: (V + (G-2) Vs) launches, ~0.2 s at 1.7B.
+static int build_qkv0_table(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    if (d.G < 2 || d.Ls < 1) return 0;
+    const int QKV = dv->QKVs();
+    const size_t rows = (size_t)d.V + (size_t)(d.G - 2) * d.Vs;
+    const int nid = d.V > d.Vs ? d.V : d.Vs;
+    std::vector<int> io(nid);
+    for (int i = 0; i < nid; ++i) io[i] = i;
+    int *ids = (int *)dalloc(dv, (size_t)nid * 4, true);
+    dv->qkv0_tab = (float *)dalloc(dv, rows * QKV * 4, true);
+    if (!ids || !dv->qkv0_tab) return -1;
+    CK(hipMemcpy(ids, io.data(), (size_t)nid * 4, hipMemcpyHostToDevice));
+    const bool proj = dv->st_proj != nullptr;
+    for (int g = 1; g < d.G; ++g) {
+        GemvArgs a = gv(dv->sl[0].wqkv, QKV, d.Hs, nullptr, d.Hs, nullptr, QKV, 1, EPI_STORE);
+        a.norm_w = dv->sl[0].in; a.eps = d.eps; a.nt = 0;
+        if (proj) a.table_f32 = g == 1 ? dv->codec_ptab : dv->st_ptab + (size_t)(g - 2) * d.Vs * d.Hs;
+        else a.table = g == 1 ? dv->codec_emb : dv->st_emb + (size_t)(g - 2) * d.Vs * d.H;
+        a.ids = ids; a.ids_bstride = 1;
+        const int n = g == 1 ? d.V : d.Vs;
+        float *base = dv->qkv0_tab + (g == 1 ? 0 : (size_t)d.V + (size_t)(g - 2) * d.Vs) * QKV;
+        for (int r = 0; r < n; ++r) {
+            a.ids_off = r;
+            a.y = base + (size_t)r * QKV;
+            CKI(qtts_gemv(a, dv->st));
+        }
+    }
+    CK(hipStreamSynchronize(dv->st));
+    return 0;
+}
+
+
 // Batch split-K (nb >= 2, k_gemvm): the O and down projections of R rows take
 // kz workgroup columns when R / 16 tiles would not fill the chip; they store
 // partials, and the next GEMV that reads the residual adds them (xadd) and
@@ -789,6 +833,10 @@ static int subtalker(qtts_dev *dv) {
             const bool kv_only = g == 0 && l == d.Ls - 1;
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
+            // batch 1, pass g >= 1, layer 0: q|k|v come from the load-time table
+            // by the input id (no GEMV); the gate|up GEMV reads the residual
+            // from the input table row itself
+            const bool tab0 = l == 0 && g >= 1 && nb == 1 && dv->attn_o && dv->qkv0_tab && (!proj || ptab);
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
             AttnArgs t;
@@ -804,8 +852,13 @@ static int subtalker(qtts_dev *dv) {
             // (batch 1 only: at batch 8 / 16 the per-row recompute measured slower than
             // the separate attention + split-K O projection, 98 vs 107 / 132 vs 155
             // audio-s/s, profiles/r01av_bench_batch_attn_o.txt)
+            if (tab0) {
+                t.qkv_tab = dv->qkv0_tab + (g == 1 ? 0 : (size_t)d.V + (size_t)(g - 2) * d.Vs) * QKV;
+                t.tab_ids = src.ids; t.tab_bstride = src.ids_bstride; t.tab_row_sel = src.row_sel;
+                t.tab_rstride = src.ids_rstride; t.tab_off = src.ids_off;
+            }
             if (dv->attn_o && nb == 1) {
-                CKI(pgemv(dv, a, PK_GEMV_SUB));
+                if (!tab0) CKI(pgemv(dv, a, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 ProfScope ps(dv, PK_ATTN, (double)d.Hs * AD * 2);
                 const int rc = qtts_attn_o(t, ly.wo, d.Hs, dv->opart, st);
@@ -829,6 +882,7 @@ static int subtalker(qtts_dev *dv) {
             if (kv_only) break;
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
+            if (tab0) set_src(a);   // the residual is the input table row (x_st was not written)
             if (fused_o) {
                 add_in(a, dv->opart, d.KVs, d.Hs, nb, xb);
             } else if (kzo) {
