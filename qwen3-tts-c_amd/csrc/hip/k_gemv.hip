@@ -358,7 +358,7 @@ __global__ __launch_bounds__(1024) void k_gemv1(GemvArgs a) {
         const int c = 4 * (tid + nthr * i);
         const int cc = c < C ? c : C - 4;
         float4 v = xv[i];
-        if (!trow && a.xadd) {   // residual + the O projection's per-head partials, summed in head order
+        if (a.xadd) {   // residual (x or table row) + the O projection's per-head partials, summed in head order
             float4 sacc = *reinterpret_cast<const float4 *>(a.xadd + cc);
             for (int p = 1; p < a.n_xadd; ++p) {
                 const float4 t = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + cc);
@@ -443,13 +443,13 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         fprintf(stderr, "qtts_gemv: unsupported shape R=%d C=%d nb=%d\n", a.R, a.C, a.nb);
         return -1;
     }
-    if (a.xadd && a.nb == 1 && !(a.C <= 8192 && a.ldx_ok1())) {
-        fprintf(stderr, "qtts_gemv: xadd needs the batch-1 fast path (R=%d C=%d)\n", a.R, a.C);
-        return -1;
-    }
     if (a.nb == 1 && a.ksplit <= 0) {   // the wave-per-row kernel where it covers the shape (k_gemvw.hip)
         const int rc = qtts_gemvw(a, st);
         if (rc != 1) return rc;
+    }
+    if (a.xadd && a.nb == 1 && !(a.C <= 8192 && a.ldx_ok1())) {
+        fprintf(stderr, "qtts_gemv: xadd needs the batch-1 fast path (R=%d C=%d)\n", a.R, a.C);
+        return -1;
     }
     if (a.nb == 1 && a.C <= 8192 && a.ldx_ok1()) {
         int nthr = 256;

@@ -46,7 +46,7 @@ struct GemvArgs {
     int epi = EPI_STORE;
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {
-        if (xadd && (table || table_f32 || ((uintptr_t)xadd & 15) || ld_xadd % 4 || n_xadd < 1)) return false;
+        if (xadd && (((uintptr_t)xadd & 15) || ld_xadd % 4 || n_xadd < 1)) return false;
         if (table) return C % 4 == 0;
         const bool nw_ok = !norm_w || ((uintptr_t)norm_w & 15) == 0;
         if (table_f32) return C % 4 == 0 && ((uintptr_t)table_f32 & 15) == 0 && nw_ok;
