@@ -1,214 +1,11 @@
-// qtts_attn_dev.h - single-workgroup decode attention for one kv head, as a
-// device function: used as the tail of the fused QKV GEMV (k_gemv.hip: the
-// last workgroup to finish a kv head's q/k/v rows runs it) so decode
-// attention costs no kernel of its own.
-//
-// For kv head `kvh` of batch row `r` at position p = pos[r] (n = p + 1 keys):
-//   per-head RMSNorm of q (GPH heads) and k (T.c:150-156), rotate-half RoPE
-//   from the host table (T.c:158-189), k/v of the current token written to
-//   the fp32 cache (T.c:191-196), then for each query head
-//   softmax(q.K^T / sqrt(HD)) V over all n keys (T.c:198-230, K.c:371-378),
-//   in chunks of CH keys merged online (running max / sum, fp32).
-// Thread mapping per chunk: LPK lanes per key for the scores (DPL dims each,
-// float4 loads, GPH dots per K row), one wave per head for the chunk
-// softmax, HD/4 float4 lanes x KG key groups for P.V with an LDS reduction.
+// qtts_attn_dev.h - the sub-talker's short-context decode attention (<= 16
+// keys, GQA 2) as a device function (k_attn_o, k_attn_short in k_attn.hip).
+// (A one-wave-per-head variant without workgroup barriers measured slower,
+// 6.95 vs 6.2 us per k_attn_o launch: the serial per-wave stream of 16 V
+// loads and 8 K loads per lane costs more than the barriers it removes.)
 #pragma once
 #include "qtts_common.h"
 #include "qtts_kernels.h"
-
-template <int HD, int GPH>
-struct AttnWG {
-    static constexpr int LPK = HD >= 32 ? HD / 32 : 1;   // lanes per key
-    static constexpr int DPL = HD / LPK;                  // dims per lane
-    static constexpr int CH = 256 / LPK;                  // keys per chunk
-    static constexpr int D4 = HD / 4;
-    static constexpr int KG = 256 / D4;                   // key groups in P.V
-    static constexpr int NO = GPH * HD;                   // outputs
-    static constexpr int NJ = (NO + 255) / 256;           // outputs per thread
-    static constexpr int NV = (CH + KG - 1) / KG;         // V rows per thread per chunk
-    // LDS pool layout (floats)
-    static constexpr int XN = 0, QK = XN + (GPH + 1) * HD, VV = QK + (GPH + 1) * HD, SC = VV + HD,
-                         ML = SC + GPH * CH, RED = ML + 8, POOL = RED + KG * NO;
-};
-
-// SC1: the q/k/v row was written by other workgroups of this launch with
-// write-through stores; read it with sc1 loads (no acquire fence needed).
-template <int HD, int GPH, bool SC1>
-__device__ __forceinline__ void attn_full_wg(const AttnArgs &a, int kvh, int r, float *pool) {
-    using W = AttnWG<HD, GPH>;
-    constexpr int LPK = W::LPK, DPL = W::DPL, CH = W::CH, D4 = W::D4, KG = W::KG, NO = W::NO, NJ = W::NJ,
-                  NV = W::NV;
-    float *xn = pool + W::XN, *qk = pool + W::QK, *vv = pool + W::VV, *sc = pool + W::SC, *ml = pool + W::ML,
-          *red = pool + W::RED;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int KVD = a.KV * HD;
-    const int p = a.pos ? a.pos[r] : a.pos_const;
-    const int n = p + 1;
-    const float *row = a.qkv + (size_t)r * a.ld_qkv;
-    const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
-    const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
-
-    // ---- prologue: q heads (waves 0..GPH-1), k head (wave GPH), v ----
-    for (int hh = w; hh <= GPH; hh += 4) {
-        const float *src = hh < GPH ? row + (kvh * GPH + hh) * HD : row + a.NH * HD + kvh * HD;
-        const float *nw = hh < GPH ? a.qn_w : a.kn_w;
-        float v[(HD + 63) / 64];
-        float ss = 0.f;
-#pragma unroll
-        for (int j = 0; j < (HD + 63) / 64; ++j) {
-            const int i = lane + 64 * j;
-            v[j] = i < HD ? (SC1 ? ld_sc1(src + i) : src[i]) : 0.f;
-            ss += v[j] * v[j];
-        }
-        ss = wave_sum(ss);
-        const float iv = rms_inv(ss, HD, a.eps);
-#pragma unroll
-        for (int j = 0; j < (HD + 63) / 64; ++j) {
-            const int i = lane + 64 * j;
-            if (i < HD) xn[hh * HD + i] = v[j] * iv * nw[i];
-        }
-    }
-    if (tid < HD) {
-        const float *vp = row + (a.NH + a.KV) * HD + kvh * HD + tid;
-        vv[tid] = SC1 ? ld_sc1(vp) : *vp;
-    }
-    __syncthreads();
-    {
-        const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
-        constexpr int half = HD / 2;
-        for (int i = tid; i < (GPH + 1) * HD; i += 256) {
-            const int e = i % HD, hb = i - e;
-            qk[i] = e < half ? xn[i] * cs[e] - xn[hb + e + half] * sn[e] : xn[i] * cs[e] + xn[hb + e - half] * sn[e];
-        }
-    }
-    __syncthreads();
-    if (tid < HD && !(a.skip && a.skip[r])) {
-        a.kc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = qk[GPH * HD + tid];
-        a.vc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = vv[tid];
-    }
-
-    const float scale = div_rn(1.0f, sqrt_rn((float)HD));
-    const int kl = tid / LPK, ksub = tid - kl * LPK;
-    const int d4 = tid % D4, kg = tid / D4;
-    float M[GPH], L[GPH], acc[NJ];
-#pragma unroll
-    for (int g = 0; g < GPH; ++g) { M[g] = -INFINITY; L[g] = 0.f; }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = 0.f;
-
-    for (int t0 = 0; t0 < n; t0 += CH) {
-        const int t1 = min(n, t0 + CH);
-        // cache loads of the chunk first
-        const int tk = t0 + kl;
-        const bool kld = tk < t1 && tk != p;
-        float4 kreg[DPL / 4];
-        {
-            const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(kld ? tk : 0) * KVD + ksub * DPL);
-#pragma unroll
-            for (int j = 0; j < DPL / 4; ++j) kreg[j] = kld ? kp[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        float4 vreg[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            const int t = t0 + kg + j * KG;
-            const bool ok = kg + j * KG < CH && t < t1 && t != p;
-            vreg[j] = ok ? reinterpret_cast<const float4 *>(Vc + (size_t)t * KVD)[d4] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        // scores
-        {
-            float d[GPH];
-#pragma unroll
-            for (int g = 0; g < GPH; ++g) d[g] = 0.f;
-            if (tk < t1) {
-                float4 kv[DPL / 4];
-#pragma unroll
-                for (int j = 0; j < DPL / 4; ++j)
-                    kv[j] = (tk == p) ? reinterpret_cast<const float4 *>(qk + GPH * HD + ksub * DPL)[j] : kreg[j];
-#pragma unroll
-                for (int g = 0; g < GPH; ++g) {
-                    const float4 *q4 = reinterpret_cast<const float4 *>(qk + g * HD + ksub * DPL);
-                    float s = 0.f;
-#pragma unroll
-                    for (int j = 0; j < DPL / 4; ++j) {
-                        const float4 q = q4[j];
-                        s += q.x * kv[j].x + q.y * kv[j].y + q.z * kv[j].z + q.w * kv[j].w;
-                    }
-                    d[g] = s;
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < GPH; ++g) {
-#pragma unroll
-                for (int o = LPK >> 1; o >= 1; o >>= 1) d[g] += __shfl_xor(d[g], o, 64);
-                if (ksub == 0) sc[g * CH + kl] = tk < t1 ? d[g] * scale : -INFINITY;
-            }
-        }
-        __syncthreads();
-        for (int g = w; g < GPH; g += 4) {
-            float m = -INFINITY;
-            for (int k = lane; k < CH; k += 64) m = fmaxf(m, sc[g * CH + k]);
-            m = wave_max(m);
-            float l = 0.f;
-            for (int k = lane; k < CH; k += 64) {
-                const float e = t0 + k < t1 ? expf(sc[g * CH + k] - m) : 0.f;
-                sc[g * CH + k] = e;
-                l += e;
-            }
-            l = wave_sum(l);
-            if (lane == 0) { ml[2 * g] = m; ml[2 * g + 1] = l; }
-        }
-        __syncthreads();
-        {
-            float4 pv[GPH];
-#pragma unroll
-            for (int g = 0; g < GPH; ++g) pv[g] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int j = 0; j < NV; ++j) {
-                const int k = kg + j * KG;
-                const int t = t0 + k;
-                if (k < CH && t < t1) {
-                    const float4 v4 = (t == p) ? reinterpret_cast<const float4 *>(vv)[d4] : vreg[j];
-#pragma unroll
-                    for (int g = 0; g < GPH; ++g) {
-                        const float pw = sc[g * CH + k];
-                        pv[g].x += pw * v4.x; pv[g].y += pw * v4.y; pv[g].z += pw * v4.z; pv[g].w += pw * v4.w;
-                    }
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < GPH; ++g) reinterpret_cast<float4 *>(red + kg * NO + g * HD)[d4] = pv[g];
-        }
-        __syncthreads();
-        // online merge of the chunk into the running (M, L, acc) per head
-        float an[GPH], ao[GPH];
-#pragma unroll
-        for (int g = 0; g < GPH; ++g) {
-            const float mc = ml[2 * g], lc = ml[2 * g + 1];
-            const float Mn = fmaxf(M[g], mc);
-            ao[g] = expf(M[g] - Mn);
-            an[g] = expf(mc - Mn);
-            L[g] = L[g] * ao[g] + lc * an[g];
-            M[g] = Mn;
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int o = tid + 256 * j;
-            if (o < NO) {
-                float s = 0.f;
-                for (int k = 0; k < KG; ++k) s += red[k * NO + o];
-                const int g = o / HD;
-                acc[j] = acc[j] * ao[g] + s * an[g];
-            }
-        }
-        __syncthreads();   // sc / red / ml are rewritten by the next chunk
-    }
-    float *outr = a.out + (size_t)r * a.ld_out + kvh * GPH * HD;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int o = tid + 256 * j;
-        if (o < NO) outr[o] = acc[j] / L[o / HD];
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Short-context decode attention: n = pos + 1 <= 16 keys (the sub-talker,
