@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     const bf16_t *trow = nullptr;
     const float *xrow = a.x;
     if (a.table || a.table_f32) {
-        const int *ip = a.ids + a.ids_off;
+        const int *ip = a.ids + a.ids_off + blockIdx.y;
         if (a.row_sel) ip += (size_t)a.row_sel[0] * a.ids_rstride;
         const size_t off = (size_t)(*ip) * C;
         if (a.table) trow = a.table + off;
@@ -154,21 +154,22 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
         acc[i] = wave_sum(s);
     }
     if (lane != 0) return;
+    float *y = a.y + blockIdx.y * a.ldy_rep;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         const int r = row0 + w + 4 * i;
         const float v = acc[i];
         switch (a.epi) {
-            case EPI_STORE: a.y[r] = v; break;
-            case EPI_BIAS: a.y[r] = v + a.bias[r]; break;
+            case EPI_STORE: y[r] = v; break;
+            case EPI_BIAS: y[r] = v + a.bias[r]; break;
             case EPI_BIAS_SILU: {
                 const float z = v + a.bias[r];
-                a.y[r] = z / (1.0f + expf(-z));
+                y[r] = z / (1.0f + expf(-z));
                 break;
             }
-            case EPI_RESID: a.y[r] += v; break;
+            case EPI_RESID: y[r] += v; break;
             case EPI_SWIGLU:
-                if ((i & 1) == 0 && i + 1 < RW) a.y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * acc[i + 1];
+                if ((i & 1) == 0 && i + 1 < RW) y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * acc[i + 1];
                 break;
         }
     }
@@ -182,6 +183,7 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
 // lane would not fit one workgroup per CU.
 int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
     if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart) return 1;
+    if (a.reps < 1 || a.reps > 65535 || (a.reps > 1 && (!a.ids || a.xadd || a.xcopy || a.row_sel))) return 1;
     // sources: an fp32 row, a bf16 / fp32 table row (+ per-head partials too:
     // the sub-talker's layer-0 gate|up reads its residual from the table)
     if (a.xadd && (((uintptr_t)a.xadd & 15) || a.ld_xadd % 4 || a.n_xadd < 1)) return 1;
@@ -192,7 +194,7 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
     int RW = a.R / 1024;
     if (RW * NV > 16 && a.R % 2048 == 0) RW = a.R / 2048;   // two workgroups per CU
     if (RW * NV > 24 || (a.epi == EPI_SWIGLU && (RW & 1))) return 1;
-    const dim3 grid(a.R / (4 * RW));
+    const dim3 grid(a.R / (4 * RW), a.reps);
     const size_t smem = (size_t)(a.C + 4) * sizeof(float);
 #define QTTS_GW(RW_, NV_)                                                                              \
     if (RW == RW_ && NV == NV_) {                                                                      \

@@ -22,6 +22,10 @@ struct GemvArgs {
     const int *ids = nullptr;       // id(b) = ids[b*ids_bstride + row_sel[b]*ids_rstride + ids_off]
     int ids_bstride = 1, ids_rstride = 0, ids_off = 0;
     const int *row_sel = nullptr;
+    // lean kernel (qtts_gemvw) only: reps consecutive ids in one launch
+    // (grid.y), rep j reads id ids[ids_off + j] and writes y + j * ldy_rep
+    int reps = 1;
+    size_t ldy_rep = 0;
     // prologue
     // batch-1 prologue only: x += sum_p xadd[p*ld_xadd + c] (p < n_xadd, summed
     // in order first) -- the O projection's per-head partials (qtts_attn_o)

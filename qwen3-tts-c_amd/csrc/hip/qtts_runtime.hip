@@ -660,9 +660,10 @@ static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float
 }
 
 // The layer-0 q|k|v table (qtts_dev::qkv0_tab): row r of group g's block is
-// exactly what the per-frame GEMV computes for input id r (same kernel, same
-// arguments but the output row), so reading it is bit-identical.  One
-// batch-1 launch per row at load: (V + (G-2) Vs) launches, ~0.2 s at 1.7B.
+// exactly what the per-frame GEMV computes for input id r (same lean kernel,
+// same arguments but the output row), so reading it is bit-identical.  One
+// launch per group, the ids on grid.y (GemvArgs::reps); a per-row launch for
+// each of ~32k ids took ~0.2 s and crashed rocprofv3's counter collection.
 static int build_qkv0_table(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     if (d.G < 2 || d.Ls < 1) return 0;
@@ -682,8 +683,17 @@ static int build_qkv0_table(qtts_dev *dv) {
         if (proj) a.table_f32 = g == 1 ? dv->codec_ptab : dv->st_ptab + (size_t)(g - 2) * d.Vs * d.Hs;
         else a.table = g == 1 ? dv->codec_emb : dv->st_emb + (size_t)(g - 2) * d.Vs * d.H;
         a.ids = ids; a.ids_bstride = 1;
-        const int n = g == 1 ? d.V : d.Vs;
-        float *base = dv->qkv0_tab + (g == 1 ? 0 : (size_t)d.V + (size_t)(g - 2) * d.Vs) * QKV;
+        a.reps = g == 1 ? d.V : d.Vs;
+        a.ldy_rep = QKV;
+        a.y = dv->qkv0_tab + (g == 1 ? 0 : (size_t)d.V + (size_t)(g - 2) * d.Vs) * QKV;
+        const int rc = qtts_gemvw(a, dv->st);
+        if (rc < 0) return -1;
+        if (rc == 0) continue;
+        // shapes the lean kernel does not cover (small test models): the
+        // per-frame path runs k_gemv1, so the table does too, one row a launch
+        const int n = a.reps;
+        float *base = a.y;
+        a.reps = 1;
         for (int r = 0; r < n; ++r) {
             a.ids_off = r;
             a.y = base + (size_t)r * QKV;

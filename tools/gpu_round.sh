@@ -13,6 +13,11 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+# keep the merge-back under gpurun's 64 MiB (raw per-dispatch traces are only
+# needed for the summaries) and show where a failing call stopped
+trim() { rc=$?; find $O -name '*.csv' -size +4M -delete; for f in gpu_tests.log prof_bench.err bench.err; do
+  [ -f $O/$f ] && { echo "== $f"; tail -n 15 $O/$f; }; done; exit $rc; }
+trap trim EXIT
 if [ "$MODE" = dist ]; then
   QTTS_BENCH_BACKEND=gloo timeout -k 10 900 python bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline \
     --no-profile > $O/dist2.json 2> $O/dist2.err
