@@ -11,6 +11,14 @@ reference loader binds (c/qwen_tts.c:433-769) and the config keys it parses
     <dir>/speech_tokenizer/config.json         decoder_config.*
     <dir>/speech_tokenizer/model.safetensors   decoder.* tensors (F32)
 
+Presets with voice-clone encoders ("enc" below: tiny_vc, 0.6b, 1.7b) add
+    <dir>/model-speaker.safetensors            speaker_encoder.* (BF16, the model dtype)
+    <dir>/speech_tokenizer/model-encoder.safetensors   encoder.* (F32)
+and the `speaker_encoder_config` / `encoder_config` keys (modeling_qwen3_tts.py
+:311-393 ECAPA-TDNN, configuration_qwen3_tts.py:47-67; the 12 Hz tokenizer's
+MimiModel encoder, configuration_qwen3_tts_tokenizer_v2.py:139-169).  They are
+extra shards, so the tiny_vc talker/codec files are byte-identical to tiny's.
+
 Shapes ("synth-0.6b", "synth-1.7b") follow SURVEY.md section 8 header; the
 values marked there as not present in the reference (1.7B dims, I=3072 for
 0.6B, mrope_section) are assumptions of this generator.
@@ -54,13 +62,22 @@ PRESETS = {
         c_inter=128, c_window=72, c_dec=64, c_cb=2048, c_q=16,
         eos_gain=1.0,
     ),
+    # tiny + voice-clone encoders (ECAPA-TDNN speaker encoder, Mimi encoder)
+    "tiny_vc": dict(
+        H=128, I=256, L=2, NH=4, KV=2, HD=32, TH=64, TV=151936, V=3072, G=16,
+        Hs=64, Is=128, Ls=2, NHs=4, KVs=2, HDs=16, Vs=2048,
+        rope_theta=1000000.0, mrope=[8, 4, 4],
+        c_hidden=64, c_latent=128, c_cbdim=64, c_layers=2, c_heads=4, c_kv=4,
+        c_inter=128, c_window=72, c_dec=64, c_cb=2048, c_q=16,
+        eos_gain=1.0, enc="tiny",
+    ),
     "0.6b": dict(
         H=1024, I=3072, L=28, NH=16, KV=8, HD=128, TH=2048, TV=151936, V=3072, G=16,
         Hs=1024, Is=3072, Ls=5, NHs=16, KVs=8, HDs=128, Vs=2048,
         rope_theta=1000000.0, mrope=[24, 20, 20],
         c_hidden=1024, c_latent=1024, c_cbdim=512, c_layers=8, c_heads=16, c_kv=16,
         c_inter=3072, c_window=72, c_dec=1536, c_cb=2048, c_q=16,
-        eos_gain=1.0,
+        eos_gain=1.0, enc="full",
     ),
     "1.7b": dict(
         H=2048, I=6144, L=28, NH=16, KV=8, HD=128, TH=2048, TV=151936, V=3072, G=16,
@@ -68,9 +85,127 @@ PRESETS = {
         rope_theta=1000000.0, mrope=[24, 20, 20],
         c_hidden=1024, c_latent=1024, c_cbdim=512, c_layers=8, c_heads=16, c_kv=16,
         c_inter=3072, c_window=72, c_dec=1536, c_cb=2048, c_q=16,
-        eos_gain=1.0,
+        eos_gain=1.0, enc="full",
     ),
 }
+
+# Voice-clone encoders.  "full" = the reference defaults
+# (Qwen3TTSSpeakerEncoderConfig, configuration_qwen3_tts.py:47-57, enc_dim =
+# the talker hidden the x-vector is added to; MimiConfig defaults, which the
+# 12 Hz tokenizer's 1920-sample frame implies: 8*6*5*4 * 2 = 1920).
+ENC = {
+    "tiny": dict(spk=dict(mel_dim=128, enc_channels=[32, 32, 32, 32, 96], enc_kernel_sizes=[5, 3, 3, 3, 1],
+                          enc_dilations=[1, 2, 3, 4, 1], enc_attention_channels=16, enc_res2net_scale=8,
+                          enc_se_channels=16),
+                 mimi=dict(hidden_size=64, num_filters=8, num_hidden_layers=2, num_attention_heads=4,
+                           num_key_value_heads=4, head_dim=16, intermediate_size=128, sliding_window=16,
+                           num_quantizers=20, codebook_size=2048, codebook_dim=32,
+                           vector_quantization_hidden_dimension=32)),
+    "full": dict(spk=dict(mel_dim=128, enc_channels=[512, 512, 512, 512, 1536], enc_kernel_sizes=[5, 3, 3, 3, 1],
+                          enc_dilations=[1, 2, 3, 4, 1], enc_attention_channels=128, enc_res2net_scale=8,
+                          enc_se_channels=128),
+                 mimi=dict(hidden_size=512, num_filters=64, num_hidden_layers=8, num_attention_heads=8,
+                           num_key_value_heads=8, head_dim=64, intermediate_size=2048, sliding_window=250,
+                           num_quantizers=32, codebook_size=2048, codebook_dim=256,
+                           vector_quantization_hidden_dimension=256)),
+}
+MIMI_FIXED = dict(sampling_rate=24000, frame_rate=12.5, audio_channels=1, upsampling_ratios=[8, 6, 5, 4],
+                  kernel_size=7, last_kernel_size=3, residual_kernel_size=3, dilation_growth_rate=2,
+                  num_residual_layers=1, compress=2, use_causal_conv=True, pad_mode="constant",
+                  trim_right_ratio=1.0, use_conv_shortcut=False, num_semantic_quantizers=1,
+                  norm_eps=1e-5, rope_theta=10000.0, hidden_act="gelu", layer_scale_initial_scale=0.01,
+                  max_position_embeddings=8000, upsample_groups=512, attention_bias=False)
+
+
+def enc_configs(p):
+    e = ENC[p["enc"]]
+    spk = dict(e["spk"], enc_dim=p["H"], sample_rate=24000)
+    mimi = dict(MIMI_FIXED, **e["mimi"])
+    mimi["upsample_groups"] = min(mimi["upsample_groups"], mimi["hidden_size"])   # decoder half only
+    return spk, mimi
+
+
+def speaker_specs(p):
+    """speaker_encoder.* (Qwen3TTSSpeakerEncoder, modeling_qwen3_tts.py:311-393)."""
+    c, _ = enc_configs(p)
+    ch, ks = c["enc_channels"], c["enc_kernel_sizes"]
+    S = []
+
+    def conv(name, co, ci, k, gain=1.4):
+        S.append((name + ".weight", (co, ci, k), "conv", gain))
+        S.append((name + ".bias", (co,), "bias", 0.02))
+
+    P = "speaker_encoder."
+    conv(P + "blocks.0.conv", ch[0], c["mel_dim"], ks[0], 0.5)
+    sc = c["enc_res2net_scale"]
+    for i in range(1, len(ch) - 1):
+        b = f"{P}blocks.{i}."
+        conv(b + "tdnn1.conv", ch[i], ch[i - 1], 1)
+        for j in range(sc - 1):
+            conv(f"{b}res2net_block.blocks.{j}.conv", ch[i] // sc, ch[i] // sc, ks[i])
+        conv(b + "tdnn2.conv", ch[i], ch[i], 1)
+        conv(b + "se_block.conv1", c["enc_se_channels"], ch[i], 1)
+        conv(b + "se_block.conv2", ch[i], c["enc_se_channels"], 1)
+    conv(P + "mfa.conv", ch[-1], ch[-1], ks[-1])
+    conv(P + "asp.tdnn.conv", c["enc_attention_channels"], ch[-1] * 3, 1)
+    conv(P + "asp.conv", ch[-1], c["enc_attention_channels"], 1, 2.0)
+    conv(P + "fc", c["enc_dim"], ch[-1] * 2, 1, 1.0)
+    return S
+
+
+def mimi_encoder_specs(p):
+    """encoder.* of the 12 Hz tokenizer (MimiModel without its decoder half,
+    modeling_qwen3_tts_tokenizer_v2.py:899-908)."""
+    _, m = enc_configs(p)
+    S = []
+
+    def conv(name, co, ci, k, gain=1.0, bias=True):
+        S.append((name + ".weight", (co, ci, k), "conv", gain))
+        if bias:
+            S.append((name + ".bias", (co,), "bias", 0.02))
+
+    P = "encoder.encoder.layers."
+    nf = m["num_filters"]
+    conv(P + "0.conv", nf, 1, m["kernel_size"], 1.0)
+    li, scale = 1, 1
+    for r in reversed(m["upsampling_ratios"]):
+        d = scale * nf
+        conv(f"{P}{li}.block.1.conv", d // m["compress"], d, m["residual_kernel_size"], 1.2)
+        conv(f"{P}{li}.block.3.conv", d, d // m["compress"], 1, 0.6)
+        li += 2
+        conv(f"{P}{li}.conv", 2 * d, d, 2 * r, 1.2)
+        li += 1
+        scale *= 2
+    li += 1
+    conv(f"{P}{li}.conv", m["hidden_size"], scale * nf, m["last_kernel_size"], 1.2)
+    hid, nh, nkv, hd, I = (m["hidden_size"], m["num_attention_heads"], m["num_key_value_heads"], m["head_dim"],
+                           m["intermediate_size"])
+    for l in range(m["num_hidden_layers"]):
+        q = f"encoder.encoder_transformer.layers.{l}."
+        S.append((q + "input_layernorm.weight", (hid,), "norm", 0.05))
+        S.append((q + "input_layernorm.bias", (hid,), "bias", 0.02))
+        S.append((q + "post_attention_layernorm.weight", (hid,), "norm", 0.05))
+        S.append((q + "post_attention_layernorm.bias", (hid,), "bias", 0.02))
+        S.append((q + "self_attn.q_proj.weight", (nh * hd, hid), "lin", 1.0))
+        S.append((q + "self_attn.k_proj.weight", (nkv * hd, hid), "lin", 1.0))
+        S.append((q + "self_attn.v_proj.weight", (nkv * hd, hid), "lin", 1.0))
+        S.append((q + "self_attn.o_proj.weight", (hid, nh * hd), "lin", 1.0))
+        S.append((q + "mlp.fc1.weight", (I, hid), "lin", 1.0))
+        S.append((q + "mlp.fc2.weight", (hid, I), "lin", 1.0))
+        S.append((q + "self_attn_layer_scale.scale", (hid,), "lscale", 0))
+        S.append((q + "mlp_layer_scale.scale", (hid,), "lscale", 0))
+    conv("encoder.downsample.conv", hid, hid, 4, 1.0, bias=False)
+    vq, cb = m["vector_quantization_hidden_dimension"], m["codebook_size"]
+    nsem = m["num_semantic_quantizers"]
+    for kind, n in (("semantic", nsem), ("acoustic", m["num_quantizers"] - nsem)):
+        q = f"encoder.quantizer.{kind}_residual_vector_quantizer."
+        S.append((q + "input_proj.weight", (vq, hid, 1), "conv", 1.0))
+        S.append((q + "output_proj.weight", (hid, vq, 1), "conv", 1.0))
+        for i in range(n):
+            S.append((f"{q}layers.{i}.codebook.initialized", (1,), "one", 0))
+            S.append((f"{q}layers.{i}.codebook.cluster_usage", (cb,), "usage", 0))
+            S.append((f"{q}layers.{i}.codebook.embed_sum", (cb, vq), "esum", 1.0 if i == 0 else 0.6))
+    return S
 
 SPEAKERS = {"aiden": 2900, "serena": 2901, "vivian": 2902}
 LANGUAGES = {"english": 2050, "chinese": 2055, "japanese": 2058}
@@ -298,6 +433,8 @@ def make_tensor(seed, name, shape, kind, gain, p):
         return np.float32(0.05) + rng.random(shape, dtype=np.float32) * np.float32(0.1)
     if kind == "snake":
         return _uniform(rng, shape, 0.1)
+    if kind == "one":
+        return np.ones(shape, dtype=np.float32)
     raise ValueError(kind)
 
 
@@ -337,15 +474,23 @@ def write_model(out, preset="tiny", seed=0, overrides=None, quiet=False):
             "upsample_rates": [8, 5, 4, 3], "upsampling_ratios": [2, 2],
         }
     }
+    files = [(os.path.join(out, "model.safetensors"), talker_specs(p)),
+             (os.path.join(out, "speech_tokenizer", "model.safetensors"), codec_specs(p))]
+    if p.get("enc"):
+        spk, mimi = enc_configs(p)
+        cfg["speaker_encoder_config"] = spk
+        ccfg.update({"encoder_config": mimi, "encoder_valid_num_quantizers": 16, "input_sample_rate": 24000,
+                     "output_sample_rate": 24000, "encode_downsample_rate": 1920, "decode_upsample_rate": 1920})
+        files += [(os.path.join(out, "model-speaker.safetensors"), speaker_specs(p)),
+                  (os.path.join(out, "speech_tokenizer", "model-encoder.safetensors"), mimi_encoder_specs(p))]
     with open(os.path.join(out, "config.json"), "w") as f:
         json.dump(cfg, f, indent=1)
     with open(os.path.join(out, "speech_tokenizer", "config.json"), "w") as f:
         json.dump(ccfg, f, indent=1)
 
-    for path, specs in ((os.path.join(out, "model.safetensors"), talker_specs(p)),
-                        (os.path.join(out, "speech_tokenizer", "model.safetensors"), codec_specs(p))):
+    for path, specs in files:
         codec = "speech_tokenizer" in path
-        sp = [(n, "F32" if (codec or k == "usage") else "BF16", s) for n, s, k, g in specs]
+        sp = [(n, "F32" if (codec or k in ("usage", "one")) else "BF16", s) for n, s, k, g in specs]
         w = StWriter(path + ".tmp", sp)
         for n, s, k, g in specs:
             if not quiet and np.prod(s) > (1 << 24):
@@ -359,7 +504,10 @@ def write_model(out, preset="tiny", seed=0, overrides=None, quiet=False):
 def ensure_model(out, preset="tiny", seed=0, overrides=None):
     """Create the model dir unless an identical one (same preset/seed) exists."""
     stamp = os.path.join(out, ".synth_stamp")
-    want = json.dumps({"preset": preset, "seed": seed, "overrides": overrides or {}}, sort_keys=True)
+    key = {"preset": preset, "seed": seed, "overrides": overrides or {}}
+    if PRESETS[preset].get("enc"):
+        key["encoders"] = 1
+    want = json.dumps(key, sort_keys=True)
     if not (os.path.exists(stamp) and open(stamp).read() == want):
         write_model(out, preset, seed, overrides, quiet=True)
         with open(stamp, "w") as f:
