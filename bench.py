@@ -292,8 +292,11 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--model-dir", default=None)
     ap.add_argument("--voice-clone", action="store_true",
-                    help="BASELINE C5: ICL voice clone (63 synthetic reference frames + reference text + x-vector "
-                         "per utterance; the audio encoders are out of scope), decode of reference ++ generated")
+                    help="BASELINE C5: ICL voice clone from 5 s of synthetic reference AUDIO per utterance "
+                         "(12 Hz encoder + speaker encoder on the GPU, inside the timed step) + reference text, "
+                         "decode of reference ++ generated")
+    ap.add_argument("--vc-codes", action="store_true",
+                    help="with --voice-clone: start from seeded reference codes + x-vector (no audio encode)")
     ap.add_argument("--c1", action="store_true",
                     help="BASELINE C1 only: the reference c/ CLI on the 0.6B synthetic model, short prompt "
                          "(test/tokens_great_power.txt), on the host cores; no GPU")
@@ -333,19 +336,34 @@ def main():
     prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
 
     vc = None
+    wavs = None
     if args.voice_clone:
-        # 5 s of reference audio = 63 frames at 12.5 Hz, seeded codes; reference
-        # text = chat template around 20 seeded ids; x-vector of the talker width
+        # 5 s of reference audio (63 frames at 12.5 Hz); reference
+        # text = chat template around 20 seeded ids.  Default: the audio itself,
+        # encoded on the GPU inside the step; --vc-codes: seeded codes + x-vector
         import numpy as np
+        from synth_model import ref_wave
         H = m.cfg.talker_hidden
         vc = []
+        wavs = []
         for i, sd in enumerate(rank_prompt_seeds(rank, args.batch)):
             r = np.random.default_rng(sd + 7)
             codes = r.integers(0, 2048, size=(63, m.cfg.num_code_groups)).astype(np.int32)
             rids = [151644, 77091, 198] + r.integers(1000, 100000, size=20).tolist() + [151645, 198]
             vc.append((rids, codes, (r.standard_normal(H) * 0.05).astype(np.float32)))
+            wavs.append(ref_wave(sd + 7, 5.0))
+        if args.vc_codes:
+            wavs = None
+        elif m.encoders_available() != 3:
+            raise SystemExit("bench.py --voice-clone: the model dir has no audio encoders (use --vc-codes)")
 
     def one_step():
+        if wavs is not None:
+            rc, aud = m.generate_voice_clone_audio_batch(prompts, wavs, [v[0] for v in vc],
+                                                         ["english"] * args.batch)
+            if rc != 0:
+                raise RuntimeError("voice-clone (reference audio) generation failed")
+            return sum(len(a) for a in aud)
         if vc is not None:
             rc, aud = m.generate_voice_clone_batch(prompts, [v[0] for v in vc], [v[1] for v in vc],
                                                    [v[2] for v in vc], ["english"] * args.batch)
@@ -400,6 +418,26 @@ def main():
                   first_packet_samples=int(len(first[0])) if first else 0, stream_chunk_frames=8,
                   prefill_ms=prefill_ms, talker_ms=talker_ms, codec_ms=codec_ms)
 
+    enc = None
+    if wavs is not None:
+        # the reference-audio encode of one step alone (both encoders, whole batch)
+        m.speaker_embed(wavs)
+        m.encode_audio(wavs)
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(3):
+            m.speaker_embed(wavs)
+        ts = time.perf_counter()
+        for _ in range(3):
+            m.encode_audio(wavs)
+        tc = time.perf_counter()
+        gf = encoder_gflop(md, [w.shape[0] for w in wavs])
+        spk_ms, cod_ms = (ts - te) / 3 * 1e3, (tc - ts) / 3 * 1e3
+        enc = dict(speaker_ms=round(spk_ms, 3), codes_ms=round(cod_ms, 3), ref_seconds=5.0, batch=len(wavs),
+                   speaker_gflop=round(gf[0], 2), codes_gflop=round(gf[1], 2),
+                   speaker_tflops=round(gf[0] / spk_ms, 2), codes_tflops=round(gf[1] / cod_ms, 2),
+                   note="wall time of the encoder call (host waveform in, host codes / x-vectors out), "
+                        "dense-contraction GFLOP counted per SURVEY.md 8f N3 shapes")
     if args.batch == 1 and vc is not None:
         # voice-clone first packet: reference frames through the streaming codec, then frame 0
         for _ in range(2):   # second request, as for the custom-voice line
@@ -434,8 +472,11 @@ def main():
             "data": "synthetic (seeded random-init weights of the 1.7B architecture, tools/synth_model.py)",
             "config": {"workload": f"Qwen3-TTS-{args.preset} synthetic, P128 prompt, fixed {args.frames} frames "
                                    f"({args.frames * 0.08:.2f} s audio), default sampling, batch {args.batch} per GPU"
-                                   + (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, "
-                                      "codec over reference ++ generated (reference part cut)" if vc else ""),
+                                   + ((", ICL voice clone from 5 s reference audio (12 Hz codes + x-vector encoded "
+                                       "on the GPU inside the step) + 20-id reference text, codec over reference ++ "
+                                       "generated (reference part cut)") if wavs is not None else
+                                      (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, "
+                                       "codec over reference ++ generated (reference part cut)") if vc else ""),
                        "global_batch": args.batch * ws, "frames": args.frames,
                        "parallelism": f"dp{ws} (independent replicas, no collective in the data path)"},
         }
@@ -443,6 +484,8 @@ def main():
             out["first_packet_ms"] = round(fp["first_packet_ms"], 2)
             out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in fp.items()}
         out["ranks"] = ranks
+        if enc:
+            out["ref_audio_encode"] = enc
         fw = FRAME_WEIGHT_BYTES.get(args.preset)
         if fw and vc is None:
             # §8(d) headline: utterance-frames per second x algorithmic bytes per
@@ -487,6 +530,43 @@ def main():
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def encoder_gflop(md, lens):
+    """Dense-contraction GFLOP of the voice-clone encoders (2 flop per MAC) for
+    reference waveforms of `lens` samples: (speaker encoder incl. the STFT,
+    12 Hz encoder incl. the codebook distances)."""
+    cfg = json.load(open(os.path.join(md, "config.json"))).get("speaker_encoder_config", {})
+    mc = json.load(open(os.path.join(md, "speech_tokenizer", "config.json"))).get("encoder_config", {})
+    ch, ks = cfg.get("enc_channels", [512, 512, 512, 512, 1536]), cfg.get("enc_kernel_sizes", [5, 3, 3, 3, 1])
+    sc, att, se = cfg.get("enc_res2net_scale", 8), cfg.get("enc_attention_channels", 128), cfg.get("enc_se_channels", 128)
+    spk = cod = 0.0
+    for n in lens:
+        T = (n - 256) // 256 + 1
+        macs = 1026 * 1024 * T + 128 * 513 * T                        # STFT basis + mel
+        macs += ch[0] * 128 * ks[0] * T
+        for i in range(1, len(ch) - 1):
+            macs += 2 * ch[i] * ch[i - 1] * T + (sc - 1) * (ch[i] // sc) ** 2 * ks[i] * T + 2 * se * ch[i]
+        macs += ch[-1] * ch[-1] * T + att * 3 * ch[-1] * T + ch[-1] * att * T + 2 * ch[-1] * cfg.get("enc_dim", 2048)
+        spk += 2 * macs
+        nf, hid = mc.get("num_filters", 64), mc.get("hidden_size", 512)
+        L, C = n, nf
+        macs = nf * 7 * L
+        for r in reversed(mc.get("upsampling_ratios", [8, 6, 5, 4])):
+            macs += (C // 2) * C * 3 * L + C * (C // 2) * L
+            L = -(-L // r)
+            macs += 2 * C * C * 2 * r * L
+            C *= 2
+        macs += hid * C * 3 * L
+        I = mc.get("intermediate_size", 2048)
+        qd = mc.get("num_attention_heads", 8) * mc.get("head_dim", 64)
+        w = min(L, mc.get("sliding_window", 250))
+        macs += mc.get("num_hidden_layers", 8) * L * (4 * hid * qd + 2 * hid * I + 2 * qd * w)
+        T12 = -(-L // 2)
+        vq = mc.get("vector_quantization_hidden_dimension", 256)
+        macs += hid * hid * 4 * T12 + 2 * vq * hid * T12 + 16 * T12 * mc.get("codebook_size", 2048) * vq
+        cod += 2 * macs
+    return spk / 1e9, cod / 1e9
 
 
 def c1_line(args):

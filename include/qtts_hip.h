@@ -45,6 +45,22 @@ typedef struct {
     int pad_id, bos_id, eos_id;
 } qtts_dims_t;
 
+/* Voice-clone encoder dimensions: config.json
+ * `speaker_encoder_config` (Qwen3TTSSpeakerEncoderConfig,
+ * configuration_qwen3_tts.py:47-67) and speech_tokenizer/config.json
+ * `encoder_config` (transformers MimiConfig) + `encoder_valid_num_quantizers`. */
+typedef struct {
+    /* speaker encoder (ECAPA-TDNN) */
+    int mel_dim, enc_dim, n_ch;              /* n_ch = len(enc_channels), 3..8 */
+    int ch[8], ks[8], dil[8];
+    int att_ch, res2net_scale, se_ch;
+    /* 12 Hz tokenizer encoder (Mimi) */
+    int hidden, n_filters, ratios[4], kernel, last_kernel, res_kernel, dil_growth, n_res, compress;
+    int layers, heads, kv_heads, head_dim, inter, window;
+    int n_q, n_sem, cb_size, vq_dim, n_valid;
+    float norm_eps, rope_theta;
+} qtts_enc_dims_t;
+
 /* Generation parameters (qwen_tts_ctx_t fields, c/qwen_tts.h:420-430). */
 typedef struct {
     float temperature, top_p, repetition_penalty;
@@ -134,6 +150,26 @@ int qtts_dev_codec_stream_push_host(qtts_dev_t *dev, const int *codes, int T, fl
 int qtts_dev_codec_async_begin(qtts_dev_t *dev, int max_frames);
 int qtts_dev_codec_async_push(qtts_dev_t *dev, int b, int frame0, int T);
 int qtts_dev_codec_async_end(qtts_dev_t *dev, float *host_out, int frames);
+
+/* ---- voice-clone audio encoders (no c/ counterpart) ---- */
+/* Encoder dimensions; call before the encoder tensors are put (speaker_encoder.*
+ * of the model dir, encoder.* of speech_tokenizer/). */
+int qtts_dev_enc_config(qtts_dev_t *dev, const qtts_enc_dims_t *dims);
+/* bit 0: the speaker encoder is loaded, bit 1: the 12 Hz encoder is loaded */
+int qtts_dev_enc_available(qtts_dev_t *dev);
+/* Speaker x-vectors (extract_speaker_embedding, modeling_qwen3_tts.py:1941-1954)
+ * of nb <= 16 host waveforms at 24 kHz (n[b] samples, > 384 each):
+ * out[nb][enc_dim] host floats.  mel_out (optional) receives each utterance's
+ * [128][T_b] log-mel back to back, T_b = (n[b] - 256) / 256 + 1. */
+int qtts_dev_speaker_embed(qtts_dev_t *dev, int nb, const float *const *wav, const int *n, float *out,
+                           float *mel_out);
+/* 12 Hz reference codes (Qwen3TTSTokenizer.encode, qwen3_tts_tokenizer.py:208-257,
+ * modeling_qwen3_tts_tokenizer_v2.py:961-991) of nb <= 16 host waveforms at
+ * 24 kHz, zero-padded to the longest as the tokenizer's batch encode does:
+ * codes[nb][max_frames][16] (host ints), frames[b] = ceil(n[b] / 1920).
+ * latent (optional): [nb][hidden][max_frames] pre-quantizer embeddings. */
+int qtts_dev_encode_audio(qtts_dev_t *dev, int nb, const float *const *wav, const int *n, int *codes,
+                          int max_frames, int *frames, float *latent);
 
 /* ---- host-pointer stage wrappers (oracle-level tests, c/qwen_tts.h:483-502) ---- */
 int qtts_dev_talker_prefill_host(qtts_dev_t *dev, const float *embeds, int n, float *hidden_out);

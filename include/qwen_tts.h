@@ -15,8 +15,9 @@
  *                        NULL and *out_samples = 0 on error
  *   qwen_tts_write_wav   0 / -1
  *
- * MI355X additions (not in the reference): qwen_tts_set_device,
- * qwen_tts_generate_batch, qwen_tts_last_codes.
+ * MI355X additions (not in the c/ reference): qwen_tts_set_device,
+ * qwen_tts_generate_batch, qwen_tts_last_codes, streaming, text input, and
+ * the Python reference's voice clone (codes / x-vector or reference audio).
  */
 #ifndef QWEN_TTS_H
 #define QWEN_TTS_H
@@ -238,6 +239,34 @@ int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char 
                                         const int *n_ref_frames, const float *const *spk_embeds,
                                         const char *const *languages, int non_streaming, float **out_audio,
                                         int *out_samples);
+/* Voice clone from reference AUDIO (the Python reference's
+ * create_voice_clone_prompt, qwen3_tts_model.py:356-458, on the device).
+ * Waveforms are mono float PCM at 24 kHz (the reference resamples other rates
+ * with librosa first; this library takes 24 kHz only).  The model directory
+ * must hold the speaker encoder (speaker_encoder.* + speaker_encoder_config)
+ * and the 12 Hz tokenizer encoder (speech_tokenizer/ encoder.* +
+ * encoder_config).
+ * qwen_tts_speaker_embedding: the x-vector of extract_speaker_embedding
+ *   (modeling_qwen3_tts.py:1941-1954: 128-bin log-mel, ECAPA-TDNN), malloc'd
+ *   [talker hidden] floats, *out_dim set; NULL on error (> 384 samples needed).
+ * qwen_tts_encode_audio: the 12 Hz codes of Qwen3TTSTokenizer.encode
+ *   (modeling_qwen3_tts_tokenizer_v2.py:961-991: Mimi encoder, first 16
+ *   codebooks), malloc'd [ceil(n / 1920)][16] ints, *out_frames set.
+ * qwen_tts_generate_voice_clone_audio[_batch]: encode (all references in one
+ *   zero-padded batch, as the tokenizer does) + qwen_tts_generate_voice_clone
+ *   [_batch]; ICL mode needs ref_text, x_vector_only drops the codes.
+ * All return NULL / -1 on error with a message on stderr; buffers are the
+ * caller's to free(). */
+float *qwen_tts_speaker_embedding(qwen_tts_ctx_t *ctx, const float *wav, int n_samples, int *out_dim);
+int *qwen_tts_encode_audio(qwen_tts_ctx_t *ctx, const float *wav, int n_samples, int *out_frames);
+float *qwen_tts_generate_voice_clone_audio(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                           const float *ref_wav, int n_ref_samples, const char *language,
+                                           int x_vector_only, int non_streaming, int *out_samples);
+int qwen_tts_generate_voice_clone_audio_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts,
+                                              const char *const *ref_texts, const float *const *ref_wavs,
+                                              const int *n_ref_samples, const char *const *languages,
+                                              const int *x_vector_only, int non_streaming, float **out_audio,
+                                              int *out_samples);
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);

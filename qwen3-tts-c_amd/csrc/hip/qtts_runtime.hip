@@ -29,6 +29,7 @@
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 #include "qtts_codec.h"
+#include "qtts_enc.h"
 #include "../../../include/qtts_hip.h"
 
 #define CK(x)                                                                                              \
@@ -94,6 +95,8 @@ struct qtts_dev {
     float *qkv0_tab = nullptr;
     // codec
     CodecModel codec;
+    // voice-clone encoders (speaker x-vector, 12 Hz reference codes)
+    EncModel enc;
     // rope
     float *rope_cos = nullptr, *rope_sin = nullptr, *rope_cos_s = nullptr, *rope_sin_s = nullptr;
     int rope_max = 0;
@@ -280,6 +283,9 @@ extern "C" int qtts_dev_put_tensor(qtts_dev_t *dv, const char *cname, const void
     for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
     const qtts_dims_t &d = dv->d;
     int rc = 0, idx;
+    const int er = enc_put_tensor(&dv->enc, name, host, dtype, shape, ndim, n);
+    if (er < 0) { fprintf(stderr, "qtts: failed to take encoder tensor %s\n", cname); return -1; }
+    if (er > 0) return 0;
     if (name.compare(0, 8, "decoder.") == 0) {
         rc = codec_put_tensor(&dv->codec, name, host, dtype, shape, ndim, n);
     } else if (name == "talker.model.codec_embedding.weight") {
@@ -351,6 +357,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
     codec_init(&dv->codec, dims, dv->st);
+    dv->enc.st = dv->st;
+    dv->enc.device = device;
     return dv;
 }
 
@@ -360,6 +368,7 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
     hipStreamSynchronize(dv->st);
     free_state(dv);
     codec_destroy(&dv->codec);
+    enc_destroy(&dv->enc);
     if (dv->cst) hipStreamSynchronize(dv->cst);
     if (dv->cwav) hipFree(dv->cwav);
     if (dv->push_codes) hipFree(dv->push_codes);
@@ -372,7 +381,7 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
 
 extern "C" size_t qtts_dev_bytes(const qtts_dev_t *dv, int which) {
     if (!dv) return 0;
-    return which == 0 ? dv->wbytes + codec_weight_bytes(&dv->codec) : dv->sbytes;
+    return which == 0 ? dv->wbytes + codec_weight_bytes(&dv->codec) + enc_weight_bytes(&dv->enc) : dv->sbytes;
 }
 
 // RoPE tables with the reference's exact libm arithmetic (T.c:97-113)
@@ -434,7 +443,37 @@ extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
     const bool ptab_on = !(pt && !atoi(pt));
     if (dv->st_proj && ptab_on) CKI(build_proj_tables(dv));
     if (ptab_on) CKI(build_qkv0_table(dv));
-    return codec_finalize(&dv->codec);
+    CKI(codec_finalize(&dv->codec));
+    return enc_finalize(&dv->enc);
+}
+
+// ----------------------------------------------------------------- voice-clone encoders
+static int join_prime(qtts_dev *dv);
+
+extern "C" int qtts_dev_enc_config(qtts_dev_t *dv, const qtts_enc_dims_t *dims) {
+    if (!dv || !dims) return -1;
+    return enc_set_dims(&dv->enc, dims);
+}
+
+extern "C" int qtts_dev_enc_available(qtts_dev_t *dv) {
+    if (!dv) return 0;
+    return (dv->enc.spk_ready ? 1 : 0) | (dv->enc.mimi_ready ? 2 : 0);
+}
+
+extern "C" int qtts_dev_speaker_embed(qtts_dev_t *dv, int nb, const float *const *wav, const int *n, float *out,
+                                      float *mel_out) {
+    if (!dv || !wav || !n || !out) return -1;
+    hipSetDevice(dv->device);
+    CKI(join_prime(dv));
+    return enc_speaker(&dv->enc, nb, wav, n, out, mel_out);
+}
+
+extern "C" int qtts_dev_encode_audio(qtts_dev_t *dv, int nb, const float *const *wav, const int *n, int *codes,
+                                     int max_frames, int *frames, float *latent) {
+    if (!dv || !wav || !n || !codes || !frames) return -1;
+    hipSetDevice(dv->device);
+    CKI(join_prime(dv));
+    return enc_codes(&dv->enc, nb, wav, n, codes, max_frames, frames, latent);
 }
 
 // ----------------------------------------------------------------- state

@@ -43,7 +43,10 @@ static void usage(const char *prog) {
             "  --benchmark-runs N (1)  --benchmark-warmup N (0)\n"
             "  --device N (HIP device, default 0)   --batch N (lock-step batch of N copies, default 1)\n"
             "  --stream N (streaming decode, audio chunks every N frames after the first)\n"
-            "voice clone (include/qwen_tts.h qwen_tts_generate_voice_clone; audio encoders not included):\n"
+            "voice clone (include/qwen_tts.h qwen_tts_generate_voice_clone[_audio]):\n"
+            "  --ref-audio <wav>   reference audio (mono/stereo PCM16 or float WAV at 24 kHz): encoded on\n"
+            "                      the GPU (12 Hz codes + speaker x-vector)\n"
+            "  --x-vector-only     with --ref-audio: x-vector only (no reference codes / ref text)\n"
             "  --ref-codes <file>  12 Hz codes of the reference audio, 16 ints per frame (any separators)\n"
             "  --ref-text <ids>    ids of \"<|im_start|>assistant\\n{ref text}<|im_end|>\\n\" (ICL mode)\n"
             "  --xvector <file>    speaker-encoder x-vector, talker-hidden floats (any separators)\n"
@@ -94,6 +97,64 @@ static double *read_numbers(const char *path, int *n_out) {
     return v;
 }
 
+/* RIFF/WAVE reader for --ref-audio: PCM 16-bit or IEEE float 32-bit, any
+ * channel count (averaged to mono, as qwen3_tts_tokenizer.py:152-153 does) */
+static float *read_wav(const char *path, int *n_out, int *sr_out) {
+    FILE *f = fopen(path, "rb");
+    if (!f) { fprintf(stderr, "Error: cannot open %s\n", path); return NULL; }
+    unsigned char h[12];
+    float *out = NULL;
+    int fmt = 0, ch = 0, bits = 0, sr = 0;
+    if (fread(h, 1, 12, f) != 12 || memcmp(h, "RIFF", 4) || memcmp(h + 8, "WAVE", 4)) {
+        fprintf(stderr, "Error: %s is not a RIFF/WAVE file\n", path);
+        fclose(f);
+        return NULL;
+    }
+    for (;;) {
+        unsigned char c[8];
+        if (fread(c, 1, 8, f) != 8) break;
+        const unsigned len = c[4] | c[5] << 8 | c[6] << 16 | (unsigned)c[7] << 24;
+        if (!memcmp(c, "fmt ", 4)) {
+            unsigned char b[40] = {0};
+            if (len < 16 || fread(b, 1, len < 40 ? len : 40, f) != (len < 40 ? len : 40)) break;
+            if (len > 40) fseek(f, len - 40, SEEK_CUR);
+            fmt = b[0] | b[1] << 8;
+            ch = b[2] | b[3] << 8;
+            sr = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+            bits = b[14] | b[15] << 8;
+            if (fmt == 0xFFFE && len >= 26) fmt = b[24] | b[25] << 8;   /* WAVE_FORMAT_EXTENSIBLE sub-format */
+        } else if (!memcmp(c, "data", 4)) {
+            const int bps = bits / 8;
+            if (ch < 1 || !((fmt == 1 && bits == 16) || (fmt == 3 && bits == 32))) {
+                fprintf(stderr, "Error: %s: only PCM16 or float32 WAV is supported\n", path);
+                break;
+            }
+            const int n = (int)(len / (unsigned)(bps * ch));
+            unsigned char *raw = (unsigned char *)malloc(len ? len : 1);
+            out = (float *)malloc((size_t)(n > 0 ? n : 1) * sizeof(float));
+            if (!raw || !out || fread(raw, 1, len, f) != len) { free(raw); free(out); out = NULL; break; }
+            for (int i = 0; i < n; i++) {
+                double acc = 0;
+                for (int k = 0; k < ch; k++) {
+                    const unsigned char *p = raw + ((size_t)i * ch + k) * bps;
+                    if (fmt == 1) acc += (short)(p[0] | p[1] << 8) / 32768.0;
+                    else { float v; memcpy(&v, p, 4); acc += v; }
+                }
+                out[i] = (float)(acc / ch);
+            }
+            free(raw);
+            *n_out = n;
+            *sr_out = sr;
+            break;
+        } else {
+            fseek(f, len + (len & 1), SEEK_CUR);
+        }
+    }
+    fclose(f);
+    if (!out) fprintf(stderr, "Error: no audio data in %s\n", path);
+    return out;
+}
+
 static void progress(int step, int total, void *u) {
     (void)total;
     (void)u;
@@ -106,8 +167,8 @@ static void progress(int step, int total, void *u) {
 int main(int argc, char **argv) {
     const char *dir = NULL, *ids = NULL, *ids_file = NULL, *spk = NULL, *lang = NULL, *out = "output.wav";
     int verbose = 0, runs = 1, warmup = 0, device = -1, batch = 1, stream_chunk = 0, non_streaming = 0;
-    const char *ref_codes_file = NULL, *ref_text = NULL, *xvec_file = NULL, *text = NULL;
-    int print_ids = 0;
+    const char *ref_codes_file = NULL, *ref_text = NULL, *xvec_file = NULL, *text = NULL, *ref_audio = NULL;
+    int print_ids = 0, xvec_only = 0;
     float temp = -1, st_temp = -1, top_p = -1, st_top_p = -1, rep = -1;
     int top_k = -1, st_top_k = -1, max_tokens = -1, fixed = -1, seed = -1;
     for (int i = 1; i < argc; i++) {
@@ -141,6 +202,8 @@ int main(int argc, char **argv) {
         else if (ARG("--ref-codes")) ref_codes_file = argv[++i];
         else if (ARG("--ref-text")) ref_text = argv[++i];
         else if (ARG("--xvector")) xvec_file = argv[++i];
+        else if (ARG("--ref-audio")) ref_audio = argv[++i];
+        else if (!strcmp(a, "--x-vector-only")) xvec_only = 1;
         else if (!strcmp(a, "--non-streaming")) non_streaming = 1;
         else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); return 0; }
         else {
@@ -183,7 +246,28 @@ int main(int argc, char **argv) {
     int *ref_codes = NULL, n_ref = 0;
     float *xvec = NULL;
     int n_xvec = 0;
-    const int clone = ref_codes_file || xvec_file;
+    const int clone = ref_codes_file || xvec_file || ref_audio;
+    if (ref_audio && (ref_codes_file || xvec_file)) {
+        fprintf(stderr, "Error: --ref-audio replaces --ref-codes / --xvector\n");
+        free(file_ids);
+        return 1;
+    }
+    float *ref_wav = NULL;
+    int n_ref_wav = 0;
+    if (ref_audio) {
+        int sr = 0;
+        if (!(ref_wav = read_wav(ref_audio, &n_ref_wav, &sr))) { free(file_ids); return 1; }
+        if (sr != QWEN_TTS_SAMPLE_RATE) {   /* the reference resamples with librosa (qwen3_tts_model.py:441-444) */
+            fprintf(stderr, "Error: --ref-audio must be %d Hz (got %d Hz); resample it first\n", QWEN_TTS_SAMPLE_RATE, sr);
+            free(ref_wav); free(file_ids);
+            return 1;
+        }
+        if (!xvec_only && !ref_text) {
+            fprintf(stderr, "Error: ref_text is required when x_vector_only_mode=False (ICL mode): pass --ref-text or --x-vector-only\n");
+            free(ref_wav); free(file_ids);
+            return 1;
+        }
+    }
     if (clone && (batch != 1 || stream_chunk > 0)) {
         fprintf(stderr, "Error: voice clone runs at --batch 1 without --stream\n");
         free(file_ids);
@@ -261,7 +345,11 @@ int main(int argc, char **argv) {
         float *ra = NULL;
         int rn = 0;
         long total_samples = 0;
-        if (clone) {
+        if (ref_wav) {
+            ra = qwen_tts_generate_voice_clone_audio(ctx, ids, xvec_only ? NULL : ref_text, ref_wav, n_ref_wav, lang,
+                                                     xvec_only, non_streaming, &rn);
+            total_samples = rn;
+        } else if (clone) {
             ra = qwen_tts_generate_voice_clone(ctx, ids, ref_text, ref_codes, n_ref, xvec, lang, non_streaming, &rn);
             total_samples = rn;
         } else if (batch == 1 && stream_chunk > 0) {
@@ -327,6 +415,7 @@ int main(int argc, char **argv) {
     free(audio);
     qwen_tts_free(ctx);
     free(file_ids);
+    free(ref_wav);
     free(ref_codes);
     free(xvec);
     return rc;

@@ -250,6 +250,74 @@ static int upload_dir(qtts_dev_t *dev, const char *dir) {
     return rc;
 }
 
+/* Voice-clone encoder config: config.json
+ * `speaker_encoder_config` (defaults of Qwen3TTSSpeakerEncoderConfig,
+ * configuration_qwen3_tts.py:47-57, enc_dim = the talker hidden the x-vector
+ * takes the place of) and speech_tokenizer/config.json `encoder_config`
+ * (transformers MimiConfig defaults).  Returns 1 when either section exists. */
+static int load_enc_config(const qwen_tts_ctx_t *ctx, qtts_enc_dims_t *e) {
+    memset(e, 0, sizeof *e);
+    char path[1100];
+    size_t len = 0;
+    int have = 0;
+    snprintf(path, sizeof path, "%s/config.json", ctx->model_dir);
+    char *txt = qj_read_file(path, &len);
+    qj_t *js = txt ? qj_parse(txt, len) : NULL;
+    free(txt);
+    if (js && qj_path(js, "speaker_encoder_config")) have = 1;
+#define SI(f, k, d) e->f = qj_int(js, "speaker_encoder_config." k, d)
+    SI(mel_dim, "mel_dim", 128);
+    SI(enc_dim, "enc_dim", ctx->config.talker_hidden);
+    SI(att_ch, "enc_attention_channels", 128);
+    SI(res2net_scale, "enc_res2net_scale", 8);
+    SI(se_ch, "enc_se_channels", 128);
+#undef SI
+    static const int dch[5] = {512, 512, 512, 512, 1536}, dks[5] = {5, 3, 3, 3, 1}, ddl[5] = {1, 2, 3, 4, 1};
+    memcpy(e->ch, dch, sizeof dch); memcpy(e->ks, dks, sizeof dks); memcpy(e->dil, ddl, sizeof ddl);
+    e->n_ch = 5;
+    if (js) {
+        int n = qj_ints(js, "speaker_encoder_config.enc_channels", e->ch, 8);
+        if (n > 0) e->n_ch = n;
+        qj_ints(js, "speaker_encoder_config.enc_kernel_sizes", e->ks, 8);
+        qj_ints(js, "speaker_encoder_config.enc_dilations", e->dil, 8);
+    }
+    qj_free(js);
+    snprintf(path, sizeof path, "%s/speech_tokenizer/config.json", ctx->model_dir);
+    txt = qj_read_file(path, &len);
+    js = txt ? qj_parse(txt, len) : NULL;
+    free(txt);
+    if (js && qj_path(js, "encoder_config")) have = 1;
+#define MI(f, k, d) e->f = qj_int(js, "encoder_config." k, d)
+    MI(hidden, "hidden_size", 512);
+    MI(n_filters, "num_filters", 64);
+    MI(kernel, "kernel_size", 7);
+    MI(last_kernel, "last_kernel_size", 3);
+    MI(res_kernel, "residual_kernel_size", 3);
+    MI(dil_growth, "dilation_growth_rate", 2);
+    MI(n_res, "num_residual_layers", 1);
+    MI(compress, "compress", 2);
+    MI(layers, "num_hidden_layers", 8);
+    MI(heads, "num_attention_heads", 8);
+    MI(kv_heads, "num_key_value_heads", 8);
+    MI(head_dim, "head_dim", 64);
+    MI(inter, "intermediate_size", 2048);
+    MI(window, "sliding_window", 250);
+    MI(n_q, "num_quantizers", 32);
+    MI(n_sem, "num_semantic_quantizers", 1);
+    MI(cb_size, "codebook_size", 2048);
+    MI(vq_dim, "vector_quantization_hidden_dimension", 256);
+#undef MI
+    e->n_valid = qj_int(js, "encoder_valid_num_quantizers", 16);
+    e->norm_eps = qj_float(js, "encoder_config.norm_eps", 1e-5f);
+    e->rope_theta = qj_float(js, "encoder_config.rope_theta", 0.f);
+    if (e->rope_theta <= 0.f) e->rope_theta = qj_float(js, "encoder_config.rope_parameters.rope_theta", 10000.0f);
+    int ratios[4] = {8, 6, 5, 4};
+    if (js) qj_ints(js, "encoder_config.upsampling_ratios", ratios, 4);
+    memcpy(e->ratios, ratios, sizeof ratios);
+    qj_free(js);
+    return have;
+}
+
 static void dims_of(const qwen_tts_config_t *c, qtts_dims_t *d) {
     memset(d, 0, sizeof *d);
     d->H = c->talker_hidden; d->I = c->talker_intermediate; d->L = c->talker_layers; d->NH = c->talker_heads;
@@ -301,6 +369,8 @@ qwen_tts_ctx_t *qwen_tts_load(const char *model_dir) {
     qtts_dev_t *dev = qtts_dev_create(&dims, dev_id);
     if (!dev) { qwen_tts_free(ctx); return NULL; }
     ctx->hip = dev;
+    qtts_enc_dims_t ed;
+    if (load_enc_config(ctx, &ed) && qtts_dev_enc_config(dev, &ed) != 0) { qwen_tts_free(ctx); return NULL; }
     char cdir[1100];
     snprintf(cdir, sizeof cdir, "%s/speech_tokenizer", model_dir);
     if (upload_dir(dev, model_dir) != 0 || upload_dir(dev, cdir) != 0 || qtts_dev_finalize(dev) != 0) {
@@ -845,6 +915,120 @@ float *qwen_tts_generate_voice_clone(qwen_tts_ctx_t *ctx, const char *text, cons
     const int nr1[1] = {n_ref_frames};
     const float *sv1[1] = {spk_embed};
     if (qwen_tts_generate_voice_clone_batch(ctx, 1, texts, rt, rc1, nr1, sv1, lang, non_streaming, &audio, &n) != 0 ||
+        !audio || n <= 0) {
+        free(audio);
+        return NULL;
+    }
+    *out_samples = n;
+    return audio;
+}
+
+/* ------------------------------------------- voice clone from reference audio (N3) */
+float *qwen_tts_speaker_embedding(qwen_tts_ctx_t *ctx, const float *wav, int n_samples, int *out_dim) {
+    if (out_dim) *out_dim = 0;
+    if (!ctx || !ctx->hip || !wav || n_samples <= 0) return NULL;
+    const int dim = ctx->config.talker_hidden;
+    float *out = (float *)malloc((size_t)dim * sizeof(float));
+    if (!out) return NULL;
+    const float *w[1] = {wav};
+    const int n[1] = {n_samples};
+    if (qtts_dev_speaker_embed((qtts_dev_t *)ctx->hip, 1, w, n, out, NULL) != 0) {
+        free(out);
+        return NULL;
+    }
+    if (out_dim) *out_dim = dim;
+    return out;
+}
+
+int *qwen_tts_encode_audio(qwen_tts_ctx_t *ctx, const float *wav, int n_samples, int *out_frames) {
+    if (out_frames) *out_frames = 0;
+    if (!ctx || !ctx->hip || !wav || n_samples <= 0) return NULL;
+    const int T = (n_samples + 1919) / 1920;
+    int *codes = (int *)malloc((size_t)T * 16 * sizeof(int));
+    if (!codes) return NULL;
+    const float *w[1] = {wav};
+    const int n[1] = {n_samples};
+    int fr = 0;
+    if (qtts_dev_encode_audio((qtts_dev_t *)ctx->hip, 1, w, n, codes, T, &fr, NULL) != 0) {
+        free(codes);
+        return NULL;
+    }
+    if (out_frames) *out_frames = fr;
+    return codes;
+}
+
+/* create_voice_clone_prompt (qwen3_tts_model.py:356-458) + generate_voice_clone:
+ * every reference audio is encoded in ONE padded batch (the tokenizer's batch
+ * encode, :427), each x-vector on its own audio (:446), then the codes /
+ * x-vector voice clone above.  x_vector_only[b] (NULL: all 0) drops the codes
+ * of slot b (ref_code=None, :451). */
+int qwen_tts_generate_voice_clone_audio_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts,
+                                              const char *const *ref_texts, const float *const *ref_wavs,
+                                              const int *n_ref_samples, const char *const *languages,
+                                              const int *x_vector_only, int non_streaming, float **out_audio,
+                                              int *out_samples) {
+    if (!ctx || !ctx->hip || nb < 1 || nb > 16 || !texts || !ref_wavs || !n_ref_samples || !out_audio ||
+        !out_samples) {
+        fprintf(stderr, "Error: voice clone from audio needs 1..16 utterances with reference audio\n");
+        return -1;
+    }
+    for (int b = 0; b < nb; b++) { out_audio[b] = NULL; out_samples[b] = 0; }
+    qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
+    if ((qtts_dev_enc_available(dev) & 3) != 3) {
+        fprintf(stderr, "Error: the model directory has no speaker encoder / 12 Hz encoder weights\n");
+        return -1;
+    }
+    for (int b = 0; b < nb; b++)
+        if (!x_vector_only || !x_vector_only[b])
+            if (!ref_texts || !ref_texts[b] || !ref_texts[b][0]) {
+                fprintf(stderr, "Error: ref_text is required when x_vector_only_mode=False (ICL mode). Bad index=%d\n", b);
+                return -1;
+            }
+    double t0 = now_ms();
+    const int H = ctx->config.talker_hidden;
+    int maxT = 0;
+    for (int b = 0; b < nb; b++) {
+        const int T = (n_ref_samples[b] + 1919) / 1920;
+        if (T > maxT) maxT = T;
+    }
+    int *codes = (int *)malloc((size_t)nb * (maxT > 0 ? maxT : 1) * 16 * sizeof(int));
+    float *xv = (float *)malloc((size_t)nb * H * sizeof(float));
+    int frames[16];
+    int rc = -1;
+    if (codes && xv && qtts_dev_encode_audio(dev, nb, ref_wavs, n_ref_samples, codes, maxT, frames, NULL) == 0 &&
+        qtts_dev_speaker_embed(dev, nb, ref_wavs, n_ref_samples, xv, NULL) == 0) {
+        const int *rc_p[16];
+        int nr[16];
+        const float *sv[16];
+        for (int b = 0; b < nb; b++) {
+            const int xo = x_vector_only && x_vector_only[b];
+            rc_p[b] = xo ? NULL : codes + (size_t)b * maxT * 16;
+            nr[b] = xo ? 0 : frames[b];
+            sv[b] = xv + (size_t)b * H;
+        }
+        if (qwen_tts_verbose >= 1) fprintf(stderr, "Reference audio encoded in %.1f ms\n", now_ms() - t0);
+        const char *const *rt = ref_texts;
+        const char *none[16] = {NULL};
+        if (!rt) rt = none;
+        rc = qwen_tts_generate_voice_clone_batch(ctx, nb, texts, rt, rc_p, nr, sv, languages, non_streaming, out_audio,
+                                                 out_samples);
+    }
+    free(codes);
+    free(xv);
+    return rc;
+}
+
+float *qwen_tts_generate_voice_clone_audio(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                           const float *ref_wav, int n_ref_samples, const char *language,
+                                           int x_vector_only, int non_streaming, int *out_samples) {
+    if (!out_samples) return NULL;
+    *out_samples = 0;
+    float *audio = NULL;
+    int n = 0;
+    const char *texts[1] = {text}, *rt[1] = {ref_text}, *lang[1] = {language};
+    const float *w[1] = {ref_wav};
+    const int nn[1] = {n_ref_samples}, xo[1] = {x_vector_only};
+    if (qwen_tts_generate_voice_clone_audio_batch(ctx, 1, texts, rt, w, nn, lang, xo, non_streaming, &audio, &n) != 0 ||
         !audio || n <= 0) {
         free(audio);
         return NULL;

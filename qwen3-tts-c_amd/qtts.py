@@ -68,7 +68,8 @@ EXPORTS = [
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
     "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
     "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream", "qwen_tts_tokenize",
-    "qwen_tts_text_prompt",
+    "qwen_tts_text_prompt", "qwen_tts_speaker_embedding", "qwen_tts_encode_audio",
+    "qwen_tts_generate_voice_clone_audio", "qwen_tts_generate_voice_clone_audio_batch",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -78,7 +79,8 @@ EXPORTS = [
     "qtts_dev_profile_frame", "qtts_dev_codec_stream_begin", "qtts_dev_codec_stream_begin_ex",
     "qtts_dev_codec_stream_prime", "qtts_dev_codec_stream_push_slot",
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
-    "qtts_dev_codec_async_end",
+    "qtts_dev_codec_async_end", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",
+    "qtts_dev_encode_audio",
 ]
 
 _LIB = None
@@ -151,6 +153,24 @@ def lib():
                                                       C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p), _ip]
     L.qwen_tts_codec_stream_begin.argtypes = [C.POINTER(Ctx), C.c_int]
     L.qwen_tts_codec_stream_push.argtypes = [C.POINTER(Ctx), _ip, C.c_int, _fp]
+    L.qwen_tts_speaker_embedding.restype = C.c_void_p
+    L.qwen_tts_speaker_embedding.argtypes = [C.POINTER(Ctx), _fp, C.c_int, _ip]
+    L.qwen_tts_encode_audio.restype = C.c_void_p
+    L.qwen_tts_encode_audio.argtypes = [C.POINTER(Ctx), _fp, C.c_int, _ip]
+    L.qwen_tts_generate_voice_clone_audio.restype = C.c_void_p
+    L.qwen_tts_generate_voice_clone_audio.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, _fp, C.c_int,
+                                                      C.c_char_p, C.c_int, C.c_int, _ip]
+    L.qwen_tts_generate_voice_clone_audio_batch.restype = C.c_int
+    L.qwen_tts_generate_voice_clone_audio_batch.argtypes = [C.POINTER(Ctx), C.c_int, C.POINTER(C.c_char_p),
+                                                            C.POINTER(C.c_char_p), C.POINTER(_fp), _ip,
+                                                            C.POINTER(C.c_char_p), _ip, C.c_int,
+                                                            C.POINTER(C.c_void_p), _ip]
+    L.qtts_dev_enc_available.restype = C.c_int
+    L.qtts_dev_enc_available.argtypes = [C.c_void_p]
+    L.qtts_dev_speaker_embed.restype = C.c_int
+    L.qtts_dev_speaker_embed.argtypes = [C.c_void_p, C.c_int, C.POINTER(_fp), _ip, _fp, _fp]
+    L.qtts_dev_encode_audio.restype = C.c_int
+    L.qtts_dev_encode_audio.argtypes = [C.c_void_p, C.c_int, C.POINTER(_fp), _ip, _ip, C.c_int, _ip, _fp]
     L.qtts_hip_device_count.restype = C.c_int
     vp = C.c_void_p
     L.qtts_hip_matvec_bf16.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
@@ -254,6 +274,110 @@ class QwenTTS:
         r = lib().qwen_tts_generate_voice_clone_batch(self.ctx, nb, tx, rt, rc, nr, sv, lg, int(non_streaming), out,
                                                       ns)
         return r, [_take_audio(out[i], ns[i]) for i in range(nb)]
+
+    # ---- voice-clone audio encoders (include/qtts_hip.h qtts_dev_speaker_embed / _encode_audio)
+    def encoders_available(self):
+        """bit 0: speaker encoder, bit 1: 12 Hz encoder."""
+        return lib().qtts_dev_enc_available(C.c_void_p(self.c.hip))
+
+    @staticmethod
+    def _wav_args(wavs):
+        ws = [np.ascontiguousarray(w, np.float32) for w in wavs]
+        nb = len(ws)
+        return ws, (_fp * nb)(*[w.ctypes.data_as(_fp) for w in ws]), (C.c_int * nb)(*[w.shape[0] for w in ws])
+
+    def speaker_embed(self, wavs, mel=False):
+        """x-vectors [nb, talker_hidden] of 24 kHz waveforms (one launch chain
+        for the batch, each utterance at its own length); with mel=True also
+        the list of [128, T_b] log-mels."""
+        ws, wp, ns = self._wav_args(wavs)
+        nb = len(ws)
+        out = np.zeros((nb, self.cfg.talker_hidden), np.float32)
+        T = [(w.shape[0] - 256) // 256 + 1 for w in ws]
+        mbuf = np.zeros(sum(128 * t for t in T), np.float32) if mel else None
+        rc = lib().qtts_dev_speaker_embed(C.c_void_p(self.c.hip), nb, wp, ns, out.ctypes.data_as(_fp),
+                                          mbuf.ctypes.data_as(_fp) if mel else None)
+        if rc != 0:
+            raise RuntimeError(f"speaker encoder failed (rc={rc})")
+        if not mel:
+            return out
+        mels, o = [], 0
+        for t in T:
+            mels.append(mbuf[o:o + 128 * t].reshape(128, t).copy())
+            o += 128 * t
+        return out, mels
+
+    def encode_audio(self, wavs, latent=False):
+        """12 Hz codes of 24 kHz waveforms, batch-encoded zero-padded to the
+        longest: list of [ceil(n / 1920), 16] int arrays (+ pre-quantizer
+        latents [hidden, frames] with latent=True)."""
+        ws, wp, ns = self._wav_args(wavs)
+        nb = len(ws)
+        maxT = max(-(-w.shape[0] // 1920) for w in ws)
+        codes = np.zeros((nb, maxT, 16), np.int32)
+        frames = (C.c_int * nb)()
+        hid = None
+        lat = None
+        if latent:
+            import json
+            with open(os.path.join(self.c.model_dir.decode(), "speech_tokenizer", "config.json")) as f:
+                hid = json.load(f).get("encoder_config", {}).get("hidden_size", 512)
+            lat = np.zeros((nb, hid, maxT), np.float32)
+        rc = lib().qtts_dev_encode_audio(C.c_void_p(self.c.hip), nb, wp, ns, codes.ctypes.data_as(_ip), maxT, frames,
+                                         lat.ctypes.data_as(_fp) if latent else None)
+        if rc != 0:
+            raise RuntimeError(f"audio encoder failed (rc={rc})")
+        cl = [codes[b, :frames[b]].copy() for b in range(nb)]
+        if not latent:
+            return cl
+        return cl, [lat[b, :, :frames[b]].copy() for b in range(nb)]
+
+    def speaker_embedding_api(self, wav):
+        """qwen_tts_speaker_embedding (the public C API)."""
+        w = np.ascontiguousarray(wav, np.float32)
+        n = C.c_int(0)
+        p = lib().qwen_tts_speaker_embedding(self.ctx, w.ctypes.data_as(_fp), w.shape[0], C.byref(n))
+        return _take_audio(p, n.value)
+
+    def encode_audio_api(self, wav):
+        """qwen_tts_encode_audio (the public C API): [frames, 16] or None."""
+        w = np.ascontiguousarray(wav, np.float32)
+        n = C.c_int(0)
+        p = lib().qwen_tts_encode_audio(self.ctx, w.ctypes.data_as(_fp), w.shape[0], C.byref(n))
+        if not p:
+            return None
+        a = np.ctypeslib.as_array(C.cast(p, _ip), shape=(n.value * 16,)).reshape(n.value, 16).copy()
+        _libc.free(C.c_void_p(p))
+        return a
+
+    def generate_voice_clone_audio(self, ids, ref_wav, ref_ids=None, language=None, x_vector_only=False,
+                                   non_streaming=False):
+        """Voice clone from reference audio (qwen_tts_generate_voice_clone_audio)."""
+        csv = ",".join(str(int(i)) for i in ids).encode()
+        rcsv = ",".join(str(int(i)) for i in ref_ids).encode() if ref_ids is not None else None
+        w = np.ascontiguousarray(ref_wav, np.float32)
+        n = C.c_int(0)
+        p = lib().qwen_tts_generate_voice_clone_audio(self.ctx, csv, rcsv, w.ctypes.data_as(_fp), w.shape[0],
+                                                      language.encode() if language else None, int(x_vector_only),
+                                                      int(non_streaming), C.byref(n))
+        return _take_audio(p, n.value)
+
+    def generate_voice_clone_audio_batch(self, id_lists, ref_wavs, ref_id_lists=None, languages=None,
+                                         x_vector_only=None, non_streaming=False):
+        """nb voice clones from reference audio in lock step (BASELINE C5 as
+        stated: ref-audio encode + decode + codec).  Returns (rc, [audio])."""
+        nb = len(id_lists)
+        enc = lambda ids: ",".join(str(int(i)) for i in ids).encode() if ids is not None else None
+        tx = (C.c_char_p * nb)(*[enc(i) for i in id_lists])
+        rt = (C.c_char_p * nb)(*[enc(i) for i in (ref_id_lists or [None] * nb)])
+        ws, wp, ns = self._wav_args(ref_wavs)
+        lg = (C.c_char_p * nb)(*[(s.encode() if s else None) for s in (languages or [None] * nb)])
+        xo = (C.c_int * nb)(*[int(bool(v)) for v in (x_vector_only or [False] * nb)])
+        out = (C.c_void_p * nb)()
+        on = (C.c_int * nb)()
+        r = lib().qwen_tts_generate_voice_clone_audio_batch(self.ctx, nb, tx, rt, wp, ns, lg, xo, int(non_streaming),
+                                                            out, on)
+        return r, [_take_audio(out[i], on[i]) for i in range(nb)]
 
     def generate_batch(self, id_lists, speakers=None, languages=None):
         nb = len(id_lists)

@@ -518,6 +518,20 @@ def ensure_model(out, preset="tiny", seed=0, overrides=None):
     return out
 
 
+def ref_wave(seed, secs=5.0, sr=24000):
+    """Seeded synthetic reference audio for voice clone (5 s
+    of pink noise plus a tone, 24 kHz mono, peak < 1)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = int(round(secs * sr))
+    f = np.fft.rfft(rng.standard_normal(n))
+    f /= np.sqrt(np.maximum(np.arange(f.shape[0]), 1.0))
+    w = np.fft.irfft(f, n)
+    w /= np.abs(w).max()
+    t = np.arange(n) / sr
+    w = 0.5 * w + 0.3 * np.sin(2 * np.pi * (150 + 13 * (seed % 11)) * t)
+    return np.clip(w, -0.95, 0.95).astype(np.float32)
+
+
 def prompt_ids(kind="short", seed=1234):
     """Token-id prompts (chat template). 'short' = test/tokens_great_power.txt
     (SURVEY.md 4); 'p128' = 3 + 30 random content ids + 5."""
