@@ -65,7 +65,27 @@ struct EConv {
     const float *res = nullptr;         // residual, res[b*rb + m*rc + n*rt]
     size_t rb = 0;
     int rc = 0, rt = 1;
+    // split-K (set by launch_econv): blockIdx.z = b * kz + split; raw partial
+    // tiles to part[split][b][M][pn], k_econv_reduce sums them in split order
+    float *part = nullptr;
+    int kz = 1, pn = 0, nb = 1;
 };
+
+__device__ __forceinline__ void econv_store(const EConv &g, int b, int m, int n, float v) {
+    const float *bias2 = g.bias2 ? g.bias2 + (size_t)b * g.bias2_b : nullptr;
+    if (g.bias) v += g.bias[m];
+    if (bias2) v += bias2[m];
+    switch (g.act_out) {
+        case 1: v = fmaxf(v, 0.f); break;
+        case 2: v = tanhf(fmaxf(v, 0.f)); break;
+        case 3: v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); break;
+        case 4: v = 1.0f / (1.0f + expf(-v)); break;
+        default: break;
+    }
+    if (g.vec) v *= g.vec[m];
+    if (g.res) v += g.res[(size_t)b * g.rb + (size_t)m * g.rc + (size_t)n * g.rt];
+    g.y[(size_t)b * g.yb + (size_t)m * g.yc + (size_t)n * g.yt] = v;
+}
 
 __device__ __forceinline__ int eswz(int r, int c) { return r * 32 + ((c ^ ((r >> 2) & 3)) << 3); }
 
@@ -109,7 +129,7 @@ __global__ __launch_bounds__(256) void k_econv(EConv g) {
     __shared__ __attribute__((aligned(16))) unsigned short As[3][64 * 32];
     __shared__ __attribute__((aligned(16))) unsigned short Bs[3][64 * 32];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int b = blockIdx.z;
+    const int kz = g.kz, b = blockIdx.z / kz, kzi = blockIdx.z - b * kz;
     const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
     const int lout = g.lout[b], lin = g.lin[b];
     if (n0 >= lout) return;   // uniform per workgroup, before any barrier
@@ -168,10 +188,10 @@ __global__ __launch_bounds__(256) void k_econv(EConv g) {
     floatx16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    const int nk = g.Kp / 32;
+    const int nk = g.Kp / 32, s0 = nk * kzi / kz, s1 = nk * (kzi + 1) / kz;
     const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32, r = lane & 31, hh = lane >> 5;
-    load(0);
-    for (int s = 0; s < nk; ++s) {
+    load(s0 * 32);
+    for (int s = s0; s < s1; ++s) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) *reinterpret_cast<uint4 *>(&As[p][eswz(ar, ac)]) = ra[p];
         {
@@ -183,7 +203,7 @@ __global__ __launch_bounds__(256) void k_econv(EConv g) {
             *reinterpret_cast<uint4 *>(&Bs[2][o]) = p3;
         }
         __syncthreads();
-        if (s + 1 < nk) load((s + 1) * 32);
+        if (s + 1 < s1) load((s + 1) * 32);
 #pragma unroll
         for (int kg = 0; kg < 2; ++kg) {
             const int c = kg * 2 + hh;
@@ -203,23 +223,31 @@ __global__ __launch_bounds__(256) void k_econv(EConv g) {
         }
         __syncthreads();
     }
-    float *y = g.y + (size_t)b * g.yb;
-    const float *res = g.res ? g.res + (size_t)b * g.rb : nullptr;
-    const float *bias2 = g.bias2 ? g.bias2 + (size_t)b * g.bias2_b : nullptr;
     const int n = n0 + wn + r;
     if (n >= lout) return;
+    if (kz > 1) {
+        float *pz = g.part + ((size_t)kzi * g.nb + b) * g.M * g.pn;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int m = m0 + wm + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (m < g.M) pz[(size_t)m * g.pn + n] = acc[i];
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int m = m0 + wm + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (m >= g.M) continue;
-        float v = acc[i];
-        if (g.bias) v += g.bias[m];
-        if (bias2) v += bias2[m];
-        v = act_apply(g.act_out, v);
-        if (g.vec) v *= g.vec[m];
-        if (res) v += res[(size_t)m * g.rc + (size_t)n * g.rt];
-        y[(size_t)m * g.yc + (size_t)n * g.yt] = v;
+        if (m < g.M) econv_store(g, b, m, n, acc[i]);
     }
+}
+
+// split-K partial sums in split order + the epilogue
+__global__ void k_econv_reduce(EConv g) {
+    const int n = blockIdx.x * 256 + threadIdx.x, m = blockIdx.y, b = blockIdx.z;
+    if (n >= g.lout[b]) return;
+    float v = 0.f;
+    for (int z = 0; z < g.kz; ++z) v += g.part[(((size_t)z * g.nb + b) * g.M + m) * g.pn + n];
+    econv_store(g, b, m, n, v);
 }
 
 // fp32 [M][K] -> three exact bf16 planes [3][M][Kp] (zero K padding)
@@ -377,21 +405,24 @@ __global__ void k_rows_bt(int *row_b, int *pos, int R, int T) {
 // (b, t) of the latent [b][hid][T12]; per chain (semantic: codebook 0,
 // acoustic: 1..nvalid-1) r = input_proj z, then per codebook the argmin
 // squared Euclidean distance (first index on ties) and r -= e[argmin].
-// 8 rows per workgroup share every codebook read.
-constexpr int RVQ_ROWS = 8;
-__global__ __launch_bounds__(256) void k_rvq_enc(const float *lat, int T12, int hid, int R, const float *psem,
-                                                 const float *pac, const float *cbk, int CB, int vq, int nvalid,
-                                                 int nsem, int *codes, int ldc_t) {
+// RVQ_ROWS rows per workgroup share every codebook read; the codebooks are
+// stored dim-major ([q][vq][CB]) and the projections transposed ([hid][vq]) so
+// that consecutive lanes read consecutive codes / outputs (coalesced).
+constexpr int RVQ_ROWS = 8, RVQ_NT = 512;
+__global__ __launch_bounds__(RVQ_NT) void k_rvq_enc(const float *lat, int T12, int hid, int R, const float *psemT,
+                                                    const float *pacT, const float *cbkT, int CB, int vq, int nvalid,
+                                                    int nsem, int *codes, int ldc_t) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
+    constexpr int NW = RVQ_NT / 64;
     float *z = sm;                                  // [ROWS][hid]
     float *rr = z + RVQ_ROWS * hid;                 // [ROWS][vq]
-    float *bd = rr + RVQ_ROWS * vq;                 // [4][ROWS] best distance per wave
-    int *bi = reinterpret_cast<int *>(bd + 4 * RVQ_ROWS);   // [4][ROWS]
-    int *best = bi + 4 * RVQ_ROWS;                  // [ROWS]
+    float *bd = rr + RVQ_ROWS * vq;                 // [NW][ROWS] best distance per wave
+    int *bi = reinterpret_cast<int *>(bd + NW * RVQ_ROWS);   // [NW][ROWS]
+    int *best = bi + NW * RVQ_ROWS;                 // [ROWS]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r0 = blockIdx.x * RVQ_ROWS;
     const int nr = min(RVQ_ROWS, R - r0);
-    for (int i = tid; i < RVQ_ROWS * hid; i += 256) {
+    for (int i = tid; i < RVQ_ROWS * hid; i += RVQ_NT) {
         const int j = i / hid, c = i - j * hid, row = r0 + j;
         float v = 0.f;
         if (j < nr) {
@@ -402,41 +433,53 @@ __global__ __launch_bounds__(256) void k_rvq_enc(const float *lat, int T12, int 
     }
     __syncthreads();
     for (int chain = 0; chain < 2; ++chain) {
-        const float *P = chain == 0 ? psem : pac;
+        const float *PT = chain == 0 ? psemT : pacT;
         const int q0 = chain == 0 ? 0 : nsem, q1 = chain == 0 ? nsem : nvalid;
-        for (int i = tid; i < RVQ_ROWS * vq; i += 256) {
+        for (int i = tid; i < RVQ_ROWS * vq; i += RVQ_NT) {
             const int j = i / vq, o = i - j * vq;
-            const float *pw = P + (size_t)o * hid, *zz = z + j * hid;
+            const float *zz = z + j * hid;
             float s = 0.f;
-            for (int c = 0; c < hid; ++c) s += pw[c] * zz[c];
+            for (int c0 = 0; c0 < hid; c0 += 16) {   // 16 loads in flight, then the FMAs in order
+                float pv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) pv[u] = PT[(size_t)(c0 + u) * vq + o];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) s += pv[u] * zz[c0 + u];
+            }
             rr[i] = s;
         }
         __syncthreads();
         for (int q = q0; q < q1; ++q) {
-            const float *E = cbk + (size_t)q * CB * vq;
+            const float *E = cbkT + (size_t)q * vq * CB;   // [vq][CB]
             float bdist[RVQ_ROWS];
             int bidx[RVQ_ROWS];
 #pragma unroll
             for (int j = 0; j < RVQ_ROWS; ++j) { bdist[j] = 3.402823466e38f; bidx[j] = 0; }
-            for (int code = tid; code < CB; code += 256) {
+            for (int code = tid; code < CB; code += RVQ_NT) {
                 float d[RVQ_ROWS];
 #pragma unroll
                 for (int j = 0; j < RVQ_ROWS; ++j) d[j] = 0.f;
-                const float4 *e4 = reinterpret_cast<const float4 *>(E + (size_t)code * vq);
-                for (int k = 0; k < vq / 4; ++k) {
-                    const float4 e = e4[k];
+                // 32 dims of this code in flight at once (the loop is otherwise
+                // one L2 round trip per 4 dims), then 8 rows x 32 dims of FMAs
+                for (int k0 = 0; k0 < vq; k0 += 32) {
+                    float e[32];
 #pragma unroll
-                    for (int j = 0; j < RVQ_ROWS; ++j) {
-                        const float4 rv = *reinterpret_cast<const float4 *>(rr + j * vq + 4 * k);
-                        const float a = rv.x - e.x, bb = rv.y - e.y, c = rv.z - e.z, dd = rv.w - e.w;
-                        d[j] += a * a + bb * bb + c * c + dd * dd;
-                    }
+                    for (int i = 0; i < 32; ++i) e[i] = E[(size_t)(k0 + i) * CB + code];
+#pragma unroll
+                    for (int i = 0; i < 32; i += 4)
+#pragma unroll
+                        for (int j = 0; j < RVQ_ROWS; ++j) {
+                            const float4 rv = *reinterpret_cast<const float4 *>(rr + j * vq + k0 + i);
+                            const float a = rv.x - e[i], bb = rv.y - e[i + 1], c = rv.z - e[i + 2],
+                                        dd = rv.w - e[i + 3];
+                            d[j] += a * a + bb * bb + c * c + dd * dd;
+                        }
                 }
 #pragma unroll
                 for (int j = 0; j < RVQ_ROWS; ++j)
                     if (d[j] < bdist[j]) { bdist[j] = d[j]; bidx[j] = code; }
             }
-            // (distance, index) argmin with first index on ties: wave, then 4 waves
+            // (distance, index) argmin with first index on ties: wave, then the waves
 #pragma unroll
             for (int j = 0; j < RVQ_ROWS; ++j) {
                 float dv = bdist[j];
@@ -452,7 +495,7 @@ __global__ __launch_bounds__(256) void k_rvq_enc(const float *lat, int T12, int 
             if (tid < RVQ_ROWS) {
                 float dv = bd[tid];
                 int iv = bi[tid];
-                for (int w = 1; w < 4; ++w) {
+                for (int w = 1; w < NW; ++w) {
                     const float d2 = bd[w * RVQ_ROWS + tid];
                     const int i2 = bi[w * RVQ_ROWS + tid];
                     if (d2 < dv || (d2 == dv && i2 < iv)) { dv = d2; iv = i2; }
@@ -464,9 +507,9 @@ __global__ __launch_bounds__(256) void k_rvq_enc(const float *lat, int T12, int 
                 }
             }
             __syncthreads();
-            for (int i = tid; i < RVQ_ROWS * vq; i += 256) {
+            for (int i = tid; i < RVQ_ROWS * vq; i += RVQ_NT) {
                 const int j = i / vq, o = i - j * vq;
-                rr[i] -= E[(size_t)best[j] * vq + o];
+                rr[i] -= E[(size_t)o * CB + best[j]];
             }
             __syncthreads();
         }
@@ -474,7 +517,8 @@ __global__ __launch_bounds__(256) void k_rvq_enc(const float *lat, int T12, int 
 }
 
 // ----------------------------------------------------------------- host helpers
-int launch_econv(const EConv &g, int nb, int nmax, hipStream_t st) {
+int launch_econv(EncModel *em, const EConv &gin, int nb, int nmax, hipStream_t st) {
+    EConv g = gin;
     if (g.M <= 0 || nmax <= 0) return 0;
     if (nb > ENC_MAXB || !g.w || g.Kp % 32 || g.K > g.Kp) {
         fprintf(stderr, "qtts enc: bad conv launch (nb %d, K %d, Kp %d)\n", nb, g.K, g.Kp);
@@ -488,11 +532,37 @@ int launch_econv(const EConv &g, int nb, int nmax, hipStream_t st) {
             return -1;
         }
     }
-    const dim3 grid((nmax + 63) / 64, (g.M + 63) / 64, nb);
     const bool rows = g.kw == 1 && g.xc == 1 && g.stride == 1 && g.padl == 0 && !g.x2 && g.act_in == ACT_NONE &&
                       g.K % 8 == 0 && g.xt % 4 == 0 && ((uintptr_t)g.x & 15) == 0;
+    // split-K when one utterance's output tiles cannot fill the chip: each
+    // K-step waits on its loads (a few steps of MFMA work cannot hide them),
+    // so more, shorter workgroups are the latency cover.  The split depends
+    // on the shape and the (padded) length only, never on the batch size, so
+    // an utterance gets the same sums alone or in a batch of equal padding.
+    const int tiles1 = (nmax + 63) / 64 * ((g.M + 63) / 64), nk = g.Kp / 32;
+    int kz = 1;
+    if (rows) kz = nk >= 8 ? std::min(4, nk / 4) : 1;
+    else if (tiles1 < 256 && nk >= 8) kz = std::max(1, std::min(std::min(nk / 4, 16), (512 + tiles1 - 1) / tiles1));
+    g.kz = kz; g.nb = nb; g.pn = nmax;
+    if (kz > 1) {
+        const size_t need = (size_t)kz * nb * g.M * nmax;
+        if (need > em->part_cap) {
+            hipStreamSynchronize(st);
+            if (em->part) hipFree(em->part);
+            em->part = nullptr;
+            em->part_cap = 0;
+            if (hipMalloc(&em->part, need * 4) != hipSuccess) {
+                fprintf(stderr, "qtts enc: split-K workspace hipMalloc(%zu) failed\n", need * 4);
+                return -1;
+            }
+            em->part_cap = need;
+        }
+        g.part = em->part;
+    }
+    const dim3 grid((nmax + 63) / 64, (g.M + 63) / 64, nb * kz);
     if (rows) hipLaunchKernelGGL((k_econv<true>), grid, dim3(256), 0, st, g);
     else hipLaunchKernelGGL((k_econv<false>), grid, dim3(256), 0, st, g);
+    if (kz > 1) hipLaunchKernelGGL(k_econv_reduce, dim3((nmax + 255) / 256, g.M, nb), dim3(256), 0, st, g);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -716,7 +786,7 @@ static int finalize_speaker(EncModel *m) {
 
 static int finalize_mimi(EncModel *m) {
     const qtts_enc_dims_t &d = m->d;
-    if (d.n_valid != 16 || d.n_sem < 1 || d.n_sem >= d.n_valid || d.hidden % 8 || d.vq_dim % 4 ||
+    if (d.n_valid != 16 || d.n_sem < 1 || d.n_sem >= d.n_valid || d.hidden % 16 || d.vq_dim % 32 ||
         d.head_dim % 8 || d.head_dim > 128 || d.hidden > 1024 || d.vq_dim > 512 || d.compress < 1) {
         fprintf(stderr, "Error: unsupported 12 Hz encoder config (hidden %d, vq %d, head_dim %d, valid %d)\n", d.hidden,
                 d.vq_dim, d.head_dim, d.n_valid);
@@ -763,10 +833,17 @@ static int finalize_mimi(EncModel *m) {
         ECK(vec_w(m, p + "mlp_layer_scale.scale", H));
     }
     ECK(conv_w(m, "encoder.downsample.conv.weight", H, H, 4));
-    ECK(vec_w(m, "encoder.quantizer.semantic_residual_vector_quantizer.input_proj.weight", (size_t)d.vq_dim * H));
-    ECK(vec_w(m, "encoder.quantizer.acoustic_residual_vector_quantizer.input_proj.weight", (size_t)d.vq_dim * H));
+    for (const char *kind : {"semantic", "acoustic"}) {   // input_proj [vq][H] -> transposed [H][vq]
+        const std::string n = std::string("encoder.quantizer.") + kind + "_residual_vector_quantizer.input_proj.weight";
+        const std::vector<float> *h = hget(m, n);
+        if (!h || h->size() != (size_t)d.vq_dim * H) return -1;
+        std::vector<float> t((size_t)H * d.vq_dim);
+        for (int o = 0; o < d.vq_dim; ++o)
+            for (int c = 0; c < H; ++c) t[(size_t)c * d.vq_dim + o] = (*h)[(size_t)o * H + c];
+        ECK((m->fw[n] = up_f32(m, t)) ? 0 : -1);
+    }
     // codebooks: embed_sum / max(cluster_usage, 1e-5) (MimiEuclideanCodebook.embed)
-    std::vector<float> cb((size_t)d.n_valid * d.cb_size * d.vq_dim);
+    std::vector<float> cb((size_t)d.n_valid * d.cb_size * d.vq_dim);   // [q][vq][CB] (dim-major)
     for (int q = 0; q < d.n_valid; ++q) {
         const std::string p = q < d.n_sem
             ? "encoder.quantizer.semantic_residual_vector_quantizer.layers." + std::to_string(q) + ".codebook."
@@ -776,7 +853,7 @@ static int finalize_mimi(EncModel *m) {
         for (int c = 0; c < d.cb_size; ++c) {
             const float u = std::max((*us)[c], 1e-5f);
             for (int k = 0; k < d.vq_dim; ++k)
-                cb[((size_t)q * d.cb_size + c) * d.vq_dim + k] = (*es)[(size_t)c * d.vq_dim + k] / u;
+                cb[((size_t)q * d.vq_dim + k) * d.cb_size + c] = (*es)[(size_t)c * d.vq_dim + k] / u;
         }
     }
     return (m->cbk = up_f32(m, cb)) ? 0 : -1;
@@ -798,6 +875,9 @@ int enc_finalize(EncModel *m) {
 void enc_destroy(EncModel *m) {
     for (void *p : m->wallocs) hipFree(p);
     for (void *p : m->sallocs) hipFree(p);
+    if (m->part) hipFree(m->part);
+    m->part = nullptr;
+    m->part_cap = 0;
     m->wallocs.clear();
     m->sallocs.clear();
     m->sbase = nullptr;
@@ -920,7 +1000,7 @@ int enc_speaker(EncModel *m, int nb, const float *const *wav, const int *n, floa
         g.x = dw; g.xb = nmax; g.xc = 0; g.xt = 1;
         g.y = spec; g.yb = (size_t)2 * nf * Tm; g.yc = Tm; g.yt = 1;
         for (int b = 0; b < nb; ++b) { g.lin[b] = n[b]; g.lout[b] = T[b]; }
-        ECK(launch_econv(g, nb, Tm, st));
+        ECK(launch_econv(m, g, nb, Tm, st));
     }
     hipLaunchKernelGGL(k_mel, dim3(Tm, nb), dim3(256), 0, st, spec, nf, Tm, lens, m->melfb,
                        reinterpret_cast<const int *>(F(m, "#melfb_lo")),
@@ -939,7 +1019,7 @@ int enc_speaker(EncModel *m, int nb, const float *const *wav, const int *n, floa
         g.bias = F(m, name + ".bias");
         g.act_out = act;
         setlen(g);
-        return launch_econv(g, nb, Tm, st);
+        return launch_econv(m, g, nb, Tm, st);
     };
     // 2. block 0
     ECK(tdnn(P + "blocks.0.conv", mel, nm, nullptr, x0, C, d.dil[0], ACT_RELU));
@@ -978,7 +1058,7 @@ int enc_speaker(EncModel *m, int nb, const float *const *wav, const int *n, floa
         chan(g, mfa, CM, a1, A);
         g.bias2 = b2; g.bias2_b = A; g.act_out = ACT_RELU_TANH;
         setlen(g);
-        ECK(launch_econv(g, nb, Tm, st));
+        ECK(launch_econv(m, g, nb, Tm, st));
     }
     ECK(tdnn(P + "asp.conv", a1, A, nullptr, lg, CM, 1, ACT_NONE));
     hipLaunchKernelGGL(k_asp_pool, dim3((CM + 3) / 4, nb), dim3(256), 0, st, mfa, (size_t)CM * Tm, lg, (size_t)CM * Tm,
@@ -1074,7 +1154,7 @@ int enc_codes(EncModel *m, int nb, const float *const *wav, const int *n, int *c
         g.bias = F(m, name + ".bias");
         if (res) { g.res = res; g.rb = g.yb; g.rc = Lout; g.rt = 1; }
         for (int b = 0; b < nb; ++b) { g.lin[b] = Lin; g.lout[b] = Lout; }
-        return launch_econv(g, nb, Lout, st);
+        return launch_econv(m, g, nb, Lout, st);
     };
     ECK(sconv(P + "0.conv", dw, 1, nmax, A, d.n_filters, nmax, 1, false, nullptr));
     int li = 1, C = d.n_filters;
@@ -1105,7 +1185,7 @@ int enc_codes(EncModel *m, int nb, const float *const *wav, const int *n, int *c
         g.y = x; g.yb = (size_t)T25 * H; g.yc = 1; g.yt = H;
         g.padl = w->kw - 1; g.act_in = 1; g.bias = F(m, name + ".bias");
         for (int b = 0; b < nb; ++b) { g.lin[b] = T25; g.lout[b] = T25; }
-        ECK(launch_econv(g, nb, T25, st));
+        ECK(launch_econv(m, g, nb, T25, st));
     }
     // transformer over R = nb * T25 rows (MimiTransformerModel, no final norm)
     hipLaunchKernelGGL(k_rows_bt, dim3((R + 255) / 256), dim3(256), 0, st, row_b, pos, R, T25);
@@ -1119,7 +1199,7 @@ int enc_codes(EncModel *m, int nb, const float *const *wav, const int *n, int *c
         g.act_out = act; g.vec = vec;
         if (resid) { g.res = y; g.rb = 0; g.rc = 1; g.rt = N; }
         g.lin[0] = R; g.lout[0] = R;
-        return launch_econv(g, 1, R, st);
+        return launch_econv(m, g, 1, R, st);
     };
     for (int l = 0; l < d.layers; ++l) {
         const std::string p = "encoder.encoder_transformer.layers." + std::to_string(l) + ".";
@@ -1151,13 +1231,13 @@ int enc_codes(EncModel *m, int nb, const float *const *wav, const int *n, int *c
         g.y = lat; g.yb = (size_t)H * T12; g.yc = T12; g.yt = 1;
         g.stride = 2; g.padl = w->kw - 2; g.pmode = PAD_REPLICATE;
         for (int b = 0; b < nb; ++b) { g.lin[b] = T25; g.lout[b] = T12; }
-        ECK(launch_econv(g, nb, T12, st));
+        ECK(launch_econv(m, g, nb, T12, st));
     }
     // split RVQ encode of the first n_valid codebooks
     {
         const int rows = nb * T12;
-        const size_t smem = ((size_t)RVQ_ROWS * (H + d.vq_dim) + 8 * RVQ_ROWS) * 4 + RVQ_ROWS * 4 + 64;
-        hipLaunchKernelGGL(k_rvq_enc, dim3((rows + RVQ_ROWS - 1) / RVQ_ROWS), dim3(256), smem, st, lat, T12, H, rows,
+        const size_t smem = ((size_t)RVQ_ROWS * (H + d.vq_dim) + 2 * (RVQ_NT / 64) * RVQ_ROWS + RVQ_ROWS) * 4 + 64;
+        hipLaunchKernelGGL(k_rvq_enc, dim3((rows + RVQ_ROWS - 1) / RVQ_ROWS), dim3(RVQ_NT), smem, st, lat, T12, H, rows,
                            F(m, "encoder.quantizer.semantic_residual_vector_quantizer.input_proj.weight"),
                            F(m, "encoder.quantizer.acoustic_residual_vector_quantizer.input_proj.weight"), m->cbk,
                            d.cb_size, d.vq_dim, d.n_valid, d.n_sem, dcodes, T12);

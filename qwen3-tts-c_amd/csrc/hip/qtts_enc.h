@@ -53,10 +53,8 @@ struct EncModel {
     std::vector<void *> sallocs;
     size_t scap = 0;
     char *sbase = nullptr;
-    float *wav = nullptr;
-    size_t wav_cap = 0;
-    int *ibuf = nullptr;
-    size_t ibuf_cap = 0;
+    float *part = nullptr;    // k_econv split-K partials (grown on demand)
+    size_t part_cap = 0;
 };
 
 int enc_set_dims(EncModel *m, const qtts_enc_dims_t *d);

@@ -62,10 +62,14 @@ def test_speaker_embedding_vs_golden(tts_vc):
 
 
 def test_speaker_embedding_batch_equals_single(tts_vc):
+    """Each utterance of a ragged batch runs at its own length: equal to its
+    single run up to the split-K order of the padded length (1e-5 relative)."""
     wavs = [G[f"wav{i}"] for i in range(3)]
     xb = tts_vc.speaker_embed(wavs)
     for i in range(3):
-        np.testing.assert_array_equal(tts_vc.speaker_embed([wavs[i]])[0], xb[i])
+        np.testing.assert_allclose(tts_vc.speaker_embed([wavs[i]])[0], xb[i], rtol=1e-5,
+                                   atol=1e-5 * np.abs(xb[i]).max())
+    np.testing.assert_array_equal(tts_vc.speaker_embed([wavs[0]])[0], xb[0])   # the longest: same padding
     api = tts_vc.speaker_embedding_api(wavs[1])
     np.testing.assert_array_equal(api, xb[1])
 

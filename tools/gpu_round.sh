@@ -40,6 +40,14 @@ cp $O/pmc.json $R/profiles/${TAG}_pmc.json
 echo $TAG > $R/profiles/LATEST
 cd $R
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
+# BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8
+timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_vc8.json 2> $O/bench_vc8.err
+cp $O/bench_vc8.json $R/profiles/${TAG}_bench_vc8.json
+# the encoders alone: timings, rocprof stats and the per-(kernel, grid) breakdown
+bash tools/gpu_enc_prof.sh $TAG/enc
+cp $O/enc/enc_times.json $R/profiles/${TAG}_enc_times.json
+cp $O/enc/enc_by_grid.txt $R/profiles/${TAG}_enc_by_grid.txt
+cp $O/enc/enc_kernel_stats.csv $R/profiles/${TAG}_enc_kernel_stats.csv
 # last (a counter the box refuses ends only this pass): matrix-core busy cycles
 # of the voice-clone batch-8 bench (prefill GEMM, batch decode GEMV, codec convs)
 cd /tmp
