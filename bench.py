@@ -246,6 +246,24 @@ def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128
                         f"process wall incl. load {wall:.0f} s"))
 
 
+def enc_cpu_baseline(md, wav):
+    """The voice-clone encoders on the host: the float64 numpy restatement
+    (oracle/enc_oracle.py, a port -- the reference's encoders are Python /
+    transformers, not runnable here) on ONE reference waveform."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import enc_oracle
+    W, scfg, M, mcfg = enc_oracle.load_encoder_weights(md)
+    t0 = time.perf_counter()
+    enc_oracle.speaker_embedding(W, scfg, wav)
+    t1 = time.perf_counter()
+    enc_oracle.mimi_encode(M, mcfg, wav)
+    t2 = time.perf_counter()
+    thr = os.environ.get("OMP_NUM_THREADS") or str(os.cpu_count())
+    return dict(speaker_ms=round((t1 - t0) * 1e3, 1), codes_ms=round((t2 - t1) * 1e3, 1), kind="port",
+                cores=int(thr), sample=f"oracle/enc_oracle.py (float64 numpy, BLAS threads {thr}) on one "
+                                       f"{wav.shape[0] / 24000:.1f} s reference")
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` without a launcher: start N ranks (one process per
     GPU) through torch.distributed.run as a CHILD process and return its exit
@@ -434,6 +452,7 @@ def main():
         gf = encoder_gflop(md, [w.shape[0] for w in wavs])
         spk_ms, cod_ms = (ts - te) / 3 * 1e3, (tc - ts) / 3 * 1e3
         enc = dict(speaker_ms=round(spk_ms, 3), codes_ms=round(cod_ms, 3), ref_seconds=5.0, batch=len(wavs),
+                   cpu_baseline=None if (args.no_cpu_baseline or rank != 0) else enc_cpu_baseline(md, wavs[0]),
                    speaker_gflop=round(gf[0], 2), codes_gflop=round(gf[1], 2),
                    speaker_tflops=round(gf[0] / spk_ms, 2), codes_tflops=round(gf[1] / cod_ms, 2),
                    note="wall time of the encoder call (host waveform in, host codes / x-vectors out), "

@@ -267,6 +267,14 @@ int qwen_tts_generate_voice_clone_audio_batch(qwen_tts_ctx_t *ctx, int nb, const
                                               const int *n_ref_samples, const char *const *languages,
                                               const int *x_vector_only, int non_streaming, float **out_audio,
                                               int *out_samples);
+/* audio chunk callback of the streaming calls (qwen_tts_generate_stream below) */
+typedef void (*qwen_tts_audio_cb)(const float *pcm, int n_samples, void *userdata);
+/* streaming form: encode, then qwen_tts_generate_voice_clone_stream; the
+ * first-packet time counts from this call's entry (encode included) */
+float *qwen_tts_generate_voice_clone_audio_stream(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                                  const float *ref_wav, int n_ref_samples, const char *language,
+                                                  int x_vector_only, int non_streaming, int chunk_frames,
+                                                  qwen_tts_audio_cb cb, void *userdata, int *out_samples);
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
@@ -276,7 +284,6 @@ int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
  * the first chunk after frame 0 (1920 samples, 80 ms), then every
  * `chunk_frames` frames, then the tail.  Returns the whole utterance like
  * qwen_tts_generate (malloc'd, caller frees); NULL on error. */
-typedef void (*qwen_tts_audio_cb)(const float *pcm, int n_samples, void *userdata);
 float *qwen_tts_generate_stream(qwen_tts_ctx_t *ctx, const char *text, const char *speaker, const char *language,
                                 int chunk_frames, qwen_tts_audio_cb cb, void *userdata, int *out_samples);
 float *qwen_tts_generate_voice_clone_stream(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,

@@ -405,10 +405,10 @@ __global__ void k_rows_bt(int *row_b, int *pos, int R, int T) {
 // (b, t) of the latent [b][hid][T12]; per chain (semantic: codebook 0,
 // acoustic: 1..nvalid-1) r = input_proj z, then per codebook the argmin
 // squared Euclidean distance (first index on ties) and r -= e[argmin].
-// RVQ_ROWS rows per workgroup share every codebook read; the codebooks are
+// RVQ_ROWS (2) rows per workgroup of 16 waves share every codebook read; the codebooks are
 // stored dim-major ([q][vq][CB]) and the projections transposed ([hid][vq]) so
 // that consecutive lanes read consecutive codes / outputs (coalesced).
-constexpr int RVQ_ROWS = 8, RVQ_NT = 512;
+constexpr int RVQ_ROWS = 2, RVQ_NT = 1024;
 __global__ __launch_bounds__(RVQ_NT) void k_rvq_enc(const float *lat, int T12, int hid, int R, const float *psemT,
                                                     const float *pacT, const float *cbkT, int CB, int vq, int nvalid,
                                                     int nsem, int *codes, int ldc_t) {
@@ -459,14 +459,14 @@ __global__ __launch_bounds__(RVQ_NT) void k_rvq_enc(const float *lat, int T12, i
                 float d[RVQ_ROWS];
 #pragma unroll
                 for (int j = 0; j < RVQ_ROWS; ++j) d[j] = 0.f;
-                // 32 dims of this code in flight at once (the loop is otherwise
-                // one L2 round trip per 4 dims), then 8 rows x 32 dims of FMAs
-                for (int k0 = 0; k0 < vq; k0 += 32) {
-                    float e[32];
+                // 16 dims of this code in flight at once (the loop is otherwise
+                // one L2 round trip per 4 dims), then 8 rows x 16 dims of FMAs
+                for (int k0 = 0; k0 < vq; k0 += 16) {
+                    float e[16];
 #pragma unroll
-                    for (int i = 0; i < 32; ++i) e[i] = E[(size_t)(k0 + i) * CB + code];
+                    for (int i = 0; i < 16; ++i) e[i] = E[(size_t)(k0 + i) * CB + code];
 #pragma unroll
-                    for (int i = 0; i < 32; i += 4)
+                    for (int i = 0; i < 16; i += 4)
 #pragma unroll
                         for (int j = 0; j < RVQ_ROWS; ++j) {
                             const float4 rv = *reinterpret_cast<const float4 *>(rr + j * vq + k0 + i);

@@ -1018,6 +1018,46 @@ int qwen_tts_generate_voice_clone_audio_batch(qwen_tts_ctx_t *ctx, int nb, const
     return rc;
 }
 
+/* streaming form of qwen_tts_generate_voice_clone_audio: the reference audio
+ * is encoded first, then qwen_tts_generate_voice_clone_stream; the first
+ * packet time (ctx->perf_first_packet_ms) counts from this call's entry */
+float *qwen_tts_generate_voice_clone_audio_stream(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
+                                                  const float *ref_wav, int n_ref_samples, const char *language,
+                                                  int x_vector_only, int non_streaming, int chunk_frames,
+                                                  qwen_tts_audio_cb cb, void *userdata, int *out_samples) {
+    if (!out_samples) return NULL;
+    *out_samples = 0;
+    if (!ctx || !ctx->hip || !ref_wav || n_ref_samples <= 0) return NULL;
+    qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
+    if ((qtts_dev_enc_available(dev) & 3) != 3) {
+        fprintf(stderr, "Error: the model directory has no speaker encoder / 12 Hz encoder weights\n");
+        return NULL;
+    }
+    if (!x_vector_only && (!ref_text || !ref_text[0])) {
+        fprintf(stderr, "Error: ref_text is required when x_vector_only_mode=False (ICL mode). Bad index=0\n");
+        return NULL;
+    }
+    const double t0 = now_ms();
+    const int T = (n_ref_samples + 1919) / 1920, H = ctx->config.talker_hidden;
+    int *codes = (int *)malloc((size_t)T * 16 * sizeof(int));
+    float *xv = (float *)malloc((size_t)H * sizeof(float));
+    const float *w[1] = {ref_wav};
+    const int n[1] = {n_ref_samples};
+    int fr = 0;
+    float *audio = NULL;
+    if (codes && xv && qtts_dev_encode_audio(dev, 1, w, n, codes, T, &fr, NULL) == 0 &&
+        qtts_dev_speaker_embed(dev, 1, w, n, xv, NULL) == 0) {
+        const double enc_ms = now_ms() - t0;
+        audio = qwen_tts_generate_voice_clone_stream(ctx, text, x_vector_only ? NULL : ref_text,
+                                                     x_vector_only ? NULL : codes, x_vector_only ? 0 : fr, xv,
+                                                     language, non_streaming, chunk_frames, cb, userdata, out_samples);
+        if (audio && ctx->perf_first_packet_ms > 0) ctx->perf_first_packet_ms += enc_ms;
+    }
+    free(codes);
+    free(xv);
+    return audio;
+}
+
 float *qwen_tts_generate_voice_clone_audio(qwen_tts_ctx_t *ctx, const char *text, const char *ref_text,
                                            const float *ref_wav, int n_ref_samples, const char *language,
                                            int x_vector_only, int non_streaming, int *out_samples) {

@@ -70,6 +70,7 @@ EXPORTS = [
     "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream", "qwen_tts_tokenize",
     "qwen_tts_text_prompt", "qwen_tts_speaker_embedding", "qwen_tts_encode_audio",
     "qwen_tts_generate_voice_clone_audio", "qwen_tts_generate_voice_clone_audio_batch",
+    "qwen_tts_generate_voice_clone_audio_stream",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -165,6 +166,10 @@ def lib():
                                                             C.POINTER(C.c_char_p), C.POINTER(_fp), _ip,
                                                             C.POINTER(C.c_char_p), _ip, C.c_int,
                                                             C.POINTER(C.c_void_p), _ip]
+    L.qwen_tts_generate_voice_clone_audio_stream.restype = C.c_void_p
+    L.qwen_tts_generate_voice_clone_audio_stream.argtypes = [C.POINTER(Ctx), C.c_char_p, C.c_char_p, _fp, C.c_int,
+                                                             C.c_char_p, C.c_int, C.c_int, C.c_int, AUDIO_CB,
+                                                             C.c_void_p, _ip]
     L.qtts_dev_enc_available.restype = C.c_int
     L.qtts_dev_enc_available.argtypes = [C.c_void_p]
     L.qtts_dev_speaker_embed.restype = C.c_int
@@ -360,6 +365,23 @@ class QwenTTS:
         p = lib().qwen_tts_generate_voice_clone_audio(self.ctx, csv, rcsv, w.ctypes.data_as(_fp), w.shape[0],
                                                       language.encode() if language else None, int(x_vector_only),
                                                       int(non_streaming), C.byref(n))
+        return _take_audio(p, n.value)
+
+    def generate_voice_clone_audio_stream(self, ids, ref_wav, ref_ids=None, language=None, x_vector_only=False,
+                                          non_streaming=False, chunk_frames=4, on_chunk=None):
+        """Streaming voice clone from reference audio; first packet counts the encode."""
+        csv = ",".join(str(int(i)) for i in ids).encode()
+        rcsv = ",".join(str(int(i)) for i in ref_ids).encode() if ref_ids is not None else None
+        w = np.ascontiguousarray(ref_wav, np.float32)
+        n = C.c_int(0)
+
+        def _cb(p, k, u):
+            if on_chunk is not None:
+                on_chunk(np.ctypeslib.as_array(p, shape=(k,)).copy())
+        cb = AUDIO_CB(_cb)
+        p = lib().qwen_tts_generate_voice_clone_audio_stream(
+            self.ctx, csv, rcsv, w.ctypes.data_as(_fp), w.shape[0], language.encode() if language else None,
+            int(x_vector_only), int(non_streaming), int(chunk_frames), cb, None, C.byref(n))
         return _take_audio(p, n.value)
 
     def generate_voice_clone_audio_batch(self, id_lists, ref_wavs, ref_id_lists=None, languages=None,

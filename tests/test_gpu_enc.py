@@ -166,6 +166,27 @@ def test_voice_clone_from_audio_equals_codes_path(tts_vc):
     np.testing.assert_array_equal(ax, bx)
 
 
+def test_voice_clone_audio_stream_equals_codes_stream(tts_vc):
+    """qwen_tts_generate_voice_clone_audio_stream == encode + the codes stream."""
+    from oracle_py import GREEDY
+    from synth_model import prompt_ids
+    tts_vc.set_params(max_tokens=4096, fixed=6, seed=42, **GREEDY)
+    ids = prompt_ids("short")
+    ref_ids = [151644, 77091, 198, 2354, 2244, 151645, 198]
+    w = G["wav1"]
+    chunks = []
+    a = tts_vc.generate_voice_clone_audio_stream(ids, w, ref_ids=ref_ids, language="english", chunk_frames=2,
+                                                 on_chunk=chunks.append)
+    codes = tts_vc.encode_audio([w])[0]
+    xv = tts_vc.speaker_embed([w])[0]
+    b = tts_vc.generate_voice_clone_stream(ids, ref_ids=ref_ids, ref_codes=codes, spk_embed=xv, language="english",
+                                           chunk_frames=2)
+    assert a is not None and chunks
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(np.concatenate(chunks), a)
+    assert tts_vc.c.perf_first_packet_ms > 0
+
+
 def test_voice_clone_audio_batch_equals_singles(tts_vc):
     from oracle_py import GREEDY
     from synth_model import prompt_ids
