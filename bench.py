@@ -467,7 +467,10 @@ def main():
     m.close()
 
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    # the reference c/ CPU leg belongs to the custom-voice line (the c/ reference
+    # has no voice clone); a voice-clone line carries the encoders' host port
+    # baseline in ref_audio_encode instead
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and vc is None:
         thr = args.cpu_threads or cpu_threads_default()
         cpu = cpu_baseline(md, prompts[0], thr, frames=args.cpu_frames, target_frames=args.frames)
         if cpu and args.cpu_1thread:

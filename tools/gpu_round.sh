@@ -41,7 +41,7 @@ echo $TAG > $R/profiles/LATEST
 cd $R
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
 # BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8
-timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_vc8.json 2> $O/bench_vc8.err
+timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 > $O/bench_vc8.json 2> $O/bench_vc8.err
 cp $O/bench_vc8.json $R/profiles/${TAG}_bench_vc8.json
 # the encoders alone: timings, rocprof stats and the per-(kernel, grid) breakdown
 bash tools/gpu_enc_prof.sh $TAG/enc
