@@ -463,6 +463,11 @@ def main():
             m.generate_voice_clone_stream(prompts[0], vc[0][0], vc[0][1], vc[0][2], "english", chunk_frames=8)
         fp = dict(first_packet_ms=m.c.perf_first_packet_ms, first_frame_ms=m.c.perf_first_frame_ms,
                   prefill_ms=m.c.perf_prefill_ms, ref_frames=63)
+        if wavs is not None:
+            # the same from the 5 s reference AUDIO: the encode is on the first-packet path
+            for _ in range(2):
+                m.generate_voice_clone_audio_stream(prompts[0], wavs[0], vc[0][0], "english", chunk_frames=8)
+            fp["first_packet_from_audio_ms"] = m.c.perf_first_packet_ms
     roof = None if args.no_profile or vc is not None else profile_roofline(m, qtts.lib())
     m.close()
 
