@@ -15,7 +15,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libqwen_tts_amd.so")
+# QTTS_LIB: another build of the same library (A/B measurements of two builds
+# in one process tree); the default is the in-tree build
+LIB_PATH = os.environ.get("QTTS_LIB") or os.path.join(HERE, "lib", "libqwen_tts_amd.so")
 CLI_PATH = os.path.join(HERE, "bin", "qwen-tts")
 
 _fp = C.POINTER(C.c_float)
