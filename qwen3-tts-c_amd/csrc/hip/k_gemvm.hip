@@ -120,7 +120,7 @@ __device__ __forceinline__ void gm_stage(const GemvArgs &a, const float *inv, un
 // thread: unit i = tid + blockDim*q, wave-uniform batch row); the per-64-unit
 // partial sums of squares of a row are adjacent and summed in order.
 // XU == 0: statistics pre-pass + (chunked) staging.
-template <bool NT, int U, int XU, int KS>
+template <int U, int XU, int KS>
 __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x, nw = nthr >> 6;
@@ -159,8 +159,7 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
             int j = g * U + u;
             j = j < J ? j : J - 1;                    // clamp: loads stay unconditional
             const v4u *p = wr + ((32 * (ksl + KS * j)) >> 3);
-            if constexpr (NT) wv[u] = __builtin_nontemporal_load(p);
-            else wv[u] = *p;
+            wv[u] = *p;   // default policy: non-temporal loads of these 64-B row fragments measured 5-20 % slower
         }
     };
     if (ng > 0) load(0);
@@ -368,9 +367,8 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     const dim3 grid((T + tpw - 1) / tpw, kz);
     a.C = Cfull;
 #define QTTS_GM(UU, XX, KK)                                                                                   \
-    if (a.nt) hipLaunchKernelGGL((k_gemvm<true, UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);            \
-    else hipLaunchKernelGGL((k_gemvm<false, UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);                \
-    qtts_last_kernel = a.nt ? "k_gemvm<true, " #UU ", " #XX ", " #KK ">" : "k_gemvm<false, " #UU ", " #XX ", " #KK ">";
+    hipLaunchKernelGGL((k_gemvm<UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);                            \
+    qtts_last_kernel = "k_gemvm<" #UU ", " #XX ", " #KK ">";
 #define QTTS_GMX(UU, KK)                                       \
     if (XU == 4) { QTTS_GM(UU, 4, KK) }                        \
     else if (XU == 8) { QTTS_GM(UU, 8, KK) }                   \
