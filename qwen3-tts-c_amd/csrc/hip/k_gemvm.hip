@@ -114,6 +114,34 @@ __device__ __forceinline__ void gm_stage(const GemvArgs &a, const float *inv, un
     }
 }
 
+// Self-reducing split-K (GemvArgs::tick), hand-off form R1 of
+// cdna_hip_programming.md Guideline 16 (as k_attn_dec's split merge): the
+// partials went out write-through (sc1), every wave drains them, one relaxed
+// ticket add per workgroup; the last column to arrive adds the kz partials of
+// its row block in column order to the residual (the order the consumer's
+// xadd prologue used) and resets the ticket.
+__device__ __forceinline__ void gm_reduce_last(const GemvArgs &a, int tpw, int *flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(a.tick + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = old == (int)gridDim.y - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    const int nr = 16 * tpw, rb = blockIdx.x * nr;
+    for (int i = threadIdx.x; i < a.nb * nr; i += blockDim.x) {
+        const int b = i / nr, r = rb + (i - b * nr);
+        if (r >= a.R) continue;
+        const float *p = a.ypart + (size_t)b * a.R + r;
+        float s = ld_sc1(p);
+        for (int z = 1; z < (int)gridDim.y; ++z) s += ld_sc1(p + z * a.ld_ypart);
+        float *y = a.y + (size_t)b * a.ldy + r;
+        *y = *y + s;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(a.tick + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // A workgroup = TPW row tiles of 16 rows x KS waves per tile (the K steps of a
 // tile dealt round-robin to its KS waves).
 // XU > 0: register prologue (whole rows, C % 256 == 0, <= XU float4 units per
@@ -265,6 +293,21 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     __syncthreads();   // the planes are dead: red aliases them
     red[w * 64 + lane] = acc;
     __syncthreads();
+    if (a.tick) {      // self-reducing split-K producer (every thread reaches the ticket barrier)
+        if (ksl == 0 && r0 < a.R) {
+            floatx4 v = red[w * 64 + lane];
+#pragma unroll
+            for (int k = 1; k < KS; ++k) v += red[(w + k) * 64 + lane];
+            const int r = r0 + rl;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int bb = 4 * (lane >> 4) + i;
+                if (bb < nb && r < a.R) st_sc1(a.ypart + blockIdx.y * a.ld_ypart + (size_t)bb * a.R + r, v[i]);
+            }
+        }
+        gm_reduce_last(a, tpw, reinterpret_cast<int *>(inv));
+        return;
+    }
     if (ksl != 0 || r0 >= a.R) return;
     floatx4 v = red[w * 64 + lane];
 #pragma unroll
@@ -366,6 +409,11 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     const size_t smem = (size_t)region + (16 + (a.nb * a.C / 256 > 64 ? a.nb * a.C / 256 : 64)) * 4;
     const dim3 grid((T + tpw - 1) / tpw, kz);
     a.C = Cfull;
+    if (a.tick && (!a.ypart || !a.y || a.epi != EPI_RESID || (int)grid.x > QTTS_GM_TICKS)) {
+        fprintf(stderr, "qtts_gemvm: self-reducing split-K needs ypart, y, EPI_RESID and <= %d row blocks\n",
+                QTTS_GM_TICKS);
+        return -1;
+    }
 #define QTTS_GM(UU, XX, KK)                                                                                   \
     hipLaunchKernelGGL((k_gemvm<UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);                            \
     qtts_last_kernel = "k_gemvm<" #UU ", " #XX ", " #KK ">";

@@ -5,6 +5,8 @@
 
 typedef uint16_t bf16_t;
 
+constexpr int QTTS_GM_TICKS = 1024;   // self-reducing split-K tickets (row blocks per launch)
+
 enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SILU = 2, EPI_RESID = 3, EPI_SWIGLU = 4 };
 
 struct GemvArgs {
@@ -38,6 +40,11 @@ struct GemvArgs {
     float *ypart = nullptr;
     size_t ld_ypart = 0;
     int kz = 1;
+    // self-reducing split-K (EPI_RESID only): one zeroed ticket per grid.x
+    // workgroup; the last of the kz columns to finish a row block adds the
+    // partials in order to the residual, y = y + (p0 + p1 + ...), and resets
+    // its ticket, so the next GEMV reads y alone (no xadd)
+    int *tick = nullptr;            // [QTTS_GM_TICKS]
     const float *norm_w = nullptr;  // RMSNorm weights [C] (nullptr: no norm)
     float eps = 1e-6f;
     float *xcopy = nullptr;         // workgroup 0 writes x rows here

@@ -118,6 +118,7 @@ struct qtts_dev {
     int *stop_step = nullptr, *kv_len = nullptr, *n_trailing = nullptr;
     float *att_part = nullptr;   // split-K decode attention partials (talker)
     int *att_cnt = nullptr, att_nsplit = 0;
+    int *btick = nullptr;        // self-reducing batch split-K tickets [QTTS_GM_TICKS] (zeroed)
     uint32_t *rng = nullptr, *st_rng = nullptr;
     float *trailing = nullptr, *prefill = nullptr, *pad_emb = nullptr;
     // prefill / prompt scratch
@@ -545,6 +546,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
         A(att_cnt, int, B * kvmax);
         CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
+        A(btick, int, QTTS_GM_TICKS);
+        CK(hipMemsetAsync(dv->btick, 0, QTTS_GM_TICKS * sizeof(int), dv->st));
     }
 #undef A
     dv->p_len_h.assign(nb, 0);
@@ -755,8 +758,15 @@ static int bsplit_kz(const qtts_dev *dv, int R, int C) {
     while (kz > 1 && C % (32 * kz)) kz /= 2;
     return kz > 1 ? kz : 0;
 }
-static void split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz) {
-    g.y = nullptr; g.ypart = part; g.kz = kz; g.ld_ypart = (size_t)dv->nrun * g.R;
+// Above 8 rows the producer reduces its own partials (GemvArgs::tick: its
+// last column adds them to the residual) and nothing is pending; up to 8 the
+// consumer adds them (returns true).  Measured (profiles/r02r_bsplit_self_ab.txt):
+// batch 16 174.3 vs 169.5 audio-s/s self-reducing, batch 8 109.9 vs 113.9.
+static bool split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz) {
+    g.ypart = part; g.kz = kz; g.ld_ypart = (size_t)dv->nrun * g.R;
+    if (dv->nrun > 8) { g.tick = dv->btick; return false; }
+    g.y = nullptr;
+    return true;
 }
 static void add_in(GemvArgs &g, const float *part, int n, int R, int nrun, float *xnew) {
     g.xadd = part; g.n_xadd = n; g.ld_xadd = nrun * R; g.ldb_xadd = R;
@@ -786,15 +796,15 @@ static int talker_layers(qtts_dev *dv) {
         CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
         if (pend) { std::swap(xa, xb); pend = nullptr; }
         GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
-        if (kzo) split_out(dv, o, dv->bpo, kzo);
+        const bool opend = kzo && split_out(dv, o, dv->bpo, kzo);
         CKI(pgemv(dv, o, PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
-        if (kzo) add_in(a, dv->bpo, kzo, d.H, nb, xb);
+        if (opend) add_in(a, dv->bpo, kzo, d.H, nb, xb);
         CKI(pgemv(dv, a, PK_GEMV_TALKER));
-        if (kzo) std::swap(xa, xb);
+        if (opend) std::swap(xa, xb);
         GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
-        if (kzd) { split_out(dv, dn, dv->bpd, kzd); pend = dv->bpd; npend = kzd; }
+        if (kzd && split_out(dv, dn, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
         CKI(pgemv(dv, dn, PK_GEMV_TALKER));
     }
     dv->tk_xfin = xa; dv->tk_pend = pend; dv->tk_npend = npend;
@@ -897,7 +907,7 @@ static int subtalker(qtts_dev *dv) {
             t.cnt = dv->att_cnt;
             GemvArgs o = gv(ly.wo, d.Hs, AD, dv->att_s, AD, xa, d.Hs, nb, EPI_RESID);
             o.nt = 0;
-            bool fused_o = false;
+            bool fused_o = false, opend = false;
             // (batch 1 only: at batch 8 / 16 the per-row recompute measured slower than
             // the separate attention + split-K O projection, 98 vs 107 / 132 vs 155
             // audio-s/s, profiles/r01av_bench_batch_attn_o.txt)
@@ -916,7 +926,7 @@ static int subtalker(qtts_dev *dv) {
                     ps.cancel();
                     { ProfScope pa(dv, PK_ATTN, 0); CKI(qtts_attention(t, st)); }
                     o.y = xa;
-                    if (kzo) split_out(dv, o, dv->bpo, kzo);
+                    if (kzo) opend = split_out(dv, o, dv->bpo, kzo);
                     if (!kv_only) CKI(pgemv(dv, o, PK_GEMV_SUB));
                 } else {
                     fused_o = true;
@@ -925,7 +935,7 @@ static int subtalker(qtts_dev *dv) {
                 CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 o.y = xa;
-                if (kzo) split_out(dv, o, dv->bpo, kzo);
+                if (kzo) opend = split_out(dv, o, dv->bpo, kzo);
                 if (!kv_only) CKI(pgemv(dv, o, PK_GEMV_SUB));
             }
             if (kv_only) break;
@@ -934,14 +944,14 @@ static int subtalker(qtts_dev *dv) {
             if (tab0) set_src(a);   // the residual is the input table row (x_st was not written)
             if (fused_o) {
                 add_in(a, dv->opart, d.KVs, d.Hs, nb, xb);
-            } else if (kzo) {
+            } else if (opend) {
                 add_in(a, dv->bpo, kzo, d.Hs, nb, xb);
             }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
-            if (fused_o || kzo) std::swap(xa, xb);
+            if (fused_o || opend) std::swap(xa, xb);
             a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xa, d.Hs, nb, EPI_RESID);
             a.nt = 0;
-            if (kzd) { split_out(dv, a, dv->bpd, kzd); pend = dv->bpd; npend = kzd; }
+            if (kzd && split_out(dv, a, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
         }
         if (g == 0) continue;  // pass 0 produces no logits

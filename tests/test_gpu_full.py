@@ -179,6 +179,23 @@ def test_full_batch8_vs_oracle_c4(full_tts, full_oracle):
         _audio_close(audio[b], full_oracle.codec_decode(codes_o))
 
 
+def test_full_batch12_self_reducing_split_k(full_tts, full_oracle):
+    """12 utterances in lock step (above 8 rows the O / down split-K producer
+    reduces its own partials): 3 distinct prompts x 4; the distinct slots
+    against their oracle runs, the repeats bit-equal to them."""
+    prompts = [prompt_ids("p128", 1450 + i % 3) for i in range(12)]
+    spk = ["aiden", "vivian", "serena"] * 4
+    full_tts.set_params(max_tokens=4096, fixed=3, seed=42, **DEFAULT)
+    rc, audio = full_tts.generate_batch(prompts, spk, ["english"] * 12)
+    assert rc == 0
+    for b in range(3):
+        s, l = lookup_ids(full_oracle.cfg, spk[b], "english")
+        codes_o, _ = full_oracle.generate_codes(prompts[b], s, l, max_tokens=4096, fixed=3, seed=42, **DEFAULT)
+        _audio_close(audio[b], full_oracle.codec_decode(codes_o))
+    for b in range(3, 12):
+        np.testing.assert_array_equal(audio[b], audio[b % 3])
+
+
 def test_full_voice_clone_b8_vs_oracle_c5(full_tts, full_oracle):
     """BASELINE C5 (1.7B voice clone, batch 8): ICL prompts of 20-34
     reference frames + x-vectors (> 64 prefill rows: the matrix-core

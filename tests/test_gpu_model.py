@@ -143,6 +143,31 @@ def test_batch_slots_match_single_runs(tiny_dir, oracle, monkeypatch, env):
         m.close()
 
 
+def test_batch12_self_reducing_split_k(tiny_dir, oracle):
+    """Above 8 slots the O / down split-K producer adds its own partials to
+    the residual (the last workgroup column of a row block, k_gemvm ticket);
+    12 slots, each equal to its own oracle run, twice on one ctx (the tickets
+    are reset by their last arriver)."""
+    m = qtts.QwenTTS(tiny_dir)
+    try:
+        prompts = [prompt_ids("p128", 1250 + i) for i in range(12)]
+        spk = ["aiden", "vivian", "serena"] * 4
+        lang = ["english", "japanese", "chinese", "english"] * 3
+        m.set_params(max_tokens=4096, fixed=8, seed=42, **DEFAULT)
+        rc, audio = m.generate_batch(prompts, spk, lang)
+        assert rc == 0
+        for b in range(12):
+            s, l = lookup_ids(oracle.cfg, spk[b], lang[b])
+            codes, _ = oracle.generate_codes(prompts[b], s, l, max_tokens=4096, fixed=8, seed=42, **DEFAULT)
+            audio_close(audio[b], oracle.codec_decode(codes))
+        rc, again = m.generate_batch(prompts, spk, lang)
+        assert rc == 0
+        for b in range(12):
+            np.testing.assert_array_equal(again[b], audio[b])
+    finally:
+        m.close()
+
+
 def test_batch_eos_slots_stop_independently(tiny_eos_dir):
     """Slots stop at their own EOS; finished slots keep their frame count."""
     o = Oracle(tiny_eos_dir)
