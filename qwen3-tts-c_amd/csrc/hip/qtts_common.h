@@ -27,15 +27,48 @@ __device__ __forceinline__ void unpack8(const v4u &w, float (&f)[8]) {
 }
 
 // wave64 reductions
+// Wave-wide reductions on the VALU cross-lane paths: DPP inside rows of 16
+// lanes, v_permlane16/32_swap across rows (gfx950).  __shfl_xor compiles to
+// ds_bpermute_b32, an LDS round trip per step (~0.3 us for a dependent
+// 6-step sum, profiles/r02r_batch_gemvm_decomp.txt).  A butterfly: lane ^ 1,
+// lane ^ 2 (quad_perm), then the other quad of the 8 (row_half_mirror) and
+// the other 8 of the row (row_mirror) -- every lane of the partner group
+// already holds the same bits, so the mirror partners are as good as xor 4 /
+// xor 8 -- then row pairs and halves (each swap's two results are the lane's
+// value and its partner's).  Every lane returns the same bits.
+template <int CTRL>
+__device__ __forceinline__ float dpp_get(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float swap16_other(float v, float &mine) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    mine = __uint_as_float(r[0]);
+    return __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap32_other(float v, float &mine) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    mine = __uint_as_float(r[0]);
+    return __uint_as_float(r[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_get<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_get<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_get<0x141>(v);   // row_half_mirror
+    v += dpp_get<0x140>(v);   // row_mirror
+    float a, b = swap16_other(v, a);
+    v = a + b;
+    b = swap32_other(v, a);
+    return a + b;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, dpp_get<0xB1>(v));
+    v = fmaxf(v, dpp_get<0x4E>(v));
+    v = fmaxf(v, dpp_get<0x141>(v));
+    v = fmaxf(v, dpp_get<0x140>(v));
+    float a, b = swap16_other(v, a);
+    v = fmaxf(a, b);
+    b = swap32_other(v, a);
+    return fmaxf(a, b);
 }
 // 256-thread block reduction (4 waves); red must hold >= 4 floats; all threads get the result
 __device__ __forceinline__ float block_sum256(float v, float *red) {

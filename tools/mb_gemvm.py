@@ -2,7 +2,10 @@
 """Micro-benchmark of the decode GEMV dispatcher (qtts_hip_decode_matvec_bf16)
 at batch 1..16 on the 1.7B decode shapes: mean us per call over a burst of
 back-to-back launches (torch events on the current stream), and the weight
-stream rate.  QTTS_LIB selects a build (A/B)."""
+stream rate.  QTTS_LIB selects a build (A/B).  The eager launches cost ~6.5 us
+of host time each, so points below that are launch-rate bound: run it under
+`rocprofv3 --kernel-trace` (tools/trace_by_grid.py) for device durations."""
+import argparse
 import json
 import os
 import sys
@@ -18,23 +21,32 @@ SHAPES = {  # name: (rows, cols, norm)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--batch", default="1,2,4,8,16", help="comma-separated batch sizes")
+    ap.add_argument("--n", type=int, default=200, help="timed launches per point")
+    args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
+    batches = [int(b) for b in args.batch.split(",")]
     import torch
     import qtts
     dev = torch.device("cuda:0")
     out = {}
     for name, (R, Cc, norm) in SHAPES.items():
+        if only and name not in only:
+            continue
         A = torch.randint(0, 1 << 15, (R, Cc), dtype=torch.int16, device=dev).view(torch.uint16) \
             if hasattr(torch, "uint16") else torch.randint(0, 1 << 15, (R, Cc), dtype=torch.int16, device=dev)
         # keep the bf16 values finite and small: exponent bits of 0x3Fxx
         A = (A.to(torch.int32) & 0x007F | 0x3F00).to(torch.int16)
         w = torch.ones(Cc, device=dev) if norm else None
-        for B in (1, 2, 4, 8, 16):
+        for B in batches:
             x = torch.randn(B, Cc, device=dev)
             y = torch.zeros(B, R, device=dev)
             for _ in range(5):
                 qtts.Kernels.decode_matvec_bf16(y, A, x, w, 1e-6, R, Cc, B)
             torch.cuda.synchronize()
-            n = 200
+            n = args.n
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(n):
