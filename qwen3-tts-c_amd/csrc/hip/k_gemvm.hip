@@ -71,46 +71,165 @@ __device__ __forceinline__ void split_store(float4 v, unsigned short *hp, int pl
     *reinterpret_cast<uint2 *>(hp + 2 * plane_stride) = make_uint2(a3, b3);
 }
 
-// float4 of batch row b at column c (fp32 row, or bf16 / fp32 table row by id)
-__device__ __forceinline__ float4 gm_load(const GemvArgs &a, int b, int c) {
-    if (a.table) {
-        const bf16_t *t = a.table + (size_t)gm_row_id(a, b) * a.C + c;
-        const uint2 q = *reinterpret_cast<const uint2 *>(t);
-        return make_float4(lo_f(q.x), hi_f(q.x), lo_f(q.y), hi_f(q.y));
-    }
-    if (a.table_f32) return *reinterpret_cast<const float4 *>(a.table_f32 + (size_t)gm_row_id(a, b) * a.C + c);
-    float4 v = *reinterpret_cast<const float4 *>(a.x + (size_t)b * a.ldx + c);
-    if (a.xadd) {   // the residual plus a split-K producer's partials, summed in order first
-        const float *xp = a.xadd + (size_t)b * a.ldb_xadd + c;
-        float4 sacc = *reinterpret_cast<const float4 *>(xp);
-        for (int p = 1; p < a.n_xadd; ++p) {
-            const float4 t = *reinterpret_cast<const float4 *>(xp + (size_t)p * a.ld_xadd);
-            sacc.x += t.x; sacc.y += t.y; sacc.z += t.z; sacc.w += t.w;
-        }
-        v.x += sacc.x; v.y += sacc.y; v.z += sacc.z; v.w += sacc.w;
-    }
-    return v;
+struct NoIssue { __device__ __forceinline__ void operator()() const {} };
+
+// Source loads of N float4 units (unit i: batch row i / n4, columns c0 +
+// 4 (i % n4); a unit at or past nu reads unit 0's address and is ignored by
+// the caller).  Every load of the batch is issued before any is used: loads
+// retire in issue order, so a load issued behind another waits for it (the
+// former per-unit loader, branching on the source kind around each load,
+// waited for the whole previous load -- the weight group included -- before
+// every unit).  Order: x / table rows, the split-K partials p < PM (held in
+// registers), the norm weights (NW), then `issue` (the weight stream); then
+// the partials are summed in order p = 0, 1, ... (p >= PM read from memory)
+// and added to the residual, as GemvArgs::xadd prescribes.
+// buffer descriptor over a wave-uniform base (kernel arguments): loads take a
+// 32-bit byte offset instead of a 64-bit address per lane (cdna_hip_programming.md T8)
+// (readfirstlane makes the uniformity provable: no waterfall loop per load, T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gm_rsrc(const void *p) {
+    const uint64_t u = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    void *q = (void *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ float4 gm_ld4(__amdgpu_buffer_rsrc_t r, unsigned eoff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, eoff * 4u, 0, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
-// normalise (inv / norm_w), copy out (workgroup 0), split into the planes
-__device__ __forceinline__ void gm_put(const GemvArgs &a, float4 v, int b, int c, int cl, float iv,
+// Source kinds (GM_SRC_*): a kernel specialised on one has no branch between
+// its loads, so the compiler's vmcnt bookkeeping stays exact (a uniform
+// branch between source kinds that issue different loads into different
+// registers makes it wait for every outstanding load -- the weights
+// included -- at the join); GM_SRC_ANY decides at run time (generic path).
+enum { GM_SRC_X = 0, GM_SRC_XADD = 1, GM_SRC_TAB = 2, GM_SRC_TABF = 3, GM_SRC_ANY = 4 };
+
+template <int SRC>
+__device__ __forceinline__ bool gm_is(const GemvArgs &a, int kind) {
+    if constexpr (SRC != GM_SRC_ANY) return SRC == kind;
+    switch (kind) {
+        case GM_SRC_TAB: return a.table != nullptr;
+        case GM_SRC_TABF: return a.table == nullptr && a.table_f32 != nullptr;
+        case GM_SRC_XADD: return !a.table && !a.table_f32 && a.xadd != nullptr;
+        default: return !a.table && !a.table_f32 && a.xadd == nullptr;
+    }
+}
+
+template <int SRC, int N, int PM, bool NW, class Issue>
+__device__ __forceinline__ void gm_fetch(const GemvArgs &a, int i0, int step, int nu, int n4, int c0,
+                                         float4 (&v)[N], float4 (&nw)[N], Issue issue) {
+    // element offsets (every source here is far below 2^29 elements)
+    unsigned b[N], c[N];
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+        int i = i0 + step * u;
+        i = i < nu ? i : 0;
+        b[u] = (unsigned)(i / n4);
+        c[u] = (unsigned)(c0 + 4 * (i - (int)b[u] * n4));
+    }
+    const bool tab = gm_is<SRC>(a, GM_SRC_TAB), tabf = gm_is<SRC>(a, GM_SRC_TABF), xadd = gm_is<SRC>(a, GM_SRC_XADD);
+    const int np = xadd ? a.n_xadd : 0;
+    float4 pv[N][PM];
+    uint2 tq[N];
+    if (tab || tabf) {
+        // ids: the row selectors of all units, then the ids (two round trips)
+        unsigned id[N];
+        const int *ip = a.ids + a.ids_off;
+        if (a.row_sel) {
+            int rs[N];
+#pragma unroll
+            for (int u = 0; u < N; ++u) rs[u] = a.row_sel[b[u]];
+#pragma unroll
+            for (int u = 0; u < N; ++u)
+                id[u] = (unsigned)ip[b[u] * (unsigned)a.ids_bstride + (unsigned)rs[u] * (unsigned)a.ids_rstride];
+        } else {
+#pragma unroll
+            for (int u = 0; u < N; ++u) id[u] = (unsigned)ip[b[u] * (unsigned)a.ids_bstride];
+        }
+        if (tab) {
+            const auto rt = gm_rsrc(a.table);
+#pragma unroll
+            for (int u = 0; u < N; ++u) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b64(rt, (id[u] * (unsigned)a.C + c[u]) * 2u, 0, 0);
+                tq[u] = make_uint2(q[0], q[1]);
+            }
+        } else {
+            const auto rt = gm_rsrc(a.table_f32);
+#pragma unroll
+            for (int u = 0; u < N; ++u) v[u] = gm_ld4(rt, id[u] * (unsigned)a.C + c[u]);
+        }
+    } else {
+        const auto rx = gm_rsrc(a.x);
+#pragma unroll
+        for (int u = 0; u < N; ++u) v[u] = gm_ld4(rx, b[u] * (unsigned)a.ldx + c[u]);
+        if (xadd) {
+            // partials p < PM: unconditional loads (p clamped to the last one),
+            // only the sum below looks at np
+            const auto rp = gm_rsrc(a.xadd);
+#pragma unroll
+            for (int p = 0; p < PM; ++p) {
+                const unsigned pp = (unsigned)(p < np ? p : np - 1);
+#pragma unroll
+                for (int u = 0; u < N; ++u)
+                    pv[u][p] = gm_ld4(rp, pp * (unsigned)a.ld_xadd + b[u] * (unsigned)a.ldb_xadd + c[u]);
+            }
+        }
+    }
+    if constexpr (NW) {
+        if (a.norm_w) {
+            const auto rn = gm_rsrc(a.norm_w);
+#pragma unroll
+            for (int u = 0; u < N; ++u) nw[u] = gm_ld4(rn, c[u]);
+        }
+    }
+    issue();
+    if (tab) {
+#pragma unroll
+        for (int u = 0; u < N; ++u) v[u] = make_float4(lo_f(tq[u].x), hi_f(tq[u].x), lo_f(tq[u].y), hi_f(tq[u].y));
+    } else if (xadd) {   // (tables carry no partials: host check)
+        const auto rp = gm_rsrc(a.xadd);
+#pragma unroll
+        for (int u = 0; u < N; ++u) {
+            float4 s = pv[u][0];
+#pragma unroll
+            for (int p = 1; p < PM; ++p)
+                if (p < np) { s.x += pv[u][p].x; s.y += pv[u][p].y; s.z += pv[u][p].z; s.w += pv[u][p].w; }
+            for (int p = PM; p < np; ++p) {
+                const float4 t = gm_ld4(rp, (unsigned)p * (unsigned)a.ld_xadd + b[u] * (unsigned)a.ldb_xadd + c[u]);
+                s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+            }
+            v[u].x += s.x; v[u].y += s.y; v[u].z += s.z; v[u].w += s.w;
+        }
+    }
+}
+
+// normalise (inv / norm weights nw), copy out (workgroup 0), split into the planes
+__device__ __forceinline__ void gm_put(const GemvArgs &a, float4 v, float4 nw, int b, int c, int cl, float iv,
                                        unsigned short *hp, int LDH, int PS) {
     if (a.xcopy && blockIdx.x == 0 && !a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + (size_t)b * a.ldxc + c) = v;
     if (a.norm_w) {
-        const float4 nw = *reinterpret_cast<const float4 *>(a.norm_w + c);
         v.x = v.x * iv * nw.x; v.y = v.y * iv * nw.y; v.z = v.z * iv * nw.z; v.w = v.w * iv * nw.w;
         if (a.xcopy && blockIdx.x == 0 && a.xcopy_normed) *reinterpret_cast<float4 *>(a.xcopy + (size_t)b * a.ldxc + c) = v;
     }
     split_store(v, hp + b * LDH + cl, PS);
 }
 
-// stage columns [c0, c0 + CCH) of the nb rows (chunked / generic path)
+// stage columns [c0, c0 + CCH) of the nb rows (chunked / generic path), 2
+// units per thread in flight (the chunked stage runs with a weight group live)
 __device__ __forceinline__ void gm_stage(const GemvArgs &a, const float *inv, unsigned short *hp, int LDH, int PS,
                                          int c0, int CCH) {
-    const int n4 = CCH / 4;
-    for (int i = threadIdx.x; i < a.nb * n4; i += blockDim.x) {
-        const int b = i / n4, cl = 4 * (i - b * n4);
-        gm_put(a, gm_load(a, b, c0 + cl), b, c0 + cl, cl, a.norm_w ? inv[b] : 1.f, hp, LDH, PS);
+    const int n4 = CCH / 4, nu = a.nb * n4, nt = blockDim.x;
+    for (int i0 = threadIdx.x; i0 < nu; i0 += 2 * nt) {
+        float4 v[2], nw[2];
+        gm_fetch<GM_SRC_ANY, 2, 1, true>(a, i0, nt, nu, n4, c0, v, nw, NoIssue());
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + nt * u;
+            if (i < nu) {
+                const int b = i / n4, cl = 4 * (i - b * n4);
+                gm_put(a, v[u], nw[u], b, c0 + cl, cl, a.norm_w ? inv[b] : 1.f, hp, LDH, PS);
+            }
+        }
     }
 }
 
@@ -148,7 +267,7 @@ __device__ __forceinline__ void gm_reduce_last(const GemvArgs &a, int tpw, int *
 // thread: unit i = tid + blockDim*q, wave-uniform batch row); the per-64-unit
 // partial sums of squares of a row are adjacent and summed in order.
 // XU == 0: statistics pre-pass + (chunked) staging.
-template <int U, int XU, int KS>
+template <int U, int XU, int KS, int SRC>
 __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nthr = blockDim.x, nw = nthr >> 6;
@@ -174,10 +293,15 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     const int tile = blockIdx.x * tpw + tw;
     const int r0 = tile * 16, rl = lane & 15, kq = 8 * (lane >> 4);
     const int row = r0 + rl < a.R ? r0 + rl : a.R - 1;
-    const v4u *wr = reinterpret_cast<const v4u *>(a.W + (size_t)row * ldw + woff + kq);
+    // weights through a buffer descriptor: one 32-bit offset per lane (host: R * C * 2 < 2^31)
+    const auto rw = gm_rsrc(a.W);
+
     const int nsteps = C / 32;
     const int J = r0 < a.R ? (nsteps - ksl + KS - 1) / KS : 0;   // this wave's K steps: s = ksl + KS * j
     const int ng = (J + U - 1) / U;
+    // (a wave with no K step, J == 0, still issues its loads unconditionally:
+    // they read the row's first step)
+    const unsigned wb = ((unsigned)row * (unsigned)ldw + (unsigned)(woff + kq + (J > 0 ? 32 * ksl : 0))) * 2u;
     const int spc = CCH / 32 / KS;                    // steps per wave per chunk (chunked mode)
 
     v4u wv[U];
@@ -185,21 +309,37 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int j = g * U + u;
-            j = j < J ? j : J - 1;                    // clamp: loads stay unconditional
-            const v4u *p = wr + ((32 * (ksl + KS * j)) >> 3);
-            wv[u] = *p;   // default policy: non-temporal loads of these 64-B row fragments measured 5-20 % slower
+            j = j < J ? j : (J > 0 ? J - 1 : 0);     // clamp: loads stay unconditional (row is clamped too)
+            // default policy: non-temporal loads of these 64-B row fragments measured 5-20 % slower
+            wv[u] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rw, wb + (unsigned)(64 * KS * j), 0, 0));
         }
     };
-    if (ng > 0) load(0);
-
     // ---- prologue
     if constexpr (XU > 0) {
         const int n4 = C / 4, nu = nb * n4;
-        float4 xv[XU];
+        // the x rows, their partials and norm weights first, then the weights
+        // (partials in registers: XU * PM <= 8 float4; above 4 units the norm
+        // weights come behind the weights, so x, partials and weights fit)
+        constexpr int PM = XU <= 2 ? 4 : 2;
+        constexpr bool NWE = XU <= 4;
+        float4 xv[XU], nwv[XU];
+        // (load(0) unconditional: a divergent branch around it would make the
+        // compiler's vmcnt bookkeeping wait for the weights at every x use)
+        gm_fetch<SRC, XU, PM, NWE>(a, tid, nthr, nu, n4, 0, xv, nwv, [&]() { load(0); });
+        if constexpr (!NWE) {
+            if (a.norm_w) {
+                // offsets recomputed from an opaque copy of tid: reusing the
+                // fetch's (spilled) ones would reload them from scratch, and a
+                // scratch load makes the next wait drain the weights too
+                int t = tid;
+                asm volatile("" : "+v"(t));
 #pragma unroll
-        for (int q = 0; q < XU; ++q) {
-            const int i = tid + nthr * q;
-            if (i < nu) xv[q] = gm_load(a, i / n4, 4 * (i % n4));
+                for (int q = 0; q < XU; ++q) {
+                    int i = t + nthr * q;
+                    i = i < nu ? i : 0;
+                    nwv[q] = gm_ld4(gm_rsrc(a.norm_w), 4u * (unsigned)(i % n4));
+                }
+            }
         }
         if (a.norm_w) {
 #pragma unroll
@@ -223,16 +363,21 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
             const int i = tid + nthr * q;
             if (i < nu) {
                 const int bb = i / n4, c = 4 * (i % n4);
-                gm_put(a, xv[q], bb, c, c, a.norm_w ? inv[bb] : 1.f, hp, LDH, PS);
+                gm_put(a, xv[q], nwv[q], bb, c, c, a.norm_w ? inv[bb] : 1.f, hp, LDH, PS);
             }
         }
     } else {
+        load(0);
         if (a.norm_w) {
+            const int n4 = C / 4;
             for (int bb = w; bb < nb; bb += nw) {
                 float ss = 0.f;
-                for (int c = 4 * lane; c < C; c += 256) {
-                    const float4 v = gm_load(a, bb, c);
-                    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                for (int k0 = lane; k0 < n4; k0 += 4 * 64) {   // columns 4 k, k = k0 + 64 u, in order
+                    float4 v[4], nwd[4];
+                    gm_fetch<GM_SRC_ANY, 4, 1, false>(a, bb * n4 + k0, 64, bb * n4 + n4, n4, 0, v, nwd, NoIssue());
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (k0 + 64 * u < n4) ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
                 }
                 ss = wave_sum(ss);
                 if (lane == 0) inv[bb] = rms_inv(ss, C, a.eps);
@@ -351,7 +496,7 @@ static int gm_planes(int nb, int cch) { return 3 * nb * (cch + 8) * 2; }
 // -1 launch error.
 int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     GemvArgs a = in;
-    if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32) return 1;
+    if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32 || (size_t)a.R * a.C * 2 >= ((size_t)1 << 31)) return 1;
     if (a.table) {
         if (a.C % 4) return 1;
     } else if (a.table_f32) {
@@ -404,7 +549,7 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     }
     const int nthr = 64 * KS * tpw, nu = a.nb * a.C / 4;
     const int xu = (cch == a.C && a.C % 256 == 0) ? (nu + nthr - 1) / nthr : 0;
-    const int XU = xu == 0 || xu > 8 ? 0 : xu <= 4 ? 4 : 8;
+    const int XU = xu == 0 || xu > 8 ? 0 : xu <= 1 ? 1 : xu <= 2 ? 2 : xu <= 4 ? 4 : xu <= 6 ? 6 : 8;
     const int region = std::max(gm_planes(a.nb, cch), nthr / 64 * 64 * 16);
     const size_t smem = (size_t)region + (16 + (a.nb * a.C / 256 > 64 ? a.nb * a.C / 256 : 64)) * 4;
     const dim3 grid((T + tpw - 1) / tpw, kz);
@@ -414,13 +559,22 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
                 QTTS_GM_TICKS);
         return -1;
     }
+    const int src = a.table ? GM_SRC_TAB : a.table_f32 ? GM_SRC_TABF : a.xadd ? GM_SRC_XADD : GM_SRC_X;
+#define QTTS_GMS(UU, XX, KK, SS)                                                                              \
+    hipLaunchKernelGGL((k_gemvm<UU, XX, KK, SS>), grid, dim3(nthr), smem, st, a, tpw);                        \
+    qtts_last_kernel = "k_gemvm<" #UU ", " #XX ", " #KK ", " #SS ">";
 #define QTTS_GM(UU, XX, KK)                                                                                   \
-    hipLaunchKernelGGL((k_gemvm<UU, XX, KK>), grid, dim3(nthr), smem, st, a, tpw);                            \
-    qtts_last_kernel = "k_gemvm<" #UU ", " #XX ", " #KK ">";
+    if (src == GM_SRC_X) { QTTS_GMS(UU, XX, KK, GM_SRC_X) }                                                   \
+    else if (src == GM_SRC_XADD) { QTTS_GMS(UU, XX, KK, GM_SRC_XADD) }                                        \
+    else if (src == GM_SRC_TAB) { QTTS_GMS(UU, XX, KK, GM_SRC_TAB) }                                          \
+    else { QTTS_GMS(UU, XX, KK, GM_SRC_TABF) }
 #define QTTS_GMX(UU, KK)                                       \
-    if (XU == 4) { QTTS_GM(UU, 4, KK) }                        \
+    if (XU == 1) { QTTS_GM(UU, 1, KK) }                        \
+    else if (XU == 2) { QTTS_GM(UU, 2, KK) }                   \
+    else if (XU == 4) { QTTS_GM(UU, 4, KK) }                   \
+    else if (XU == 6) { QTTS_GM(UU, 6, KK) }                   \
     else if (XU == 8) { QTTS_GM(UU, 8, KK) }                   \
-    else { QTTS_GM(UU, 0, KK) }
+    else { QTTS_GMS(UU, 0, KK, GM_SRC_ANY) }
 #define QTTS_GMK(UU)                                           \
     if (KS == 16) { QTTS_GMX(UU, 16) }                         \
     else if (KS == 8) { QTTS_GMX(UU, 8) }                      \
@@ -430,6 +584,7 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     else { QTTS_GMK(2) }
 #undef QTTS_GMK
 #undef QTTS_GMX
+#undef QTTS_GMS
 #undef QTTS_GM
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
