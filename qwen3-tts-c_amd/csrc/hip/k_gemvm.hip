@@ -525,6 +525,10 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
     int KS = 16 / (tpw == 3 ? 4 : tpw);
     while (KS > 4 && nsteps < 2 * KS) KS /= 2;
     if (tpw * KS > 16) tpw = 16 / KS;
+    // three tiles x 4 waves leave 768 threads, so > 4 x units per thread at
+    // batch >= 8 (whose registers, with the partials and the weight group in
+    // flight, spill): four tiles per 1024-thread workgroup instead
+    if (tpw == 3 && (a.nb * a.C / 4 + 767) / 768 > 4) { tpw = 4; KS = 4; }
     // column chunk: the whole row when it fits, else the fewest equal chunks
     // of whole 32 x KS-column step rounds with an even step count per wave
     int cch = a.C;
