@@ -264,16 +264,51 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
     const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
 
-    // ---- issue every cache load of this split first: K rows for the scores,
-    // V rows for P.V (the current token's come from LDS later) ----
+    // ---- the token's own inputs first (q / k head values, norm weights, RoPE
+    // rows, v): issued behind the cache loads they would wait for all of them
+    // (loads retire in issue order) ----
+    constexpr int HJ = (HD + 63) / 64;
+    static_assert(GPH + 1 <= 4, "one wave per q / k head");
+    // (every load of the kernel is unconditional, from a clamped valid
+    // address: a load under a divergent branch makes the compiler's vmcnt
+    // bookkeeping drain everything outstanding at the join)
+    const int hh0 = w < GPH ? w : GPH;   // GPH + 1 <= 4 heads: one per wave (wave 3 repeats the k head)
+    float hv[HJ], hw[HJ];
+    {
+        const float *src = hh0 < GPH ? row + (kvh * GPH + hh0) * HD : row + a.NH * HD + kvh * HD;
+        const float *nw = hh0 < GPH ? a.qn_w : a.kn_w;
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) {
+            const int i = (lane + 64 * j) % HD;
+            hv[j] = src[i];
+            hw[j] = nw[i];
+        }
+    }
+    constexpr int RJ = ((GPH + 1) * HD + 255) / 256;
+    float rc[RJ], rs[RJ];
+    {
+        const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) {
+            const int e = (tid + 256 * j) % HD;
+            rc[j] = cs[e];
+            rs[j] = sn[e];
+        }
+    }
+    const float vtok = row[(a.NH + a.KV) * HD + kvh * HD + tid % HD];
+    __builtin_amdgcn_sched_barrier(0);   // keep the cache loads behind these
+
+    // ---- then every cache load of this split: K rows for the scores, V rows
+    // for P.V (the current token's come from LDS later) ----
     const int kl = tid / LPK, ksub = tid - kl * LPK;
     const int tk = t0 + kl;
-    const bool kld = tk < t1 && tk != p;
+    // (rows past the split or the current token's own read a valid row and
+    // are never used: the scores skip t >= t1 and take t == p from LDS)
     float4 kreg[DPL / 4];
     {
-        const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(kld ? tk : 0) * KVD + ksub * DPL);
+        const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(tk < t1 ? tk : t0) * KVD + ksub * DPL);
 #pragma unroll
-        for (int j = 0; j < DPL / 4; ++j) kreg[j] = kld ? kp[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < DPL / 4; ++j) kreg[j] = kp[j];
     }
     const int d4 = tid % D4, kg = tid / D4;
     constexpr int NV = (CH + KG - 1) / KG;
@@ -281,38 +316,32 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int t = t0 + kg + j * KG;
-        const bool ok = kg + j * KG < CH && t < t1 && t != p;
-        vreg[j] = ok ? reinterpret_cast<const float4 *>(Vc + (size_t)t * KVD)[d4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = kg + j * KG < CH && t < t1;   // (t == p: read, then replaced from LDS)
+        vreg[j] = reinterpret_cast<const float4 *>(Vc + (size_t)(ok ? t : t0) * KVD)[d4];
     }
 
     // ---- prologue: q heads (waves 0..GPH-1), k head (wave GPH), v ----
-    for (int hh = w; hh <= GPH; hh += 4) {
-        const float *src = hh < GPH ? row + (kvh * GPH + hh) * HD : row + a.NH * HD + kvh * HD;
-        const float *nw = hh < GPH ? a.qn_w : a.kn_w;
-        float v[(HD + 63) / 64];
+    if (w <= GPH) {
         float ss = 0.f;
 #pragma unroll
-        for (int j = 0; j < (HD + 63) / 64; ++j) {
-            const int i = lane + 64 * j;
-            v[j] = i < HD ? src[i] : 0.f;
-            ss += v[j] * v[j];
-        }
+        for (int j = 0; j < HJ; ++j) ss += lane + 64 * j < HD ? hv[j] * hv[j] : 0.f;   // (HD < 64: lanes past HD repeat)
         ss = wave_sum(ss);
         const float iv = rms_inv(ss, HD, a.eps);
 #pragma unroll
-        for (int j = 0; j < (HD + 63) / 64; ++j) {
+        for (int j = 0; j < HJ; ++j) {
             const int i = lane + 64 * j;
-            if (i < HD) xn[hh * HD + i] = v[j] * iv * nw[i];
+            if (i < HD) xn[hh0 * HD + i] = hv[j] * iv * hw[j];
         }
     }
-    if (owner && tid < HD) vv[tid] = row[(a.NH + a.KV) * HD + kvh * HD + tid];
+    if (owner && tid < HD) vv[tid] = vtok;
     __syncthreads();
-    {
-        const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
-        for (int i = tid; i < (GPH + 1) * HD; i += 256) {
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+        const int i = tid + 256 * j;
+        if (i < (GPH + 1) * HD) {
             const int e = i % HD, hb = i - e;
             constexpr int half = HD / 2;
-            qk[i] = e < half ? xn[i] * cs[e] - xn[hb + e + half] * sn[e] : xn[i] * cs[e] + xn[hb + e - half] * sn[e];
+            qk[i] = e < half ? xn[i] * rc[j] - xn[hb + e + half] * rs[j] : xn[i] * rc[j] + xn[hb + e - half] * rs[j];
         }
     }
     __syncthreads();

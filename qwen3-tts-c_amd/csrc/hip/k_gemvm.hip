@@ -24,9 +24,18 @@
 // steps round-robin; lane l loads W[r0 + (l & 15)][32 s + 8 (l >> 4) .. +7]
 // (one 16-B load = the B fragment) and reads x[l & 15][same columns] of the
 // three planes from LDS (the A fragments).  Weight loads run U steps ahead in
-// registers, the first group issued before the prologue.  The four partial
-// 16x16 tiles are summed in wave order through LDS; wave 0 applies the
-// epilogue.
+// registers, the first group issued right behind the prologue's own loads.
+// The KS partial 16x16 tiles are summed in wave order through LDS; the
+// tile's first wave applies the epilogue.
+//
+// Load order (loads retire in issue order, so a load waits for every load
+// issued before it): x rows / table rows, split-K partials and norm weights
+// first, then the weight group, all through buffer descriptors (32-bit
+// offsets) and with no branch between them -- the kernel is specialised on
+// the source kind (GM_SRC_*), because a branch between differently-loading
+// paths makes the compiler drain every outstanding load, the weights
+// included, at the join.  (The former per-unit loader did exactly that for
+// every x unit: batch 8 117.1 -> 123.4 audio-s/s.)
 //
 // Prologue: the nb x rows (fp32 rows, or bf16 / fp32 table rows gathered by
 // device-side ids) are RMS-normalised (K.c:27-39, x * inv * w), split once and

@@ -58,6 +58,15 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
                                            ld_sc1(src + 4 * l + 3));
         else x = reinterpret_cast<const float4 *>(src)[l];
     }
+    // the norm weights and RoPE rows of this lane right behind x: issued after
+    // the K / V / W_o loads they would wait for all of them (in-order retire)
+    float4 nwq = zero4, c4 = zero4, s4 = zero4;
+    if (seg < 3) {
+        nwq = reinterpret_cast<const float4 *>(seg < 2 ? a.qn_w : a.kn_w)[l];
+        c4 = reinterpret_cast<const float4 *>(a.rope_cos + (size_t)p * HD)[l];
+        s4 = reinterpret_cast<const float4 *>(a.rope_sin + (size_t)p * HD)[l];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the K / V / W_o loads behind these
     const int dI = tid / LPK, sub = tid - dI * LPK, gs = dI / NK, ts = dI - gs * NK;
     const bool kld = gs < 2 && ts < p;
     float4 kr[4];
@@ -76,7 +85,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
     for (int o = D4 / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
     if (seg < 3) {
         const float iv = rms_inv(ss, HD, a.eps);
-        const float4 w = reinterpret_cast<const float4 *>(seg < 2 ? a.qn_w : a.kn_w)[l];
+        const float4 w = nwq;
         x.x = x.x * iv * w.x; x.y = x.y * iv * w.y; x.z = x.z * iv * w.z; x.w = x.w * iv * w.w;
     }
     float4 o4;
@@ -85,8 +94,6 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
     if (seg < 4) {
         float4 y = x;
         if (seg < 3) {
-            const float4 c4 = reinterpret_cast<const float4 *>(a.rope_cos + (size_t)p * HD)[l];
-            const float4 s4 = reinterpret_cast<const float4 *>(a.rope_sin + (size_t)p * HD)[l];
             if (l < D4 / 2) {   // x[i] c[i] - x[i+half] s[i]
                 y.x = x.x * c4.x - o4.x * s4.x; y.y = x.y * c4.y - o4.y * s4.y;
                 y.z = x.z * c4.z - o4.z * s4.z; y.w = x.w * c4.w - o4.w * s4.w;
