@@ -337,21 +337,24 @@ __global__ __launch_bounds__(1024) void k_gemv1(GemvArgs a) {
         if (a.table) trow = a.table + off;
         else xrow = a.table_f32 + off;
     }
+    // (a bf16 table row stays packed until the weights are in flight)
     float4 xv[XV], wn[XV];
+    uint2 tv[XV];
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const int c = 4 * (tid + nthr * i);
         const int cc = c < C ? c : C - 4;
-        if (trow) {
-            const uint2 t = *reinterpret_cast<const uint2 *>(trow + cc);
-            xv[i] = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
-                                __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
-        } else {
-            xv[i] = *reinterpret_cast<const float4 *>(xrow + cc);
-        }
+        if (trow) tv[i] = *reinterpret_cast<const uint2 *>(trow + cc);
+        else xv[i] = *reinterpret_cast<const float4 *>(xrow + cc);
         if (a.norm_w) wn[i] = *reinterpret_cast<const float4 *>(a.norm_w + cc);
     }
     ws.load(0);
+    if (trow) {
+#pragma unroll
+        for (int i = 0; i < XV; ++i)
+            xv[i] = make_float4(__uint_as_float(tv[i].x << 16), __uint_as_float(tv[i].x & 0xFFFF0000u),
+                                __uint_as_float(tv[i].y << 16), __uint_as_float(tv[i].y & 0xFFFF0000u));
+    }
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
@@ -476,7 +479,8 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
         if (nthr != 256 && nblk > 8 && nblk <= 16) {   // wide: every weight load of a lane in one group
             switch (xv) { case 1: QTTS_G1(16, 1) break; case 2: QTTS_G1(16, 2) break;
                           case 4: QTTS_G1(16, 4) break; default: QTTS_G1(8, 8) break; }
-        } else if (nblk >= 8) {
+        } else if (nblk > 4) {   // (5..8 blocks: one group of 8, not two of 4 -- the second
+                                 //  would only issue after the prologue's barrier)
             switch (xv) { case 1: QTTS_G1(8, 1) break; case 2: QTTS_G1(8, 2) break;
                           case 4: QTTS_G1(8, 4) break; default: QTTS_G1(8, 8) break; }
         } else {

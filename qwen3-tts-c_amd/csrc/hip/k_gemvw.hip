@@ -68,19 +68,17 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     // partials held in registers (the sub-talker's 8 per-head O partials at
     // C = 1024); wider rows sum them from memory below
     constexpr int PMAX = XQ == 1 ? 8 : 0;
+    // (a bf16 table row stays packed until the weights are in flight:
+    // converting it here would wait for it before the weight loads issue)
     float4 xv[XQ], pv[XQ][PMAX > 0 ? PMAX : 1], nwv[XQ];
+    uint2 tv[XQ];
     const int np = a.xadd ? a.n_xadd : 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
         const int c = 4 * (tid + 256 * q);
         const int cc = c < C ? c : 0;
-        if (trow) {
-            const uint2 t = *reinterpret_cast<const uint2 *>(trow + cc);
-            xv[q] = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xFFFF0000u),
-                                __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xFFFF0000u));
-        } else {
-            xv[q] = *reinterpret_cast<const float4 *>(xrow + cc);
-        }
+        if (trow) tv[q] = *reinterpret_cast<const uint2 *>(trow + cc);
+        else xv[q] = *reinterpret_cast<const float4 *>(xrow + cc);
 #pragma unroll
         for (int p = 0; p < PMAX; ++p)
             if (p < np) pv[q][p] = *reinterpret_cast<const float4 *>(a.xadd + (size_t)p * a.ld_xadd + cc);
@@ -100,6 +98,12 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     }
 
     // 3. residual + partials summed in partial order, RMS statistic
+    if (trow) {
+#pragma unroll
+        for (int q = 0; q < XQ; ++q)
+            xv[q] = make_float4(__uint_as_float(tv[q].x << 16), __uint_as_float(tv[q].x & 0xFFFF0000u),
+                                __uint_as_float(tv[q].y << 16), __uint_as_float(tv[q].y & 0xFFFF0000u));
+    }
     float ss = 0.f;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {

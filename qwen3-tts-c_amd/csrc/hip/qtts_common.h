@@ -113,7 +113,8 @@ __constant__ uint64_t kExp2fTab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull,
 };
-__device__ __forceinline__ float expf_glibc(float x) {
+template <class Tab>
+__device__ __forceinline__ float expf_glibc_core(float x, Tab tab) {
 #pragma clang fp contract(off)
     if (x > 0x1.62e42ep6f) return __builtin_inff();
     if (x < -0x1.9fe368p6f) return 0.0f;
@@ -128,7 +129,7 @@ __device__ __forceinline__ float expf_glibc(float x) {
     uint64_t ki = (uint64_t)__double_as_longlong(kd);
     kd -= kShift;
     double r = __fma_rn(kInvLn2N, xd, -kd);
-    uint64_t t = kExp2fTab[ki % 32];
+    uint64_t t = tab((int)(ki % 32));
     t += ki << (52 - 5);
     double s = __longlong_as_double((long long)t);
     double zz = __fma_rn(C0, r, C1);
@@ -137,6 +138,20 @@ __device__ __forceinline__ float expf_glibc(float x) {
     y = __fma_rn(zz, r2, y);
     y = y * s;
     return (float)y;
+}
+__device__ __forceinline__ float expf_glibc(float x) {
+    return expf_glibc_core(x, [](int i) { return kExp2fTab[i]; });
+}
+// The same with the table held by the wave (lane l: kExp2fTab[l & 31], loaded
+// with the kernel's first loads) and read across lanes: the global table read
+// is a dependent memory round trip per call.  Every lane of the wave must be
+// active.
+__device__ __forceinline__ float expf_glibc_wave(float x, uint64_t tab_lane) {
+    return expf_glibc_core(x, [&](int i) {
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)tab_lane, i, 64);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(tab_lane >> 32), i, 64);
+        return ((uint64_t)hi << 32) | lo;
+    });
 }
 
 // Write-through ("sc1") 4-byte store / load at agent scope: the hand-off form

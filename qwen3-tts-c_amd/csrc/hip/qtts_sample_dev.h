@@ -276,7 +276,7 @@ __device__ __forceinline__ void block_scan2(FastSmem &fs, int x, int y, int &ex,
 // and the first j whose running sum reaches r (K.c:451-477), every lane
 // walking the same broadcast values.  Lane 0 owns the RNG.  Returns the id
 // (all lanes).  (v_readlane per step measured 2-3x slower than the LDS reads.)
-__device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rng) {
+__device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rng, uint64_t etab) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     unsigned long long *keys = reinterpret_cast<unsigned long long *>(fs.top_v);   // 64 x 8 B scratch
@@ -305,7 +305,10 @@ __device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rn
     if (lane < ke) pv[rank] = vj;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const float v0 = pv[0];
-    if (lane < ke) e = expf_glibc(pv[lane] - v0);
+    {   // every lane active for the table's cross-lane reads
+        const float ee = expf_glibc_wave(lane < ke ? pv[lane] - v0 : 0.f, etab);
+        if (lane < ke) e = ee;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane < ke) pv[lane] = e;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -340,7 +343,8 @@ __device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rn
 
 // Returns the sampled id (all threads).  v[]: logits / temperature.
 template <int EM>
-__device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[EM], int E, int n, int k, uint32_t &rng) {
+__device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[EM], int E, int n, int k, uint32_t &rng,
+                                                uint64_t etab) {
 #pragma clang fp contract(off)
     const int tid = threadIdx.x;
     uint32_t kk[EM];
@@ -377,7 +381,7 @@ __device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[E
     __syncthreads();
     if (ke <= 64) {   // the common case (top-k 50): one wave sorts and draws
         if (tid < 64) {
-            const int t = wave_sort_draw(fs, ke, rng);
+            const int t = wave_sort_draw(fs, ke, rng, etab);
             if (tid == 0) fs.misc[0] = t;
         }
         __syncthreads();
@@ -461,6 +465,7 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
         x[j] = ok ? (FAST_ONLY ? ld_sc1(lg + i) : lg[i]) : -INFINITY;   // FAST_ONLY = GEMV tail: sc1 hand-off
         cnt[j] = (ok && pen) ? a.counts[(size_t)b * n + i] : 0;
     }
+    const uint64_t etab = kExp2fTab[tid & 31];   // expf_glibc_wave's table, with the first loads
     if (tid == 0) { U.fast.misc[1] = stopped; U.fast.misc[2] = ng; }
     __syncthreads();
     if (U.fast.misc[1]) return;
@@ -484,12 +489,12 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
         float v[EM];
 #pragma unroll
         for (int j = 0; j < EM; ++j) v[j] = div_rn(x[j], temp);
-        tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng);
+        tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
         if (a.mode == 1 && a.fixed > 0 && tok == a.eos && ng < a.fixed) {   // Q.c:1315-1321
 #pragma unroll
             for (int j = 0; j < EM; ++j)
                 if (i0 + j == a.eos) v[j] = div_rn(-1e9f, temp);
-            tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng);
+            tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
         }
     } else if constexpr (!FAST_ONLY) {
         SampSmem &sm = U.full;
