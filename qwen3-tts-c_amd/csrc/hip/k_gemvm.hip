@@ -257,15 +257,22 @@ __device__ __forceinline__ void gm_reduce_last(const GemvArgs &a, int tpw, int *
     }
     __syncthreads();
     if (!flag[0]) return;
-    const int nr = 16 * tpw, rb = blockIdx.x * nr;
+    const int nr = 16 * tpw, rb = blockIdx.x * nr, kz = gridDim.y;
     for (int i = threadIdx.x; i < a.nb * nr; i += blockDim.x) {
         const int b = i / nr, r = rb + (i - b * nr);
         if (r >= a.R) continue;
+        // every partial (kz <= 4, host) and the residual issued before the sum
         const float *p = a.ypart + (size_t)b * a.R + r;
-        float s = ld_sc1(p);
-        for (int z = 1; z < (int)gridDim.y; ++z) s += ld_sc1(p + z * a.ld_ypart);
         float *y = a.y + (size_t)b * a.ldy + r;
-        *y = *y + s;
+        float t[4];
+#pragma unroll
+        for (int z = 0; z < 4; ++z) t[z] = ld_sc1(p + (size_t)(z < kz ? z : 0) * a.ld_ypart);
+        const float y0 = *y;
+        float s = t[0];
+#pragma unroll
+        for (int z = 1; z < 4; ++z)
+            if (z < kz) s += t[z];
+        *y = y0 + s;
     }
     if (threadIdx.x == 0) __hip_atomic_store(a.tick + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -519,7 +526,7 @@ int qtts_gemvm(const GemvArgs &in, hipStream_t st) {
                    a.n_xadd < 1))
         return 1;
     const int kz = a.ypart ? a.kz : 1;
-    if (a.ypart && (kz < 2 || a.norm_w || a.table || a.table_f32 || a.xcopy || a.C % (32 * kz) ||
+    if (a.ypart && (kz < 2 || (a.tick && kz > 4) || a.norm_w || a.table || a.table_f32 || a.xcopy || a.C % (32 * kz) ||
                     ((uintptr_t)a.ypart & 3)))
         return 1;
     const int Cfull = a.C;

@@ -761,7 +761,10 @@ static int bsplit_kz(const qtts_dev *dv, int R, int C) {
 // Above 8 rows the producer reduces its own partials (GemvArgs::tick: its
 // last column adds them to the residual) and nothing is pending; up to 8 the
 // consumer adds them (returns true).  Measured (profiles/r02r_bsplit_self_ab.txt):
-// batch 16 174.3 vs 169.5 audio-s/s self-reducing, batch 8 109.9 vs 113.9.
+// batch 16 174.3 vs 169.5 audio-s/s self-reducing, batch 8 109.9 vs 113.9;
+// again after the loads of both sides were unserialised (gpurun_out ab5, same
+// box): self-reducing at every batch size gave batch 2 38.7 vs 42.6, 4 70.5
+// vs 76.0, 8 123.6 vs 126.3, 16 193.3 vs 189.0.
 static bool split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz) {
     g.ypart = part; g.kz = kz; g.ld_ypart = (size_t)dv->nrun * g.R;
     if (dv->nrun > 8) { g.tick = dv->btick; return false; }
