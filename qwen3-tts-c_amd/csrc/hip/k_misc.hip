@@ -13,15 +13,35 @@ __global__ __launch_bounds__(256) void k_embed_sum(EmbedSumArgs a) {
 #pragma clang fp contract(off)
     const int b = blockIdx.y;
     const int d = blockIdx.x * 256 + threadIdx.x;
-    if (a.stopped && a.stopped[b]) return;
+    // three dependent round trips, each with all of its loads in flight:
+    // (stop flag, row, trailing count) -> (16 codes) -> (16 embedding rows + the text row)
+    const int stop = a.stopped ? a.stopped[b] : 0;
     const int row = a.cur_row[b];
+    const int ntr = a.n_trailing[b];
+    if (stop) return;
     const int *cd = a.codes + (size_t)b * a.codes_bstride + (size_t)row * a.G;
+    constexpr int GM = 16;   // code groups (host: G <= 16)
+    // (groups past G repeat group G - 1's load and are left out of the sum:
+    // no branch around a load)
+    int c[GM];
+#pragma unroll
+    for (int g = 0; g < GM; ++g) c[g] = cd[g < a.G ? g : a.G - 1];
     if (d < a.H) {
+        const float *tt = row < ntr ? a.trailing + ((size_t)b * a.tr_cap + row) * a.H : a.pad;
+        float e[GM];
+        e[0] = bf2f(a.codec_emb[(size_t)c[0] * a.H + d]);
+#pragma unroll
+        for (int g = 1; g < GM; ++g) {
+            const int gg = g < a.G ? g : a.G - 1;
+            e[g] = bf2f(a.st_emb[((size_t)(gg - 1) * a.Vs + c[g]) * a.H + d]);
+        }
+        const float t = tt[d];
         float s = 0.0f;
-        s += bf2f(a.codec_emb[(size_t)cd[0] * a.H + d]);
-        for (int g = 1; g < a.G; ++g) s += bf2f(a.st_emb[((size_t)(g - 1) * a.Vs + cd[g]) * a.H + d]);
-        const float *tt = row < a.n_trailing[b] ? a.trailing + ((size_t)b * a.tr_cap + row) * a.H : a.pad;
-        s += tt[d];
+        s += e[0];
+#pragma unroll
+        for (int g = 1; g < GM; ++g)
+            if (g < a.G) s += e[g];
+        s += t;
         a.out[(size_t)b * a.H + d] = s;
     }
     if (a.advance && blockIdx.x == 0 && threadIdx.x == 0) a.kv_len[b] += 1;
@@ -65,6 +85,10 @@ __global__ void k_copy_rows(float *dst, int ldd, const float *src, int lds, cons
 }  // namespace
 
 int qtts_embed_sum(const EmbedSumArgs &a, hipStream_t st) {
+    if (a.G < 2 || a.G > 16) {
+        fprintf(stderr, "qtts_embed_sum: %d code groups (2..16 supported)\n", a.G);
+        return -1;
+    }
     hipLaunchKernelGGL(k_embed_sum, dim3((a.H + 255) / 256, a.nb), dim3(256), 0, st, a);
     qtts_last_kernel = "k_embed_sum";
     return hipGetLastError() == hipSuccess ? 0 : -1;

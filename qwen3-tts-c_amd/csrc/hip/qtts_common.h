@@ -60,6 +60,18 @@ __device__ __forceinline__ float wave_sum(float v) {
     b = swap32_other(v, a);
     return a + b;
 }
+// Inclusive wave prefix sum of ints on DPP: row_shr 1, 2, 4, 8 inside rows of
+// 16 (zeros shifted in), then row_bcast:15 / row_bcast:31 carry the row
+// totals (the 6-step __shfl_up scan is six LDS round trips).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_get<0xB1>(v));
     v = fmaxf(v, dpp_get<0x4E>(v));

@@ -209,14 +209,9 @@ __device__ __forceinline__ void radix_select_regs(FastSmem &fs, const uint32_t (
             c[i] = fs.hist[par][0][bin] + fs.hist[par][1][bin] + fs.hist[par][2][bin] + fs.hist[par][3][bin];
             tot += c[i];
         }
-        int inc = tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-        }
+        const int inc = wave_incl_scan(tot);
         if (ne < 0) {
-            ne = __shfl(inc, 63, 64);
+            ne = __builtin_amdgcn_readlane(inc, 63);
             if (k > ne) k = ne;
             rem = k;
         }
@@ -232,9 +227,9 @@ __device__ __forceinline__ void radix_select_regs(FastSmem &fs, const uint32_t (
         }
         const unsigned long long hit = __ballot(bin >= 0);
         const int src = hit ? __ffsll((long long)hit) - 1 : 0;
-        bin = __shfl(bin, src, 64);
-        nrem = __shfl(nrem, src, 64);
-        cbin = __shfl(cbin, src, 64);
+        bin = __builtin_amdgcn_readlane(bin, src);   // (src is wave-uniform: from the ballot)
+        nrem = __builtin_amdgcn_readlane(nrem, src);
+        cbin = __builtin_amdgcn_readlane(cbin, src);
         // clear this wave's other buffer for the next pass (its readers finished before this barrier)
 #pragma unroll
         for (int i = 0; i < 4; ++i) fs.hist[par ^ 1][w][lane + 64 * i] = 0;
@@ -253,12 +248,7 @@ __device__ __forceinline__ void block_scan2(FastSmem &fs, int x, int y, int &ex,
     // exclusive scans of two small per-thread counts packed in one int (16 | 16 bits)
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int v = x | (y << 16);
-    int inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int z = __shfl_up(inc, o, 64);
-        if (l >= o) inc += z;
-    }
+    const int inc = wave_incl_scan(v);
     if (l == 63) fs.scan[0][w] = inc;
     __syncthreads();
     int base = 0;
