@@ -377,8 +377,7 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
         }
 #pragma unroll
         for (int g = 0; g < GPH; ++g) {
-#pragma unroll
-            for (int o = LPK >> 1; o >= 1; o >>= 1) d[g] += __shfl_xor(d[g], o, 64);
+            d[g] = group_sum<LPK>(d[g]);
             if (sub == 0) sc[g][kl] = t < t1 ? d[g] * scale : -INFINITY;
         }
     }
@@ -529,8 +528,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
         acc = fmaf(f[4], x1.x, acc); acc = fmaf(f[5], x1.y, acc);
         acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
     }
-#pragma unroll
-    for (int o = LPS / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    acc = group_sum<LPS>(acc);
     if (sub == 0 && row < R) part[((size_t)kvh * gridDim.z + b) * R + row] = acc;
 }
 

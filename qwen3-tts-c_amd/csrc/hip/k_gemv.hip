@@ -140,9 +140,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         float v = acc[b];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
+        v = group_sum<8>(v);
         acc[b] = v;
     }
     __syncthreads();  // xs no longer read; red may alias nothing but be safe
@@ -231,9 +229,7 @@ struct G1Stream {
                     acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
                 }
             }
-            acc += __shfl_xor(acc, 1, 64);
-            acc += __shfl_xor(acc, 2, 64);
-            acc += __shfl_xor(acc, 4, 64);
+            acc = group_sum<8>(acc);
             return acc;
         }
         for (int g = 0; g < ng; ++g) {
@@ -257,9 +253,7 @@ struct G1Stream {
                 }
             }
         }
-        acc += __shfl_xor(acc, 1, 64);
-        acc += __shfl_xor(acc, 2, 64);
-        acc += __shfl_xor(acc, 4, 64);
+        acc = group_sum<8>(acc);
         return acc;
     }
 };

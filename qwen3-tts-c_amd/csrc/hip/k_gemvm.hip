@@ -478,7 +478,8 @@ __global__ __launch_bounds__(1024) void k_gemvm(GemvArgs a, int tpw) {
     for (int i = 0; i < 4; ++i) {
         const int bb = 4 * (lane >> 4) + i;
         const float val = v[i];
-        const float up = __shfl(val, (lane & 15) < 12 ? lane + 4 : lane, 64);
+        // lane + 4 within the 16-lane row (row_shl:4; lanes 12-15 keep their own, unused)
+        const float up = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(val), __float_as_int(val), 0x104, 0xF, 0xF, false));
         if (bb >= nb || r >= a.R) continue;
         if (a.ypart) {
             a.ypart[blockIdx.y * a.ld_ypart + (size_t)bb * a.R + r] = val;

@@ -81,16 +81,19 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
 
     // ---- per-head RMSNorm (T.c:646-649) + RoPE (T.c:650-653) -> LDS; k, v -> cache (T.c:654-655)
     float ss = x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
-#pragma unroll
-    for (int o = D4 / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    ss = group_sum<D4>(ss);
     if (seg < 3) {
         const float iv = rms_inv(ss, HD, a.eps);
         const float4 w = nwq;
         x.x = x.x * iv * w.x; x.y = x.y * iv * w.y; x.z = x.z * iv * w.z; x.w = x.w * iv * w.w;
     }
     float4 o4;
-    o4.x = __shfl_xor(x.x, D4 / 2, 64); o4.y = __shfl_xor(x.y, D4 / 2, 64);
-    o4.z = __shfl_xor(x.z, D4 / 2, 64); o4.w = __shfl_xor(x.w, D4 / 2, 64);
+    if constexpr (D4 / 2 == 16) {   // the rotate-half partner one row away
+        o4.x = xor16_get(x.x); o4.y = xor16_get(x.y); o4.z = xor16_get(x.z); o4.w = xor16_get(x.w);
+    } else {
+        o4.x = __shfl_xor(x.x, D4 / 2, 64); o4.y = __shfl_xor(x.y, D4 / 2, 64);
+        o4.z = __shfl_xor(x.z, D4 / 2, 64); o4.w = __shfl_xor(x.w, D4 / 2, 64);
+    }
     if (seg < 4) {
         float4 y = x;
         if (seg < 3) {
@@ -122,8 +125,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
                 d += q.x * k.x + q.y * k.y + q.z * k.z + q.w * k.w;
             }
         }
-#pragma unroll
-        for (int o = LPK / 2; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
+        d = group_sum<LPK>(d);
         if (sub == 0 && gs < 2) sc[gs][ts] = ts < n ? d * div_rn(1.0f, sqrt_rn((float)HD)) : -INFINITY;
     }
     __syncthreads();
@@ -133,12 +135,10 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
         const int g = tid / NK, t = tid - g * NK;
         const float s = sc[g][t];
         float m = s;
-#pragma unroll
-        for (int o = NK / 2; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        m = group_max<NK>(m);
         const float e = t < n ? expf(s - m) : 0.f;
         float sum = e;
-#pragma unroll
-        for (int o = NK / 2; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        sum = group_sum<NK>(sum);
         sc[g][t] = e * div_rn(1.0f, sum);
     }
     __syncthreads();

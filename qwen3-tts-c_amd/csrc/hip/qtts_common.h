@@ -60,6 +60,39 @@ __device__ __forceinline__ float wave_sum(float v) {
     b = swap32_other(v, a);
     return a + b;
 }
+// Sums / maxima over aligned groups of N lanes (N a power of two <= 64; every
+// lane of a group gets the group's value) on the same DPP / permlane steps as
+// wave_sum -- the __shfl_xor butterflies they replace were one ds_bpermute
+// (an LDS round trip) per step.
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {
+    if constexpr (N >= 2) v += dpp_get<0xB1>(v);
+    if constexpr (N >= 4) v += dpp_get<0x4E>(v);
+    if constexpr (N >= 8) v += dpp_get<0x141>(v);
+    if constexpr (N >= 16) v += dpp_get<0x140>(v);
+    if constexpr (N >= 32) { float a, b = swap16_other(v, a); v = a + b; }
+    if constexpr (N >= 64) { float a, b = swap32_other(v, a); v = a + b; }
+    return v;
+}
+template <int N>
+__device__ __forceinline__ float group_max(float v) {
+    if constexpr (N >= 2) v = fmaxf(v, dpp_get<0xB1>(v));
+    if constexpr (N >= 4) v = fmaxf(v, dpp_get<0x4E>(v));
+    if constexpr (N >= 8) v = fmaxf(v, dpp_get<0x141>(v));
+    if constexpr (N >= 16) v = fmaxf(v, dpp_get<0x140>(v));
+    if constexpr (N >= 32) { float a, b = swap16_other(v, a); v = fmaxf(a, b); }
+    if constexpr (N >= 64) { float a, b = swap32_other(v, a); v = fmaxf(a, b); }
+    return v;
+}
+// value of lane ^ 16: v_permlane16_swap(v, v) swaps the odd rows of its first
+// result with the even rows of its second, so an even row finds its partner
+// in the second result and an odd row in the first (swap16_other returns the
+// second, which only a symmetric use -- a + b -- may take as "the other")
+__device__ __forceinline__ float xor16_get(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+}
+
 // Inclusive wave prefix sum of ints on DPP: row_shr 1, 2, 4, 8 inside rows of
 // 16 (zeros shifted in), then row_bcast:15 / row_bcast:31 carry the row
 // totals (the 6-step __shfl_up scan is six LDS round trips).
