@@ -459,6 +459,37 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     }
     __syncthreads();
     if (!last) return;
+    if (nact <= 8) {   // every partial of this thread's outputs in flight at once, then the merge in split order
+#pragma unroll
+        for (int j = 0; j < (NO + 255) / 256; ++j) {
+            const int o = tid + 256 * j;
+            const int oc = o < NO ? o : 0, g = oc / HD;
+            float mm[8], ll[8], aa[8];
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) {
+                const float *ps = base + (size_t)(s2 < nact ? s2 : 0) * stride;
+                mm[s2] = ld_sc1(ps + NO + 2 * g);
+                ll[s2] = ld_sc1(ps + NO + 2 * g + 1);
+                aa[s2] = ld_sc1(ps + oc);
+            }
+            float M = -INFINITY;
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2)
+                if (s2 < nact) M = fmaxf(M, mm[s2]);
+            float num = 0.f, den = 0.f;
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) {
+                if (s2 < nact) {
+                    const float f = expf(mm[s2] - M);
+                    num += f * aa[s2];
+                    den += f * ll[s2];
+                }
+            }
+            if (o < NO) outr[o] = num / den;
+        }
+        if (tid == 0) __hip_atomic_store(a.cnt + r * a.KV + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < (NO + 255) / 256; ++j) {
         const int o = tid + 256 * j;

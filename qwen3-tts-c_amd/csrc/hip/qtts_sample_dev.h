@@ -314,7 +314,7 @@ __device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rn
     if (!(sum > 0.0f)) return fs.top_i[0];
     float r = 0.f;
     if (lane == 0) r = rand_uniform(rng) * sum;
-    r = __shfl(r, 0, 64);
+    r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 0));
     float c = 0.f;
     for (int j0 = 0; j0 < ke; j0 += 8) {
         float p[8];
