@@ -196,7 +196,10 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
     if (a.xcopy && ((uintptr_t)a.xcopy & 15)) return 1;
     const int NV = a.C / 512;
     int RW = a.R / 1024;
-    if (RW * NV > 16 && a.R % 2048 == 0) RW = a.R / 2048;   // two workgroups per CU
+    // two workgroups per CU where the slice would be large -- except the 1.7B
+    // talker's down projection (2048 x 6144): one workgroup of 2 x 12 loads
+    // per lane, 32.0 vs 31.96 audio-s/s for k_gemv1's wide config (same box)
+    if (RW * NV > 16 && a.R % 2048 == 0 && NV != 12) RW = a.R / 2048;
     if (RW * NV > 24 || (a.epi == EPI_SWIGLU && (RW & 1))) return 1;
     const dim3 grid(a.R / (4 * RW), a.reps);
     const size_t smem = (size_t)(a.C + 4) * sizeof(float);
@@ -214,11 +217,11 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
     // sub-talker (Hs 1024) and 0.6B talker (H 1024): q|k|v 4096x1024, gate|up
     // 6144x1024, down 1024x3072, lm heads 2048x1024, O 1024x2048, codec head
     // 3072x1024; 1.7B talker (H 2048): q|k|v 4096x2048, O 2048x2048, gate|up
-    // 12288x2048 (grid 512), codec head 3072x2048.  (The talker's down
-    // projection 2048x6144 as RW 1, NV 12 measured 6.8 vs 5.9 us on k_gemv1's
-    // wide config, profiles/r02h_frame_trace_*.txt: left to k_gemv1.)
+    // 12288x2048 (grid 512), down 2048x6144 (RW 2, NV 12), codec head
+    // 3072x2048.  (The down projection as RW 1, NV 12 on grid 512 measured
+    // 6.8 vs 5.9 us on k_gemv1's wide config, profiles/r02h_frame_trace_*.txt.)
     QTTS_GW(4, 2) QTTS_GW(6, 2) QTTS_GW(1, 6) QTTS_GW(2, 2) QTTS_GW(1, 4) QTTS_GW(1, 2) QTTS_GW(3, 2)
-    QTTS_GW(2, 4) QTTS_GW(4, 4) QTTS_GW(6, 4) QTTS_GW(3, 4)
+    QTTS_GW(2, 4) QTTS_GW(4, 4) QTTS_GW(6, 4) QTTS_GW(3, 4) QTTS_GW(2, 12)
 #undef QTTS_GW
     return 1;
 }
