@@ -123,6 +123,13 @@ int qtts_dev_get_codes(qtts_dev_t *dev, int b, int *host_codes, int max_frames);
 /* Codec decode of slot b's generated codes (device-resident) into a malloc'd
  * host buffer of T*1920 samples (caller frees). */
 float *qtts_dev_codec_slot(qtts_dev_t *dev, int b, int T, int *out_samples);
+/* Per-stage timing of the full codec decodes (the reference's -v -v line
+ * "Codec stages (ms): rvq= preconv= transformer= upsample= vocoder=",
+ * c/qwen_tts_codec.c:743-746): on != 0 records HIP events between the stages
+ * of every later qtts_dev_codec_slot / _decode_host; stage_ms fills ms[5] in
+ * that order for the last one (-1 when it was not timed). */
+int qtts_dev_codec_timing(qtts_dev_t *dev, int on);
+int qtts_dev_codec_stage_ms(const qtts_dev_t *dev, float *ms);
 
 /* Streaming codec decode, exact and incremental (every codec op is causal:
  * conv histories, transposed-conv tails and the window-72 transformer K/V are

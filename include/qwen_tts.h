@@ -15,7 +15,8 @@
  *                        NULL and *out_samples = 0 on error
  *   qwen_tts_write_wav   0 / -1
  *
- * MI355X additions (not in the c/ reference): qwen_tts_set_device,
+ * MI355X additions (not in the c/ reference): qwen_tts_load_on (device
+ * choice per ctx; qwen_tts_load takes $QWEN_TTS_HIP_DEVICE or 0),
  * qwen_tts_generate_batch, qwen_tts_last_codes, streaming, text input, and
  * the Python reference's voice clone (codes / x-vector or reference audio).
  */
@@ -203,18 +204,21 @@ float *qwen_tts_codec_decode(qwen_tts_ctx_t *ctx, const int *codes, int time_ste
 int qwen_tts_talker_hidden(qwen_tts_ctx_t *ctx, float *out);
 
 /* ---- MI355X additions ---- */
-/* HIP device used by the next qwen_tts_load (default: $QWEN_TTS_HIP_DEVICE or 0) */
-void qwen_tts_set_device(int device);
+/* qwen_tts_load on HIP device `device` (< 0: $QWEN_TTS_HIP_DEVICE or 0, which
+ * is what qwen_tts_load uses).  No process-global state: one ctx per device
+ * and host thread, each owning its device model, streams and graphs. */
+qwen_tts_ctx_t *qwen_tts_load_on(const char *model_dir, int device);
 /* nb utterances in lock-step frames on this ctx's GPU (weights read once per
  * frame for all of them).  out_audio[i] malloc'd (caller frees), out_samples[i]
  * set; returns 0 when every utterance produced audio. */
 int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                             const char *const *languages, float **out_audio, int *out_samples);
 /* Voice clone (no c/ counterpart: the Python reference's generate_voice_clone,
- * qwen3_tts_model.py:506-630, modeling_qwen3_tts.py:1967-2232).  The
- * reference-audio encoders are not part of this library: the caller passes
- * the 12 Hz codes of the reference audio (ref_codes [n_ref_frames][16]) and/or
- * the speaker encoder's x-vector (spk_embed [talker hidden]).
+ * qwen3_tts_model.py:506-630, modeling_qwen3_tts.py:1967-2232) from the 12 Hz
+ * codes of the reference audio (ref_codes [n_ref_frames][16]) and/or the
+ * speaker encoder's x-vector (spk_embed [talker hidden]); to start from the
+ * reference AUDIO, use qwen_tts_generate_voice_clone_audio[_batch] below, which
+ * run the encoders on the device first.
  *   ICL mode  : ref_codes + ref_text (ids CSV of
  *               "<|im_start|>assistant\n{ref}<|im_end|>\n"), spk_embed optional;
  *               the audio is decoded from reference ++ generated codes and the

@@ -567,11 +567,14 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
 
 // Sub-talker attention + O projection by kv head, rows b < nrows (grid z):
 // part[(kvh * nrows + b) * R + row]; 1 = not covered.
-int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st) {
+bool qtts_attn_o_covers(const AttnArgs &a, const bf16_t *Wo) {
     const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
-    if (!(a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.S <= 16 && a.nrows >= 1 &&
-          ((uintptr_t)Wo & 15) == 0 && (a.NH * a.HD) % 8 == 0))
-        return 1;
+    return a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.S <= 16 && a.nrows >= 1 &&
+           ((uintptr_t)Wo & 15) == 0 && (a.NH * a.HD) % 8 == 0;
+}
+
+int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st) {
+    if (!qtts_attn_o_covers(a, Wo)) return 1;
     const int W2 = 2 * a.HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
     const dim3 grid((R + RPW - 1) / RPW, a.KV, a.nrows);
     switch (a.HD) {

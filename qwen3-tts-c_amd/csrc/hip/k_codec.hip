@@ -869,6 +869,8 @@ void codec_free_state(CodecModel *m) {
 }
 
 void codec_destroy(CodecModel *m) {
+    for (hipEvent_t &e : m->tev)
+        if (e) { hipEventDestroy(e); e = nullptr; }
     codec_stream_free(m);
     codec_free_state(m);
     for (auto &kv : m->w) hipFree(kv.second);
@@ -1216,17 +1218,26 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
     const int lat = d.clat, vq = d.ccbdim / 2, half = lat / 2;
     float *A = m->bufA, *B = m->bufB, *Cb = m->bufC, *D = m->bufD;
 #define DCK(x) do { if ((x) != 0) { fprintf(stderr, "qtts codec: stage failed at %s:%d\n", __FILE__, __LINE__); return nullptr; } } while (0)
+    m->timed = false;
+    if (m->timing && !m->tev[0])
+        for (hipEvent_t &e : m->tev)
+            if (hipEventCreate(&e) != hipSuccess) { e = nullptr; m->timing = false; }
+    auto mark = [&](int i) { if (m->timing) hipEventRecord(m->tev[i], st); };
+    mark(0);
     // 1. RVQ dequantise -> A [half][T]
     hipLaunchKernelGGL(k_rvq_sum, dim3(T), dim3(vq < 64 ? 64 : (vq + 63) / 64 * 64), 0, st, codes, T, d.cq, d.ccb, vq,
                        m->cb, B, Cb);
     hipLaunchKernelGGL(k_rvq_proj, dim3((half * T + 3) / 4), dim3(256), 0, st,
                        cw(m, "decoder.quantizer.rvq_first.output_proj.weight"),
                        cw(m, "decoder.quantizer.rvq_rest.output_proj.weight"), B, Cb, vq, half, T, T, A);
+    mark(1);
     // 2. pre-conv k=3 -> B [lat][T]
     DCK(conv(m, A, d.ccbdim, T, "decoder.pre_conv.conv.weight", "decoder.pre_conv.conv.bias", lat, 3, 1, B, XE_BIAS_M,
              nullptr, nullptr, nullptr));
+    mark(2);
     // 3. transformer -> A [lat][T]
     DCK(codec_transformer(m, B, T, A));
+    mark(3);
     // 4. upsample: transposed conv + ConvNeXt, x2
     int L = T;
     float *cur = A;
@@ -1252,6 +1263,7 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
         g2.res = cur; g2.ldres = L; g2.ldc = L;
         DCK(xgm(m, g2, st));
     }
+    mark(4);
     // 5. vocoder
     float *voc = cur == A ? B : A;
     DCK(conv(m, cur, lat, L, "decoder.decoder.0.conv.weight", "decoder.decoder.0.conv.bias", d.cdec, 7, 1, voc,
@@ -1283,12 +1295,17 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
     DCK(conv(m, voc, C, L, "decoder.decoder.6.conv.weight", "decoder.decoder.6.conv.bias", 1, 7, 1, wav, XE_BIAS_M,
              cw(m, "decoder.decoder.5.alpha"), cw(m, "decoder.decoder.5.beta"), nullptr));
     hipLaunchKernelGGL(k_clamp, dim3((L + 255) / 256), dim3(256), 0, st, wav, L);
+    mark(5);
     float *host = (float *)malloc((size_t)L * sizeof(float));
     if (!host) return nullptr;
     if (hipMemcpyAsync(host, wav, (size_t)L * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {
         free(host);
         return nullptr;
+    }
+    if (m->timing) {
+        for (int i = 0; i < 5; ++i) hipEventElapsedTime(&m->stage_ms[i], m->tev[i], m->tev[i + 1]);
+        m->timed = true;
     }
     if (out_samples) *out_samples = L;
     return host;

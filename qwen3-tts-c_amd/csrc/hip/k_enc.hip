@@ -859,14 +859,29 @@ static int finalize_mimi(EncModel *m) {
     return (m->cbk = up_f32(m, cb)) ? 0 : -1;
 }
 
-int enc_finalize(EncModel *m) {
-    if (!m->got_spk && !m->got_mimi) return 0;
-    if (!m->have_dims) {
-        fprintf(stderr, "Error: encoder tensors without an encoder config\n");
-        return -1;
+// Never fatal: a model whose encoders do not fit still decodes (custom voice,
+// voice clone from given codes / x-vectors); the failing encoder stays off
+// (spk_ready / mimi_ready false) and its entry points refuse with a message.
+int enc_finalize(EncModel *m, int talker_hidden) {
+    if ((m->got_spk || m->got_mimi) && !m->have_dims) {
+        fprintf(stderr, "Warning: encoder tensors without an encoder config: voice-clone encoders disabled\n");
+    } else {
+        if (m->got_spk) {
+            // the x-vector takes the place of a talker codec-embedding row
+            // (modeling_qwen3_tts.py:2104-2125): its width must be the talker's
+            if (m->d.enc_dim != talker_hidden)
+                fprintf(stderr, "Warning: speaker encoder enc_dim %d != talker hidden %d: speaker encoder disabled\n",
+                        m->d.enc_dim, talker_hidden);
+            else if (finalize_speaker(m) == 0)
+                m->spk_ready = true;
+            else
+                fprintf(stderr, "Warning: speaker encoder weights rejected: speaker encoder disabled\n");
+        }
+        if (m->got_mimi) {
+            if (finalize_mimi(m) == 0) m->mimi_ready = true;
+            else fprintf(stderr, "Warning: 12 Hz encoder weights rejected: reference-audio encoding disabled\n");
+        }
     }
-    if (m->got_spk) { ECK(finalize_speaker(m)); m->spk_ready = true; }
-    if (m->got_mimi) { ECK(finalize_mimi(m)); m->mimi_ready = true; }
     m->host.clear();
     m->shape.clear();
     return 0;

@@ -57,6 +57,12 @@ struct CodecModel {
     float *xg_part = nullptr;                  // split-K workspace of the codec GEMMs
     size_t xg_part_elems = 0;
     CodecStream cs;
+    // per-stage timing of codec_decode (the reference's -v -v "Codec stages
+    // (ms)" line, c/qwen_tts_codec.c:743-746): events around rvq / preconv /
+    // transformer / upsample / vocoder when `timing` is on
+    bool timing = false, timed = false;
+    hipEvent_t tev[6] = {};
+    float stage_ms[5] = {};
 };
 
 void codec_init(CodecModel *m, const qtts_dims_t *d, hipStream_t st);

@@ -61,7 +61,7 @@ int enc_set_dims(EncModel *m, const qtts_enc_dims_t *d);
 // returns 1 when the tensor belongs to an encoder (taken), 0 when not, <0 on error
 int enc_put_tensor(EncModel *m, const std::string &name, const void *host, int dtype, const int64_t *shape, int ndim,
                    size_t n);
-int enc_finalize(EncModel *m);
+int enc_finalize(EncModel *m, int talker_hidden);
 void enc_destroy(EncModel *m);
 size_t enc_weight_bytes(const EncModel *m);
 // x-vectors of nb waveforms (24 kHz, host) -> out[nb][enc_dim] (host); mel_out

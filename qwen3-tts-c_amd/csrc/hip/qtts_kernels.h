@@ -105,6 +105,8 @@ int qtts_attn_keys_per_split(int HD);
 // sub-talker attention + O projection split by kv head: part [KV][nrows][R]
 // (GQA 2, <= 16 keys); 1 = not covered
 int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st);
+// true when qtts_attn_o takes these arguments (it returns 1 otherwise)
+bool qtts_attn_o_covers(const AttnArgs &a, const bf16_t *Wo);
 
 // Name of the kernel instantiation the last launcher on this thread chose
 // (diagnostics: per-kernel profile rows match rocprofv3's kernel names).

@@ -144,6 +144,8 @@ struct qtts_dev {
     int *push_codes = nullptr;
     size_t push_cap = 0;
     bool prime_pending = false;   // a qtts_dev_codec_stream_prime push runs on cst (cev marks its end)
+    float *pwav = nullptr;        // the prime's discarded audio (never the codec_async output cwav)
+    size_t pwav_cap = 0;
     // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
@@ -372,6 +374,7 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
     enc_destroy(&dv->enc);
     if (dv->cst) hipStreamSynchronize(dv->cst);
     if (dv->cwav) hipFree(dv->cwav);
+    if (dv->pwav) hipFree(dv->pwav);
     if (dv->push_codes) hipFree(dv->push_codes);
     if (dv->cev) hipEventDestroy(dv->cev);
     if (dv->cst) hipStreamDestroy(dv->cst);
@@ -445,7 +448,12 @@ extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
     if (dv->st_proj && ptab_on) CKI(build_proj_tables(dv));
     if (ptab_on) CKI(build_qkv0_table(dv));
     CKI(codec_finalize(&dv->codec));
-    return enc_finalize(&dv->enc);
+    // the streaming codec's state for up to 4096 frames, allocated now so the
+    // first streaming request of a process does not pay for it (its buffers
+    // are reused by every later stream of <= 4096 frames; longer ones re-grow)
+    if (codec_stream_begin(&dv->codec, 4096) != 0)
+        fprintf(stderr, "qtts: streaming codec state not pre-allocated (allocated on first use)\n");
+    return enc_finalize(&dv->enc, d.H);
 }
 
 // ----------------------------------------------------------------- voice-clone encoders
@@ -709,6 +717,7 @@ static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float
 static int build_qkv0_table(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     if (d.G < 2 || d.Ls < 1) return 0;
+    if (d.NHs != 2 * d.KVs) return 0;   // read only by the fused attention + O kernel (qtts_attn_o_covers)
     const int QKV = dv->QKVs();
     const size_t rows = (size_t)d.V + (size_t)(d.G - 2) * d.Vs;
     const int nid = d.V > d.Vs ? d.V : d.Vs;
@@ -895,10 +904,6 @@ static int subtalker(qtts_dev *dv) {
             const bool kv_only = g == 0 && l == d.Ls - 1;
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
-            // batch 1, pass g >= 1, layer 0: q|k|v come from the load-time table
-            // by the input id (no GEMV); the gate|up GEMV reads the residual
-            // from the input table row itself
-            const bool tab0 = l == 0 && g >= 1 && nb == 1 && dv->attn_o && dv->qkv0_tab && (!proj || ptab);
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
             AttnArgs t;
@@ -908,6 +913,14 @@ static int subtalker(qtts_dev *dv) {
             t.pos = nullptr; t.pos_const = g; t.NH = d.NHs; t.KV = d.KVs; t.HD = d.HDs; t.out = dv->att_s;
             t.ld_out = AD; t.nrows = nb; t.skip = dv->stopped;
             t.cnt = dv->att_cnt;
+            // batch 1, pass g >= 1, layer 0: q|k|v come from the load-time table
+            // by the input id (no GEMV); the gate|up GEMV reads the residual
+            // from the input table row itself.  Only where the fused attention +
+            // O kernel runs: it alone reads the table, and the skipped GEMV is
+            // also what copies the residual (the generic paths would read a
+            // stale qkv_s and an unwritten x_st)
+            const bool tab0 = l == 0 && g >= 1 && nb == 1 && dv->attn_o && dv->qkv0_tab && (!proj || ptab) &&
+                              qtts_attn_o_covers(t, ly.wo);
             GemvArgs o = gv(ly.wo, d.Hs, AD, dv->att_s, AD, xa, d.Hs, nb, EPI_RESID);
             o.nt = 0;
             bool fused_o = false, opend = false;
@@ -1027,6 +1040,7 @@ static bool same_params(const qtts_gen_params_t &a, const qtts_gen_params_t &b) 
 extern "C" int qtts_dev_begin(qtts_dev_t *dv, int nb, int max_frames, int max_prefill, const qtts_gen_params_t *p) {
     if (!dv || nb < 1 || max_frames < 1) return -1;
     hipSetDevice(dv->device);
+    CKI(join_prime(dv));   // a prime left pending by a run that pushed no frames
     if (max_prefill < 16) max_prefill = 16;
     const bool realloc_ = nb != dv->nb || max_frames > dv->max_frames || max_prefill > dv->p_cap;
     if (realloc_) {
@@ -1226,7 +1240,20 @@ extern "C" float *qtts_dev_codec_slot(qtts_dev_t *dv, int b, int T, int *out_sam
     if (out_samples) *out_samples = 0;
     if (!dv || b < 0 || b >= dv->nb || T < 1) return nullptr;
     hipSetDevice(dv->device);
+    if (join_prime(dv)) return nullptr;   // the prime shares the codec scratch and split-K workspace
     return codec_decode(&dv->codec, dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G, T, out_samples);
+}
+
+extern "C" int qtts_dev_codec_timing(qtts_dev_t *dv, int on) {
+    if (!dv) return -1;
+    dv->codec.timing = on != 0;
+    return 0;
+}
+
+extern "C" int qtts_dev_codec_stage_ms(const qtts_dev_t *dv, float *ms) {
+    if (!dv || !ms || !dv->codec.timed) return -1;
+    for (int i = 0; i < 5; ++i) ms[i] = dv->codec.stage_ms[i];
+    return 0;
 }
 
 // ----------------------------------------------------------------- streaming codec (exact, incremental)
@@ -1282,19 +1309,19 @@ extern "C" int qtts_dev_codec_stream_prime(qtts_dev_t *dv, const int *codes, int
     CKI(ensure_cst(dv));
     CKI(ensure_push_codes(dv, (size_t)T * dv->d.cq));
     const size_t need = (size_t)T * 1920;
-    if (need > dv->cwav_cap) {
+    if (need > dv->pwav_cap) {
         CK(hipStreamSynchronize(dv->cst));
-        if (dv->cwav) CK(hipFree(dv->cwav));
-        dv->cwav = nullptr;
-        dv->cwav_cap = 0;
-        CK(hipMalloc(&dv->cwav, need * 4));
-        dv->cwav_cap = need;
+        if (dv->pwav) CK(hipFree(dv->pwav));
+        dv->pwav = nullptr;
+        dv->pwav_cap = 0;
+        CK(hipMalloc(&dv->pwav, need * 4));
+        dv->pwav_cap = need;
     }
     CK(hipEventRecord(dv->cev, dv->st));          // after the begin's resets on st
     CK(hipStreamWaitEvent(dv->cst, dv->cev, 0));
     CK(hipMemcpyAsync(dv->push_codes, codes, (size_t)T * dv->d.cq * 4, hipMemcpyHostToDevice, dv->cst));
     dv->codec.st = dv->cst;
-    const int n = codec_stream_push_to(&dv->codec, dv->push_codes, dv->d.cq, T, dv->cwav, false);
+    const int n = codec_stream_push_to(&dv->codec, dv->push_codes, dv->d.cq, T, dv->pwav, false);
     dv->codec.st = dv->st;
     if (n < 0) return -1;
     CK(hipEventRecord(dv->cev, dv->cst));
@@ -1447,6 +1474,7 @@ extern "C" float *qtts_dev_codec_decode_host(qtts_dev_t *dv, const int *codes, i
     if (out_samples) *out_samples = 0;
     if (!dv || T < 1) return nullptr;
     hipSetDevice(dv->device);
+    if (join_prime(dv)) return nullptr;
     int *dc = nullptr;
     if (hipMalloc(&dc, (size_t)T * dv->d.cq * 4) != hipSuccess) return nullptr;
     float *r = nullptr;

@@ -297,9 +297,8 @@ int main(int argc, char **argv) {
         if (verbose >= 1) fprintf(stderr, "x-vector: %d floats\n", n);
     }
     qwen_tts_verbose = verbose;
-    if (device >= 0) qwen_tts_set_device(device);
     if (verbose >= 1) fprintf(stderr, "Loading model from %s...\n", dir);
-    qwen_tts_ctx_t *ctx = qwen_tts_load(dir);
+    qwen_tts_ctx_t *ctx = qwen_tts_load_on(dir, device);
     if (!ctx) {
         fprintf(stderr, "Error: failed to load model\n");
         free(file_ids);

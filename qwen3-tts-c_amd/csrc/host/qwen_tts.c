@@ -28,7 +28,6 @@
 #include "qjson.h"
 
 int qwen_tts_verbose = 0;
-static int g_device = -1;
 
 static double now_ms(void) {
     struct timespec ts;
@@ -36,7 +35,6 @@ static double now_ms(void) {
     return (double)ts.tv_sec * 1000.0 + (double)ts.tv_nsec / 1e6;
 }
 
-void qwen_tts_set_device(int device) { g_device = device; }
 
 /* ------------------------------------------------------------------ config */
 static void read_map(const qj_t *root, const char *path, int *n, char ***names, int **ids) {
@@ -252,8 +250,8 @@ static int upload_dir(qtts_dev_t *dev, const char *dir) {
 
 /* Voice-clone encoder config: config.json
  * `speaker_encoder_config` (defaults of Qwen3TTSSpeakerEncoderConfig,
- * configuration_qwen3_tts.py:47-57, enc_dim = the talker hidden the x-vector
- * takes the place of) and speech_tokenizer/config.json `encoder_config`
+ * configuration_qwen3_tts.py:47-57: enc_dim 1024; it must equal the talker
+ * hidden the x-vector takes the place of, else the speaker encoder stays off) and speech_tokenizer/config.json `encoder_config`
  * (transformers MimiConfig defaults).  Returns 1 when either section exists. */
 static int load_enc_config(const qwen_tts_ctx_t *ctx, qtts_enc_dims_t *e) {
     memset(e, 0, sizeof *e);
@@ -267,7 +265,7 @@ static int load_enc_config(const qwen_tts_ctx_t *ctx, qtts_enc_dims_t *e) {
     if (js && qj_path(js, "speaker_encoder_config")) have = 1;
 #define SI(f, k, d) e->f = qj_int(js, "speaker_encoder_config." k, d)
     SI(mel_dim, "mel_dim", 128);
-    SI(enc_dim, "enc_dim", ctx->config.talker_hidden);
+    SI(enc_dim, "enc_dim", 1024);   /* Qwen3TTSSpeakerEncoderConfig default */
     SI(att_ch, "enc_attention_channels", 128);
     SI(res2net_scale, "enc_res2net_scale", 8);
     SI(se_ch, "enc_se_channels", 128);
@@ -337,7 +335,9 @@ static void dims_of(const qwen_tts_config_t *c, qtts_dims_t *d) {
     d->pad_id = c->codec_pad_id; d->bos_id = c->codec_bos_id; d->eos_id = c->codec_eos_id;
 }
 
-qwen_tts_ctx_t *qwen_tts_load(const char *model_dir) {
+qwen_tts_ctx_t *qwen_tts_load(const char *model_dir) { return qwen_tts_load_on(model_dir, -1); }
+
+qwen_tts_ctx_t *qwen_tts_load_on(const char *model_dir, int device) {
     double t0 = now_ms();
     qwen_tts_ctx_t *ctx = (qwen_tts_ctx_t *)calloc(1, sizeof(qwen_tts_ctx_t));
     if (!ctx) return NULL;
@@ -353,7 +353,7 @@ qwen_tts_ctx_t *qwen_tts_load(const char *model_dir) {
     ctx->fixed_codec_tokens = 0;
     ctx->sample_seed = 42;
     if (load_config(ctx) != 0) { qwen_tts_free(ctx); return NULL; }
-    int dev_id = g_device;
+    int dev_id = device;
     if (dev_id < 0) {
         const char *e = getenv("QWEN_TTS_HIP_DEVICE");
         dev_id = e ? atoi(e) : 0;
@@ -370,7 +370,8 @@ qwen_tts_ctx_t *qwen_tts_load(const char *model_dir) {
     if (!dev) { qwen_tts_free(ctx); return NULL; }
     ctx->hip = dev;
     qtts_enc_dims_t ed;
-    if (load_enc_config(ctx, &ed) && qtts_dev_enc_config(dev, &ed) != 0) { qwen_tts_free(ctx); return NULL; }
+    if (load_enc_config(ctx, &ed) && qtts_dev_enc_config(dev, &ed) != 0)   /* not fatal: encoders stay off */
+        fprintf(stderr, "Warning: unsupported voice-clone encoder config: encoders disabled\n");
     char cdir[1100];
     snprintf(cdir, sizeof cdir, "%s/speech_tokenizer", model_dir);
     if (upload_dir(dev, model_dir) != 0 || upload_dir(dev, cdir) != 0 || qtts_dev_finalize(dev) != 0) {
@@ -606,6 +607,24 @@ static void lookup(const qwen_tts_ctx_t *ctx, const char *speaker, const char *l
     }
 }
 
+/* the reference codec's stderr lines around one full decode
+ * (c/qwen_tts_codec.c:598-599 at -v, 740-746 at -v / -v -v) */
+static void codec_log_begin(qwen_tts_ctx_t *ctx, int T) {
+    qtts_dev_codec_timing((qtts_dev_t *)ctx->hip, qwen_tts_verbose >= 2);
+    if (qwen_tts_verbose >= 1)
+        fprintf(stderr, "Codec decode: %d timesteps, %d quantizers\n", T, ctx->config.codec_num_quantizers);
+}
+
+static void codec_log_end(qwen_tts_ctx_t *ctx, int samples) {
+    if (qwen_tts_verbose < 1 || samples <= 0) return;
+    fprintf(stderr, "Codec decode complete: %d samples (%.2f seconds)\n", samples,
+            (float)samples / QWEN_TTS_SAMPLE_RATE);
+    float ms[5];
+    if (qwen_tts_verbose >= 2 && qtts_dev_codec_stage_ms((qtts_dev_t *)ctx->hip, ms) == 0)
+        fprintf(stderr, "Codec stages (ms): rvq=%.1f preconv=%.1f transformer=%.1f upsample=%.1f vocoder=%.1f\n",
+                ms[0], ms[1], ms[2], ms[3], ms[4]);
+}
+
 static void params_of(const qwen_tts_ctx_t *ctx, qtts_gen_params_t *p) {
     p->temperature = ctx->temperature; p->top_p = ctx->top_p; p->repetition_penalty = ctx->repetition_penalty;
     p->top_k = ctx->top_k; p->st_temperature = ctx->subtalker_temperature; p->st_top_p = ctx->subtalker_top_p;
@@ -771,7 +790,9 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
                 int *all = (int *)malloc((size_t)tot * G * sizeof(int)), nw = 0;
                 if (all && qtts_dev_get_codes(dev, b, all + (size_t)vc->n_ref * G, ngen[b]) == ngen[b]) {
                     memcpy(all, vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
+                    codec_log_begin(ctx, tot);
                     float *w = qtts_dev_codec_decode_host(dev, all, tot, &nw);
+                    codec_log_end(ctx, w ? nw : 0);
                     const int cut = (int)((double)vc->n_ref / (double)tot * (double)nw);
                     if (w && nw > cut) {
                         memmove(w, w + cut, (size_t)(nw - cut) * sizeof(float));
@@ -785,7 +806,9 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
                 if (!audio[b]) rc = -1;
                 continue;
             }
+            codec_log_begin(ctx, ngen[b]);
             audio[b] = qtts_dev_codec_slot(dev, b, ngen[b], &samples[b]);
+            codec_log_end(ctx, audio[b] ? samples[b] : 0);
             if (!audio[b] || samples[b] <= 0) rc = -1;
         }
         ctx->perf_codec_ms = now_ms() - t_codec;
@@ -1151,7 +1174,10 @@ float *qwen_tts_codec_decode(qwen_tts_ctx_t *ctx, const int *codes, int time_ste
         if (out_samples) *out_samples = 0;
         return NULL;
     }
-    return qtts_dev_codec_decode_host((qtts_dev_t *)ctx->hip, codes, time_steps, out_samples);
+    codec_log_begin(ctx, time_steps);
+    float *w = qtts_dev_codec_decode_host((qtts_dev_t *)ctx->hip, codes, time_steps, out_samples);
+    codec_log_end(ctx, w ? *out_samples : 0);
+    return w;
 }
 
 int qwen_tts_talker_hidden(qwen_tts_ctx_t *ctx, float *out) {

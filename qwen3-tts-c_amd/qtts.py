@@ -66,13 +66,13 @@ class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
 EXPORTS = [
     "qwen_tts_load", "qwen_tts_free", "qwen_tts_set_progress_callback", "qwen_tts_generate", "qwen_tts_write_wav",
     "qwen_tts_talker_prefill", "qwen_tts_talker_forward", "qwen_tts_subtalker_generate", "qwen_tts_codec_decode",
-    "qwen_tts_talker_hidden", "qwen_tts_set_device", "qwen_tts_generate_batch", "qwen_tts_last_codes",
+    "qwen_tts_talker_hidden", "qwen_tts_load_on", "qwen_tts_generate_batch", "qwen_tts_last_codes",
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
     "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
     "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream", "qwen_tts_tokenize",
     "qwen_tts_text_prompt", "qwen_tts_speaker_embedding", "qwen_tts_encode_audio",
     "qwen_tts_generate_voice_clone_audio", "qwen_tts_generate_voice_clone_audio_batch",
-    "qwen_tts_generate_voice_clone_audio_stream",
+    "qwen_tts_generate_voice_clone_audio_stream", "qtts_dev_codec_timing", "qtts_dev_codec_stage_ms",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -133,7 +133,8 @@ def lib():
     L.qwen_tts_codec_decode.restype = C.c_void_p
     L.qwen_tts_codec_decode.argtypes = [C.POINTER(Ctx), _ip, C.c_int, _ip]
     L.qwen_tts_talker_hidden.argtypes = [C.POINTER(Ctx), _fp]
-    L.qwen_tts_set_device.argtypes = [C.c_int]
+    L.qwen_tts_load_on.restype = C.POINTER(Ctx)
+    L.qwen_tts_load_on.argtypes = [C.c_char_p, C.c_int]
     L.qwen_tts_set_progress_callback.argtypes = [C.POINTER(Ctx), PROGRESS_CB, C.c_void_p]
     L.qwen_tts_write_wav.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
     L.qwen_tts_abi_sizeof_ctx.restype = C.c_size_t
@@ -214,8 +215,7 @@ class QwenTTS:
 
     def __init__(self, model_dir, device=0):
         L = lib()
-        L.qwen_tts_set_device(int(device))
-        self.ctx = L.qwen_tts_load(model_dir.encode())
+        self.ctx = L.qwen_tts_load_on(model_dir.encode(), int(device))
         if not self.ctx:
             raise RuntimeError(f"qwen_tts_load({model_dir}) failed")
         self.c = self.ctx.contents

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "qwen3-tts-c_amd")
 GOLDEN = os.path.join(HERE, "golden")
-for p in (HERE, os.path.join(ROOT, "tools"), PKG, ROOT, os.path.join(ROOT, "oracle")):
+for p in (HERE, os.path.join(ROOT, "tools"), PKG, ROOT, os.path.join(ROOT, "oracle"), GOLDEN):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -229,7 +229,10 @@ def cli_fixture(md_eos):
         pcm = np.frombuffer(open(wav, "rb").read()[44:], np.int16).copy()
     stop = re.search(r"Stop: (eos|max_tokens) at step (\d+)", r.stderr)
     gen = re.search(r"Generated (\d+) codec tokens", r.stderr)
-    meta = {"args": args, "stop_line": stop.group(0), "generated": int(gen.group(1))}
+    # the codec's -v lines (c/qwen_tts_codec.c:598-599, 740-742)
+    codec = [ln for ln in r.stderr.splitlines() if ln.startswith("Codec decode:") and "timesteps" in ln
+             or ln.startswith("Codec decode complete:")]
+    meta = {"args": args, "stop_line": stop.group(0), "generated": int(gen.group(1)), "codec_lines": codec}
     return {"cli_eos_pcm": pcm}, meta
 
 

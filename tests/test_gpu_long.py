@@ -1,0 +1,121 @@
+"""Long-context parity on the GPU against the REFERENCE's own outputs.
+
+Fixtures (tests/golden/make_golden_long.py, from the reference c/ build):
+
+* `long_hd128.npz` -- the `hd128` synthetic model (the talker's real attention
+  shape NH 16 / KV 8 / HD 128, 2 narrow layers): a 640-frame default-sampling
+  decode.  `k_attn_dec` takes 64-key splits at HD 128, so the talker positions
+  (38 .. 678) run through the 1-split path, the 2-8-split merge and the
+  > 8-split serial merge (k_attn.hip); the codes must be bit-exact all the
+  way.  A 600-row prefill (> 512 rows) and 4 decode steps over 600+ keys.
+* `long_17b.npz` -- the benchmark workload itself (bench.py): synthetic 1.7B,
+  P128 prompt, fixed 128 frames, default sampling, seed 42.
+
+Bars: codes bit-exact (the first divergent frame / group is reported if not);
+waveform MSE < 1e-4 and max |d| < 1e-3 (north star); hidden / logits
+allclose(1e-4, 1e-4) as the tiny stage goldens.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, model_dir
+from make_golden_long import prefill_inputs
+from oracle_py import DEFAULT, Oracle
+
+import qtts
+
+pytestmark = [pytest.mark.gpu]
+
+
+def _man():
+    return json.load(open(os.path.join(GOLDEN, "long_manifest.json")))
+
+
+def _codes_equal(got, want, what):
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    bad = np.argwhere(got != want)
+    if len(bad):
+        f, g = bad[0]
+        raise AssertionError(f"{what}: first divergent code at frame {f} group {g} "
+                             f"(got {got[f, g]}, reference {want[f, g]}; {len(bad)} codes differ)")
+
+
+def _audio_close(a, ref, what, mse_bar=1e-4, max_bar=1e-3):
+    assert a is not None and a.shape == ref.shape, (what, None if a is None else a.shape, ref.shape)
+    d = a.astype(np.float64) - ref
+    mse, mx = float(np.mean(d * d)), float(np.abs(d).max())
+    assert mse < mse_bar and mx < max_bar, (what, mse, mx)
+
+
+@pytest.fixture(scope="module")
+def hd128(gpu):
+    md = model_dir("hd128")
+    m = qtts.QwenTTS(md)
+    yield m, md, np.load(os.path.join(GOLDEN, "long_hd128.npz")), _man()["hd128"]
+    m.close()
+
+
+def test_hd128_640_frames_vs_reference(hd128):
+    """640 frames: every split-merge path of the talker's decode attention,
+    codes bit-exact against the reference, waveform against its samples."""
+    m, md, g, man = hd128
+    m.set_params(max_tokens=4096, fixed=man["frames"], seed=man["seed"], **DEFAULT)
+    a = m.generate(g["prompt_ids"], "aiden", "english")
+    _codes_equal(m.last_codes(), g["decode_codes"], "hd128 640-frame decode")
+    assert a.shape[0] == int(g["decode_audio_len"])
+    _audio_close(a[::man["audio_stride"]], g["decode_audio_sub"], "every 16th sample")
+    _audio_close(a[:1920], g["decode_audio_first"], "first frame")
+    _audio_close(a[-1920:], g["decode_audio_last"], "last frame")
+    # the whole waveform against the oracle port's decode of the same codes
+    o = Oracle(md)
+    try:
+        _audio_close(a, o.codec_decode(g["decode_codes"]), "full waveform vs oracle")
+    finally:
+        o.close()
+
+
+def test_hd128_640_frames_lock_step_batch(hd128):
+    """The same utterance as slot 0 and 2 of a lock-step batch of 3 (batch
+    attention rows through the same split merges): bit-equal to the reference."""
+    m, md, g, man = hd128
+    other = g["prompt_ids"].copy()
+    other[5] += 17
+    m.set_params(max_tokens=4096, fixed=man["frames"], seed=man["seed"], **DEFAULT)
+    rc, audio = m.generate_batch([g["prompt_ids"], other, g["prompt_ids"]], ["aiden", "vivian", "aiden"],
+                                 ["english"] * 3)
+    assert rc == 0
+    np.testing.assert_array_equal(audio[0], audio[2])
+    _audio_close(audio[0][::man["audio_stride"]], g["decode_audio_sub"], "batch slot 0, every 16th sample")
+    _audio_close(audio[0][-1920:], g["decode_audio_last"], "batch slot 0, last frame")
+
+
+def test_hd128_600_row_prefill_and_steps_vs_reference(hd128):
+    """A 600-row prefill (the matrix-core prefill GEMM, prefill attention over
+    600 rows), then decode steps at positions 600-603 (10 key splits)."""
+    m, md, g, man = hd128
+    emb, steps = prefill_inputs(m.cfg.talker_hidden, man["prefill_seed"])
+    h = m.prefill(emb)
+    np.testing.assert_allclose(h, g["prefill_hidden"], atol=1e-4, rtol=1e-4)
+    for i in range(man["prefill_steps"]):
+        lg, hid = m.step(steps[i])
+        np.testing.assert_allclose(lg, g["step_logits"][i], atol=1e-4, rtol=1e-4)
+        np.testing.assert_allclose(hid, g["step_hidden"][i], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.slow
+def test_full_bench_workload_vs_reference(gpu):
+    """BASELINE's workload as bench.py runs it (1.7B, P128, fixed 128 frames,
+    default sampling, seed 42): codes bit-exact, waveform MSE < 1e-4."""
+    g = np.load(os.path.join(GOLDEN, "long_17b.npz"))
+    man = _man()["1.7b"]
+    m = qtts.QwenTTS(model_dir("1.7b"))
+    try:
+        m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
+        _codes_equal(m.last_codes(), g["codes"], "1.7B bench workload")
+        _audio_close(a, g["audio"], "1.7B bench workload waveform")
+    finally:
+        m.close()

@@ -206,6 +206,28 @@ def test_cli_eos_regression_like_reference(tiny_eos_dir):
     assert np.abs(pcm.astype(np.int32) - ref).max() <= 1
 
 
+def test_cli_codec_verbose_lines_like_reference(tiny_eos_dir):
+    """The codec's stderr lines: at -v the reference CLI's own
+    `Codec decode: N timesteps, 16 quantizers` / `Codec decode complete: S
+    samples (X seconds)` (tests/golden/manifest.json, c/qwen_tts_codec.c:598,
+    740-742); at -v -v also `Codec stages (ms): rvq=.. preconv=.. transformer=..
+    upsample=.. vocoder=..` (:743-746), timed on the device by HIP events."""
+    man = manifest()["cli_eos"]
+    ids = ",".join(str(i) for i in prompt_ids("short"))
+    stages = re.compile(r"Codec stages \(ms\): rvq=[\d.]+ preconv=[\d.]+ transformer=[\d.]+ upsample=[\d.]+ "
+                        r"vocoder=[\d.]+")
+    with tempfile.TemporaryDirectory() as d:
+        for extra, want_stages in ((["-v"], False), (["-v", "-v"], True)):
+            args = [a for a in man["args"] if a != "-v"] + extra
+            r = subprocess.run([qtts.CLI_PATH, "-d", tiny_eos_dir, "-t", ids, "-o", os.path.join(d, "o.wav")] + args,
+                               capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, r.stderr
+            lines = r.stderr.splitlines()
+            for want in man["codec_lines"]:
+                assert want in lines, (want, r.stderr)
+            assert bool(stages.search(r.stderr)) == want_stages, r.stderr
+
+
 def test_cli_persistent_benchmark_lines(tiny_dir):
     ids = ",".join(str(i) for i in prompt_ids("short"))
     with tempfile.TemporaryDirectory() as d:   # the writer goes through <path>.tmp like the reference's
@@ -322,3 +344,27 @@ def test_e2e_debug_switch_paths(tiny_dir, monkeypatch, env):
             audio_close(a, E[f"{name}_audio"])
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("heads", [(6, 2), (2, 2)])
+def test_subtalker_head_layouts_vs_oracle(gpu, heads):
+    """Sub-talker head layouts the fused attention + O kernel does not take
+    (NH != 2 KV): the layer-0 q|k|v table must not be read there (its skipped
+    GEMV is what writes the residual), so the generic attention path runs
+    with the GEMV.  Codes bit-exact and audio against the oracle."""
+    nh, kv = heads
+    md = model_dir("tiny", NHs=nh, KVs=kv)
+    ids = prompt_ids("short")
+    o = Oracle(md)
+    m = qtts.QwenTTS(md)
+    try:
+        s, l = lookup_ids(o.cfg, "aiden", "english")
+        for pp in (GREEDY, DEFAULT):
+            want, _ = o.generate_codes(ids, s, l, max_tokens=4096, fixed=6, seed=42, **pp)
+            m.set_params(max_tokens=4096, fixed=6, seed=42, **pp)
+            a = m.generate(ids, "aiden", "english")
+            np.testing.assert_array_equal(m.last_codes(), want)
+            audio_close(a, o.codec_decode(want))
+    finally:
+        m.close()
+        o.close()

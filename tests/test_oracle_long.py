@@ -1,0 +1,51 @@
+"""The oracle port against the long-context reference fixtures (CPU only).
+
+tests/golden/long_hd128.npz comes from the reference c/ build
+(tests/golden/make_golden_long.py) on the `hd128` synthetic model: the
+talker's real attention shape (NH 16 / KV 8 / HD 128) decoding 640 frames
+(positions up to ~680) and a 600-row prefill followed by 4 decode steps.  The
+oracle must reproduce it bit-exactly before it checks the GPU at those
+lengths (tests/test_gpu_long.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, model_dir
+from make_golden_long import model_hashes, prefill_inputs
+from oracle_py import DEFAULT, Oracle
+from qtts_io import lookup_ids
+
+
+@pytest.fixture(scope="module")
+def hd128():
+    md = model_dir("hd128")
+    man = json.load(open(os.path.join(GOLDEN, "long_manifest.json")))
+    assert model_hashes(md) == man["models"]["hd128"], "synthetic hd128 model no longer reproduces"
+    o = Oracle(md)
+    yield o, np.load(os.path.join(GOLDEN, "long_hd128.npz")), man["hd128"]
+    o.close()
+
+
+def test_oracle_long_decode_bit_exact(hd128):
+    o, g, m = hd128
+    s, l = lookup_ids(o.cfg, "aiden", "english")
+    codes, _ = o.generate_codes(g["prompt_ids"], s, l, max_tokens=4096, fixed=m["frames"], seed=m["seed"],
+                                **DEFAULT)
+    np.testing.assert_array_equal(codes, g["decode_codes"])
+    a = o.codec_decode(codes)
+    assert a.shape[0] == int(g["decode_audio_len"])
+    np.testing.assert_array_equal(a[::m["audio_stride"]], g["decode_audio_sub"])
+    np.testing.assert_array_equal(a[-1920:], g["decode_audio_last"])
+
+
+def test_oracle_long_prefill_and_steps_bit_exact(hd128):
+    o, g, m = hd128
+    emb, steps = prefill_inputs(o.cfg["H"], m["prefill_seed"])
+    np.testing.assert_array_equal(o.prefill(emb), g["prefill_hidden"])
+    for i in range(m["prefill_steps"]):
+        lg, hid = o.step(steps[i])
+        np.testing.assert_array_equal(lg, g["step_logits"][i])
+        np.testing.assert_array_equal(hid, g["step_hidden"][i])

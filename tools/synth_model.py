@@ -71,6 +71,18 @@ PRESETS = {
         c_inter=128, c_window=72, c_dec=64, c_cb=2048, c_q=16,
         eos_gain=1.0, enc="tiny",
     ),
+    # the 0.6B talker's attention shape (NH 16 / KV 8 / HD 128, H 1024) in 2
+    # narrow layers, tiny sub-talker and codec: cheap enough for the CPU
+    # checkers to decode 600+ frames, so the talker's split-K attention runs
+    # through 1, 2-8 and > 8 key splits (64 keys per split at HD 128)
+    "hd128": dict(
+        H=1024, I=1024, L=2, NH=16, KV=8, HD=128, TH=64, TV=151936, V=3072, G=16,
+        Hs=64, Is=128, Ls=2, NHs=4, KVs=2, HDs=16, Vs=2048,
+        rope_theta=1000000.0, mrope=[24, 20, 20],
+        c_hidden=64, c_latent=128, c_cbdim=64, c_layers=2, c_heads=4, c_kv=4,
+        c_inter=128, c_window=72, c_dec=64, c_cb=2048, c_q=16,
+        eos_gain=1.0,
+    ),
     "0.6b": dict(
         H=1024, I=3072, L=28, NH=16, KV=8, HD=128, TH=2048, TV=151936, V=3072, G=16,
         Hs=1024, Is=3072, Ls=5, NHs=16, KVs=8, HDs=128, Vs=2048,
