@@ -484,8 +484,9 @@ int qtts_gemv(const GemvArgs &in, hipStream_t st) {
 #undef QTTS_G1
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (a.nb >= 2) {   // lock-step batch: the matrix-core kernel (k_gemvm.hip) where it covers the shape
-        const int rc = qtts_gemvm(a, st);
+    if (a.nb >= 2) {   // lock-step batch: the matrix-core kernels (k_gemvb.hip, k_gemvm.hip) where they cover the shape
+        int rc = qtts_gemvb(a, st);
+        if (rc == 1) rc = qtts_gemvm(a, st);
         if (rc != 1) return rc;
     }
     if (a.ypart || (a.xadd && a.nb >= 2)) {

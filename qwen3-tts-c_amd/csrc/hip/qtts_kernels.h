@@ -69,6 +69,8 @@ int qtts_gemv(const GemvArgs &a, hipStream_t st);
 int qtts_gemvw(const GemvArgs &a, hipStream_t st);
 // lock-step batch (2..16 rows) on the bf16 matrix cores (k_gemvm.hip); 1 = not covered
 int qtts_gemvm(const GemvArgs &a, hipStream_t st);
+// the same with the x rows sliced per wave (k_gemvb.hip, tried first); 1 = not covered
+int qtts_gemvb(const GemvArgs &a, hipStream_t st);
 // multi-row (2..64) projection on the bf16 matrix cores (k_mgemm.hip); 1 = not covered
 int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st);
 

@@ -439,6 +439,14 @@ extern "C" int qtts_dev_finalize(qtts_dev_t *dv) {
         fprintf(stderr, "Error: unsupported head_dim (talker=%d subtalker=%d) or code groups %d\n", d.HD, d.HDs, d.G);
         return -1;
     }
+    // every decode GEMV's reduction width (qtts_gemv streams 64-column blocks)
+    const int widths[] = {d.H, d.I, d.NH * d.HD, d.Hs, d.Is, d.NHs * d.HDs, d.TH};
+    for (int c : widths)
+        if (c % 64) {
+            fprintf(stderr, "Error: unsupported layer width %d (hidden / intermediate / heads x head_dim must be "
+                            "multiples of 64)\n", c);
+            return -1;
+        }
     if (d.V > 4096 || d.Vs > 4096) {
         fprintf(stderr, "Error: vocab > 4096 unsupported by the device sampler\n");
         return -1;

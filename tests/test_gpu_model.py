@@ -346,7 +346,7 @@ def test_e2e_debug_switch_paths(tiny_dir, monkeypatch, env):
         m.close()
 
 
-@pytest.mark.parametrize("heads", [(6, 2), (2, 2)])
+@pytest.mark.parametrize("heads", [(8, 2), (4, 4)])
 def test_subtalker_head_layouts_vs_oracle(gpu, heads):
     """Sub-talker head layouts the fused attention + O kernel does not take
     (NH != 2 KV): the layer-0 q|k|v table must not be read there (its skipped
