@@ -284,13 +284,16 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
             hw[j] = nw[i];
         }
     }
-    constexpr int RJ = ((GPH + 1) * HD + 255) / 256;
+    // RoPE rows: HD 128 -- a lane holds elements lane and lane + 64, its own
+    // rotate-half partner, so its wave rotates in registers; else by thread
+    constexpr bool RREG = HD == 128;
+    constexpr int RJ = RREG ? 2 : ((GPH + 1) * HD + 255) / 256;
     float rc[RJ], rs[RJ];
     {
         const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
 #pragma unroll
         for (int j = 0; j < RJ; ++j) {
-            const int e = (tid + 256 * j) % HD;
+            const int e = RREG ? lane + 64 * j : (tid + 256 * j) % HD;
             rc[j] = cs[e];
             rs[j] = sn[e];
         }
@@ -327,24 +330,32 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
         for (int j = 0; j < HJ; ++j) ss += lane + 64 * j < HD ? hv[j] * hv[j] : 0.f;   // (HD < 64: lanes past HD repeat)
         ss = wave_sum(ss);
         const float iv = rms_inv(ss, HD, a.eps);
+        if constexpr (RREG) {   // normalise and rotate in registers (T.c:150-189)
+            const float n0 = hv[0] * iv * hw[0], n1 = hv[1] * iv * hw[1];
+            qk[hh0 * HD + lane] = n0 * rc[0] - n1 * rs[0];
+            qk[hh0 * HD + lane + 64] = n1 * rc[1] + n0 * rs[1];
+        } else {
 #pragma unroll
-        for (int j = 0; j < HJ; ++j) {
-            const int i = lane + 64 * j;
-            if (i < HD) xn[hh0 * HD + i] = hv[j] * iv * hw[j];
+            for (int j = 0; j < HJ; ++j) {
+                const int i = lane + 64 * j;
+                if (i < HD) xn[hh0 * HD + i] = hv[j] * iv * hw[j];
+            }
         }
     }
     if (owner && tid < HD) vv[tid] = vtok;
     __syncthreads();
+    if constexpr (!RREG) {
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-        const int i = tid + 256 * j;
-        if (i < (GPH + 1) * HD) {
-            const int e = i % HD, hb = i - e;
-            constexpr int half = HD / 2;
-            qk[i] = e < half ? xn[i] * rc[j] - xn[hb + e + half] * rs[j] : xn[i] * rc[j] + xn[hb + e - half] * rs[j];
+        for (int j = 0; j < RJ; ++j) {
+            const int i = tid + 256 * j;
+            if (i < (GPH + 1) * HD) {
+                const int e = i % HD, hb = i - e;
+                constexpr int half = HD / 2;
+                qk[i] = e < half ? xn[i] * rc[j] - xn[hb + e + half] * rs[j] : xn[i] * rc[j] + xn[hb + e - half] * rs[j];
+            }
         }
+        __syncthreads();
     }
-    __syncthreads();
     if (owner && tid < HD && !(a.skip && a.skip[r])) {
         a.kc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = qk[GPH * HD + tid];
         a.vc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = vv[tid];
@@ -429,6 +440,18 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
         res[j] = s;
     }
     float *outr = a.out + (size_t)r * a.ld_out + kvh * GPH * HD;
+    const int stride = NO + 2 * GPH;
+    float *base = a.part + (size_t)(r * a.KV + kvh) * a.nsplit * stride;
+    if (a.defer) {   // every split leaves (acc, max, sum); the O projection merges (GemvArgs::amerge)
+        float *mine = base + (size_t)split * stride;
+#pragma unroll
+        for (int j = 0; j < (NO + 255) / 256; ++j) {
+            const int o = tid + 256 * j;
+            if (o < NO) mine[o] = res[j];
+        }
+        if (tid < GPH) { mine[NO + 2 * tid] = ml[tid][0]; mine[NO + 2 * tid + 1] = ml[tid][1]; }
+        return;
+    }
     if (nact == 1) {
 #pragma unroll
         for (int j = 0; j < (NO + 255) / 256; ++j) {
@@ -442,8 +465,6 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     // costs ~3.5 us per workgroup): write-through (sc1) stores, every wave
     // drains them, one relaxed ticket add per workgroup, the last arriver
     // reads the partials with sc1 loads ----
-    const int stride = NO + 2 * GPH;
-    float *base = a.part + (size_t)(r * a.KV + kvh) * a.nsplit * stride;
     float *mine = base + (size_t)split * stride;
 #pragma unroll
     for (int j = 0; j < (NO + 255) / 256; ++j) {
@@ -481,8 +502,8 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
             for (int s2 = 0; s2 < 8; ++s2) {
                 if (s2 < nact) {
                     const float f = expf(mm[s2] - M);
-                    num += f * aa[s2];
-                    den += f * ll[s2];
+                    num = fmaf(f, aa[s2], num);
+                    den = fmaf(f, ll[s2], den);
                 }
             }
             if (o < NO) outr[o] = num / den;
@@ -501,8 +522,8 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
             for (int s2 = 0; s2 < nact; ++s2) {
                 const float *ps = base + (size_t)s2 * stride;
                 const float f = expf(ld_sc1(ps + NO + 2 * g) - M);
-                num += f * ld_sc1(ps + o);
-                den += f * ld_sc1(ps + NO + 2 * g + 1);
+                num = fmaf(f, ld_sc1(ps + o), num);
+                den = fmaf(f, ld_sc1(ps + NO + 2 * g + 1), den);
             }
             outr[o] = num / den;
         }
@@ -593,6 +614,11 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
 static int attn_lpk(int HD) { return HD >= 32 ? HD / 32 : 1; }
 int qtts_attn_keys_per_split(int HD) { return 256 / attn_lpk(HD); }
 
+bool qtts_attn_defer_ok(const AttnArgs &a) {
+    const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
+    return a.mode == 0 && a.win == 0 && a.KV > 0 && a.NH == 2 * a.KV && hd_ok && a.S > 16 && a.part && a.nsplit >= 1;
+}
+
 int qtts_attention(const AttnArgs &a, hipStream_t st) {
     if (a.HD > 128 || a.HD < 8 || (a.HD & 7) || a.NH % a.KV) {
         fprintf(stderr, "qtts_attention: unsupported head config NH=%d KV=%d HD=%d\n", a.NH, a.KV, a.HD);
@@ -613,7 +639,7 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
     if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok) {
         const int ch = qtts_attn_keys_per_split(a.HD);
         const int nsplit = (a.S + ch - 1) / ch;
-        if (nsplit > 1 && (!a.part || !a.cnt || a.nsplit < nsplit)) {
+        if ((nsplit > 1 || a.defer) && (!a.part || !a.cnt || a.nsplit < nsplit)) {
             fprintf(stderr, "qtts_attention: split scratch missing (need %d splits)\n", nsplit);
             return -1;
         }

@@ -44,8 +44,13 @@ __device__ __forceinline__ float dot8w(const v4u &w, const float *x) {
     return s;
 }
 
+// AM: x is the talker decode attention's output, merged here from its split
+// partials (GemvArgs::amerge, AttnArgs::defer) -- the merge the attention's
+// last split would do (k_attn.hip), in the same order and arithmetic:
+// M = max_s m_s, f_s = expf(m_s - M), x = (sum_s f_s acc_s) / (sum_s f_s l_s).
+constexpr int AM_MS = 4;   // splits whose partials are loaded before the weights
 // Dynamic LDS: [xs: C floats][red: 4 floats] (16-B aligned, Guideline 17).
-template <int RW, int NV, bool NT>
+template <int RW, int NV, bool NT, bool AM = false>
 __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int C = 512 * NV, XQ = C / 1024 > 0 ? (C + 1023) / 1024 : 1;   // float4 of x per thread
@@ -73,8 +78,33 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     float4 xv[XQ], pv[XQ][PMAX > 0 ? PMAX : 1], nwv[XQ];
     uint2 tv[XQ];
     const int np = a.xadd ? a.n_xadd : 0;
+    // AM: the first AM_MS splits' partials of every unit (their addresses need
+    // no live length: slots past it hold stale values, masked below), and the
+    // position, all in one round trip
+    float4 am_a[AM ? XQ : 1][AM_MS];
+    float am_m[AM ? XQ : 1][AM_MS], am_l[AM ? XQ : 1][AM_MS];
+    int am_p = 0;
+    if constexpr (AM) {
+        am_p = a.am_pos[0];
+        const int HDm = a.am_hd, GP = a.am_gph, NO = GP * HDm, stride = NO + 2 * GP;
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) {
+            const int c = 4 * (tid + 256 * q);
+            const int cc = c < C ? c : 0;
+            const int h = cc / HDm, kvh = h / GP, g = h - kvh * GP;
+            const float *mb = a.amerge + (size_t)kvh * a.am_nsplit * stride;
+#pragma unroll
+            for (int s2 = 0; s2 < AM_MS; ++s2) {
+                const int sc = s2 < a.am_nsplit ? s2 : 0;
+                am_a[q][s2] = *reinterpret_cast<const float4 *>(mb + (size_t)sc * stride + (cc - h * HDm) + g * HDm);
+                am_m[q][s2] = mb[(size_t)sc * stride + NO + 2 * g];
+                am_l[q][s2] = mb[(size_t)sc * stride + NO + 2 * g + 1];
+            }
+        }
+    }
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
+        if constexpr (AM) break;
         const int c = 4 * (tid + 256 * q);
         const int cc = c < C ? c : 0;
         if (trow) tv[q] = *reinterpret_cast<const uint2 *>(trow + cc);
@@ -97,6 +127,42 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
         }
     }
 
+    if constexpr (AM) {   // 3a. the attention merge, split order (k_attn_dec's last-split merge)
+        const int HDm = a.am_hd, GP = a.am_gph, NO = GP * HDm, stride = NO + 2 * GP;
+        const int nact = (am_p + 1 + a.am_ch - 1) / a.am_ch;
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) {
+            const int c = 4 * (tid + 256 * q);
+            const int cc = c < C ? c : 0;
+            const int h = cc / HDm, kvh = h / GP, g = h - kvh * GP, eo = (cc - h * HDm) + g * HDm;
+            const float *mb = a.amerge + (size_t)kvh * a.am_nsplit * stride;
+            float M = -INFINITY;
+#pragma unroll
+            for (int s2 = 0; s2 < AM_MS; ++s2)
+                if (s2 < nact) M = fmaxf(M, am_m[q][s2]);
+            for (int s2 = AM_MS; s2 < nact; ++s2) M = fmaxf(M, mb[(size_t)s2 * stride + NO + 2 * g]);
+            float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+            float den = 0.f;
+#pragma unroll
+            for (int s2 = 0; s2 < AM_MS; ++s2) {
+                if (s2 < nact) {
+                    const float f = expf(am_m[q][s2] - M);
+                    num.x = fmaf(f, am_a[q][s2].x, num.x); num.y = fmaf(f, am_a[q][s2].y, num.y);
+                    num.z = fmaf(f, am_a[q][s2].z, num.z); num.w = fmaf(f, am_a[q][s2].w, num.w);
+                    den = fmaf(f, am_l[q][s2], den);
+                }
+            }
+            for (int s2 = AM_MS; s2 < nact; ++s2) {
+                const float *ps = mb + (size_t)s2 * stride;
+                const float f = expf(ps[NO + 2 * g] - M);
+                const float4 av = *reinterpret_cast<const float4 *>(ps + eo);
+                num.x = fmaf(f, av.x, num.x); num.y = fmaf(f, av.y, num.y);
+                num.z = fmaf(f, av.z, num.z); num.w = fmaf(f, av.w, num.w);
+                den = fmaf(f, ps[NO + 2 * g + 1], den);
+            }
+            xv[q] = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+        }
+    }
     // 3. residual + partials summed in partial order, RMS statistic
     if (trow) {
 #pragma unroll
@@ -185,7 +251,26 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
 // -1 on a launch error.  Covers nb == 1, C = 512 NV, R = 1024 RW (grid 256,
 // one workgroup per CU) or R = 2048 RW (grid 512) where RW * NV loads per
 // lane would not fit one workgroup per CU.
+bool qtts_gemvw_amerge_ok(int R, int C) { return C == 2048 && (R == 1024 || R == 2048); }
+
 int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
+    if (a.amerge) {   // the talker O projection with the attention merge in its prologue
+        if (a.nb != 1 || !qtts_gemvw_amerge_ok(a.R, a.C) || a.xadd || a.table || a.table_f32 || a.norm_w ||
+            a.am_gph * a.am_hd * (a.C / (a.am_gph * a.am_hd)) != a.C || a.am_hd % 4 || a.am_nsplit < 1 || a.reps != 1) {
+            fprintf(stderr, "qtts_gemvw: attention-merge prologue unsupported (R=%d C=%d)\n", a.R, a.C);
+            return -1;
+        }
+        const dim3 grid(a.R / (4 * (a.R / 1024)));
+        const size_t smem = (size_t)(a.C + 4) * sizeof(float);
+        if (a.R == 2048) {
+            hipLaunchKernelGGL((k_gemvw<2, 4, true, true>), grid, dim3(256), smem, st, a);
+            qtts_last_kernel = "k_gemvw<2, 4, true, true>";
+        } else {
+            hipLaunchKernelGGL((k_gemvw<1, 4, true, true>), grid, dim3(256), smem, st, a);
+            qtts_last_kernel = "k_gemvw<1, 4, true, true>";
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart) return 1;
     if (a.reps < 1 || a.reps > 65535 || (a.reps > 1 && (!a.ids || a.xadd || a.xcopy || a.row_sel))) return 1;
     // sources: an fp32 row, a bf16 / fp32 table row (+ per-head partials too:

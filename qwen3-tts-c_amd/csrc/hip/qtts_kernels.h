@@ -34,6 +34,12 @@ struct GemvArgs {
     const float *xadd = nullptr;
     int n_xadd = 0, ld_xadd = 0;
     int ldb_xadd = 0;               // batch path (k_gemvm): row b of partial p at xadd + p*ld_xadd + b*ldb_xadd
+    // batch-1 prologue only: x = the decode attention's output, merged here
+    // from its split partials (AttnArgs::defer): amerge [KV][am_nsplit][GPH*HD
+    // + 2*GPH], am_ch keys per split, the live key count am_pos[0] + 1
+    const float *amerge = nullptr;
+    const int *am_pos = nullptr;
+    int am_nsplit = 0, am_ch = 0, am_hd = 0, am_gph = 0;
     // batch path split-K producer (k_gemvm): kz > 1 workgroup columns each take
     // C / kz of K and store raw partials ypart[z*ld_ypart + b*R + r] (the
     // consumer adds them with the residual through xadd); y / epi unused
@@ -67,6 +73,8 @@ struct GemvArgs {
 int qtts_gemv(const GemvArgs &a, hipStream_t st);
 // batch-1 wave-per-row GEMV for Infinity-Cache-resident weights (k_gemvw.hip); 1 = not covered
 int qtts_gemvw(const GemvArgs &a, hipStream_t st);
+// shapes whose batch-1 GEMV takes the decode attention's merge in its prologue (GemvArgs::amerge)
+bool qtts_gemvw_amerge_ok(int R, int C);
 // lock-step batch (2..16 rows) on the bf16 matrix cores (k_gemvm.hip); 1 = not covered
 int qtts_gemvm(const GemvArgs &a, hipStream_t st);
 // the same with the x rows sliced per wave (k_gemvb.hip, tried first); 1 = not covered
@@ -102,8 +110,15 @@ struct AttnArgs {
     float *part = nullptr;
     int *cnt = nullptr;
     int nsplit = 0;
+    // decode: every split (one or more) leaves its (acc, max, sum) in `part`
+    // and the merge is the consumer's (GemvArgs::amerge, the O projection's
+    // prologue) instead of the last split's
+    int defer = 0;
 };
 int qtts_attn_keys_per_split(int HD);
+// true when the decode attention takes these arguments on its split kernel,
+// whose merge AttnArgs::defer hands to the consumer
+bool qtts_attn_defer_ok(const AttnArgs &a);
 // sub-talker attention + O projection split by kv head: part [KV][nrows][R]
 // (GQA 2, <= 16 keys); 1 = not covered
 int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStream_t st);

@@ -112,6 +112,8 @@ struct qtts_dev {
     const float *tk_pend = nullptr;
     int tk_npend = 0;
     bool bsplit = true;      // QTTS_HIP_BSPLIT=0: batch O / down projections without split-K
+    int bself_min = 9;       // batch split-K producers reduce their own partials from this many rows up
+    int bkz_max = 0;         // QTTS_HIP_BKZ_MAX: cap on the batch split-K columns (0: 2 up to 8 rows, else 4)
     float *x_st = nullptr, *qkv_s = nullptr, *att_s = nullptr, *h_s = nullptr, *logits_s = nullptr;
     float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
     int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
@@ -151,6 +153,7 @@ struct qtts_dev {
     std::vector<Prof> prof;
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
+    bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
     int pinv_cap = 0;
 
@@ -357,6 +360,12 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     // O projection as two kernels
     const char *bs = getenv("QTTS_HIP_BSPLIT");
     dv->bsplit = !(bs && !atoi(bs));
+    const char *bk = getenv("QTTS_HIP_BKZ_MAX");
+    if (bk) dv->bkz_max = atoi(bk) < 1 ? 1 : atoi(bk) > 4 ? 4 : atoi(bk);
+    const char *bm = getenv("QTTS_HIP_BSELF_MIN");
+    if (bm) dv->bself_min = atoi(bm);
+    const char *ad = getenv("QTTS_HIP_ATTN_DEFER");
+    dv->attn_defer = !(ad && !atoi(ad));
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
     codec_init(&dv->codec, dims, dv->st);
@@ -771,7 +780,10 @@ static int build_qkv0_table(qtts_dev *dv) {
 static int bsplit_kz(const qtts_dev *dv, int R, int C) {
     if (!dv->bsplit || dv->nrun < 2) return 0;
     int kz = R / 16 >= 256 ? 1 : 256 / (R / 16);
-    if (kz > 4) kz = 4;
+    // (up to 8 rows the consumers add the partials: 2 columns measured +0.8 %
+    // at batch 8 over 4, gpurun_out/kz1, profiles/r03b_batch_kz_ab.txt)
+    const int cap = dv->bkz_max > 0 ? dv->bkz_max : dv->nrun <= 8 ? 2 : 4;
+    if (kz > cap) kz = cap;
     while (kz > 1 && C % (32 * kz)) kz /= 2;
     return kz > 1 ? kz : 0;
 }
@@ -784,7 +796,7 @@ static int bsplit_kz(const qtts_dev *dv, int R, int C) {
 // vs 76.0, 8 123.6 vs 126.3, 16 193.3 vs 189.0.
 static bool split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz) {
     g.ypart = part; g.kz = kz; g.ld_ypart = (size_t)dv->nrun * g.R;
-    if (dv->nrun > 8) { g.tick = dv->btick; return false; }
+    if (dv->nrun >= dv->bself_min) { g.tick = dv->btick; return false; }
     g.y = nullptr;
     return true;
 }
@@ -813,9 +825,17 @@ static int talker_layers(qtts_dev *dv) {
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
         t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
+        // batch 1: the attention's split merge moves into the O projection's
+        // prologue (one dependent hand-off fewer per layer)
+        const bool defer = dv->attn_defer && nb == 1 && qtts_attn_defer_ok(t) && qtts_gemvw_amerge_ok(d.H, AD);
+        t.defer = defer;
         CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
         if (pend) { std::swap(xa, xb); pend = nullptr; }
         GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
+        if (defer) {
+            o.amerge = dv->att_part; o.am_pos = dv->kv_len; o.am_nsplit = dv->att_nsplit;
+            o.am_ch = qtts_attn_keys_per_split(d.HD); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
+        }
         const bool opend = kzo && split_out(dv, o, dv->bpo, kzo);
         CKI(pgemv(dv, o, PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
