@@ -25,7 +25,13 @@ Also reported:
   roofline         dominant kernel (weight-streaming GEMV), measured live with
                    HIP events on the context stream over one eager frame
   cpu_baseline     the reference c/ build (oracle/_ref/qwen-tts, scalar+OpenMP)
-                   on a bounded sample of the same workload, rank 0, N=1 only
+                   on a bounded sample of the same workload, rank 0, N=1 only:
+                   3 timed runs of 8 frames at the host cores this process may
+                   use, plus a 1-thread row (one 2-frame run), the 128-frame
+                   workload extrapolated from the median run
+  --eos            the reference's default mode instead of fixed length
+                   (max_new_tokens 4096, EOS stop), with the same-length
+                   fixed-mode time beside it (eos_mode)
 """
 import argparse
 import glob
@@ -55,14 +61,21 @@ def dist_setup():
     return ws, rank, local
 
 
+def _pg():
+    """True once a torch.distributed process group exists (every multi-rank run;
+    a one-rank run with QTTS_BENCH_PG=1, tests/test_dist.py)."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(ws):
-    if ws > 1:
+    if ws > 1 or _pg():
         import torch.distributed as dist
         dist.barrier()
 
 
 def _reduce(ws, v, op):
-    if ws == 1:
+    if ws == 1 and not _pg():
         return v
     import torch
     import torch.distributed as dist
@@ -88,12 +101,12 @@ def rank_prompt_seeds(rank, batch):
     return [1234 + rank * batch + i for i in range(batch)]
 
 
-def ensure_model_shared(md, preset, ws, local):
+def ensure_model_shared(md, preset, ws, local, overrides=None):
     """local rank 0 of the node writes the model; the others wait."""
     from synth_model import ensure_model
     if local == 0:
         t = time.time()
-        ensure_model(md, preset, seed=0)
+        ensure_model(md, preset, seed=0, overrides=overrides)
         log(f"[bench] model {preset} ready in {time.time() - t:.1f}s at {md}")
     barrier(ws)
 
@@ -281,13 +294,18 @@ def spawn_ranks(n):
 def gather_ranks(ws, rec):
     """Per-rank records {rank, device, utterances, samples, frames, wall_ms} to
     every rank (the only exchange is this gather)."""
-    if ws == 1:
+    if ws == 1 and not _pg():
         return [rec]
     import torch.distributed as dist
     out = [None] * ws
     dist.all_gather_object(out, rec)
     return out
 
+
+# bench.py --eos: the codec head's EOS row gain of the synthetic model
+# (tools/synth_model.py eos_gain; tools/eos_gain_probe.py: rank 0's P128
+# utterance stops at frame 157 under the default sampling at 1.2-1.4)
+EOS_GAIN = 1.4
 
 # SURVEY.md §8(d): algorithmic bytes per frame at batch 1 = unique weights +
 # talker KV at 2 B/element (bf16) per position
@@ -305,7 +323,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU per step (lock-step batch)")
     ap.add_argument("--cpu-frames", type=int, default=8, help="frames per run of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the physical cores this process may use")
-    ap.add_argument("--cpu-1thread", action="store_true", help="also time the reference with 1 thread (slow)")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="timed runs of the CPU-baseline sample (SURVEY.md 8d: 3)")
+    ap.add_argument("--no-cpu-1thread", action="store_true", help="skip the reference's 1-thread row")
+    ap.add_argument("--cpu-1thread", action="store_true", help="(C1 line) also time the reference with 1 thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--model-dir", default=None)
@@ -315,6 +335,10 @@ def main():
                          "decode of reference ++ generated")
     ap.add_argument("--vc-codes", action="store_true",
                     help="with --voice-clone: start from seeded reference codes + x-vector (no audio encode)")
+    ap.add_argument("--eos", action="store_true",
+                    help="the reference's default generation mode: max_new_tokens 4096 with the EOS stop, on the "
+                         "synthetic model with the codec head's EOS row x EOS_GAIN (its utterance stops at frame 157); "
+                         "also times fixed-length decodes of the same length")
     ap.add_argument("--c1", action="store_true",
                     help="BASELINE C1 only: the reference c/ CLI on the 0.6B synthetic model, short prompt "
                          "(test/tokens_great_power.txt), on the host cores; no GPU")
@@ -334,23 +358,29 @@ def main():
     backend = os.environ.get("QTTS_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     dev = local % ndev if ndev else local
-    if ws > 1:
+    if ws > 1 or os.environ.get("QTTS_BENCH_PG") == "1":
         import torch.distributed as dist
         torch.cuda.set_device(dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+        log(f"[bench] rank {rank}: process group {dist.get_backend()} (world {dist.get_world_size()}, device {dev})")
     import qtts
     from synth_model import prompt_ids
 
     # the same synthetic dir the GPU tests generate (tests/conftest.py model_dir): one 3.4 GB write per box
-    md = args.model_dir or os.path.join(os.environ.get("QTTS_TEST_MODELS", "/tmp/qtts_test_models"), args.preset)
-    ensure_model_shared(md, args.preset, ws, local)
+    ovr = {"eos_gain": EOS_GAIN} if args.eos else None
+    mtag = args.preset + (f"_eos_gain{EOS_GAIN}" if args.eos else "")
+    md = args.model_dir or os.path.join(os.environ.get("QTTS_TEST_MODELS", "/tmp/qtts_test_models"), mtag)
+    ensure_model_shared(md, args.preset, ws, local, ovr)
     t = time.time()
     m = qtts.QwenTTS(md, device=dev)
     log(f"[bench] rank {rank}: model loaded on HIP device {dev} in {time.time() - t:.1f}s")
-    m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
+    if args.eos:   # the reference's defaults: max_new_tokens 4096, EOS stop (Q.c:871-880, 1324-1330)
+        m.set_params(max_tokens=4096, fixed=0, seed=42 + rank)
+    else:
+        m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
     prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
 
     vc = None
@@ -409,12 +439,29 @@ def main():
     torch.cuda.synchronize()
     barrier(ws)
     el = time.perf_counter() - t0
+    eos = None
+    if args.eos:
+        # the same utterances at the same length in fixed-length mode: what the
+        # EOS mode itself costs (host polling every 8 frames, the attention grid
+        # sized from the 4096-frame KV capacity)
+        n_eos = samples // (1920 * args.steps * args.batch)
+        m.set_params(max_tokens=n_eos, fixed=n_eos, seed=42 + rank)
+        one_step()
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        sf = sum(one_step() for _ in range(args.steps))
+        torch.cuda.synchronize()
+        elf = time.perf_counter() - tf
+        m.set_params(max_tokens=4096, fixed=0, seed=42 + rank)
+        eos = dict(eos_gain=EOS_GAIN, frames_per_utterance=n_eos, max_new_tokens=4096,
+                   fixed_same_length_audio_s_per_s=round(sf / 24000.0 / elf, 3),
+                   fixed_same_length_ms_per_step=round(elf / args.steps * 1e3, 2))
     el_max = reduce_max(ws, el)
     audio_total = reduce_sum(ws, samples / 24000.0)
     value = audio_total / el_max
     ms_per_step = el_max / args.steps * 1e3
     ranks = gather_ranks(ws, dict(rank=rank, device=dev, utterances=args.batch * args.steps, samples=samples,
-                                  frames=args.batch * args.steps * args.frames, wall_ms=round(el * 1e3, 2)))
+                                  frames=samples // 1920, wall_ms=round(el * 1e3, 2)))
 
     # ---- first packet (BASELINE.json metric, configs[2]): streaming generation,
     # wall time from the call to the first audio chunk (frame 0 decoded by the
@@ -475,13 +522,13 @@ def main():
     # the reference c/ CPU leg belongs to the custom-voice line (the c/ reference
     # has no voice clone); a voice-clone line carries the encoders' host port
     # baseline in ref_audio_encode instead
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and vc is None:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and vc is None and not args.eos:
         thr = args.cpu_threads or cpu_threads_default()
-        cpu = cpu_baseline(md, prompts[0], thr, frames=args.cpu_frames, target_frames=args.frames)
-        if cpu and args.cpu_1thread:
-            one = cpu_baseline(md, prompts[0], 1, frames=2, warmup=0, runs=2, target_frames=args.frames, timeout=3000)
+        cpu = cpu_baseline(md, prompts[0], thr, frames=args.cpu_frames, runs=args.cpu_runs, target_frames=args.frames)
+        if cpu and not args.no_cpu_1thread:
+            one = cpu_baseline(md, prompts[0], 1, frames=2, warmup=0, runs=1, target_frames=args.frames, timeout=3000)
             if one:
-                cpu["one_thread"] = {k: one[k] for k in ("value", "unit", "cores", "sample")}
+                cpu["one_thread"] = {k: one[k] for k in ("value", "unit", "cores", "sample", "runs")}
 
     if rank == 0:
         out = {
@@ -503,8 +550,10 @@ def main():
                                        "on the GPU inside the step) + 20-id reference text, codec over reference ++ "
                                        "generated (reference part cut)") if wavs is not None else
                                       (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, "
-                                       "codec over reference ++ generated (reference part cut)") if vc else ""),
-                       "global_batch": args.batch * ws, "frames": args.frames,
+                                       "codec over reference ++ generated (reference part cut)") if vc else
+                                      (f", EOS mode (max_new_tokens 4096, codec-head EOS row x {EOS_GAIN}: the "
+                                       f"utterance stops at frame {eos['frames_per_utterance']})") if eos else ""),
+                       "global_batch": args.batch * ws, "frames": eos["frames_per_utterance"] if eos else args.frames,
                        "parallelism": f"dp{ws} (independent replicas, no collective in the data path)"},
         }
         if fp:
@@ -513,8 +562,10 @@ def main():
         out["ranks"] = ranks
         if enc:
             out["ref_audio_encode"] = enc
+        if eos:
+            out["eos_mode"] = eos
         fw = FRAME_WEIGHT_BYTES.get(args.preset)
-        if fw and vc is None:
+        if fw and vc is None and not args.eos:
             # §8(d) headline: utterance-frames per second x algorithmic bytes per
             # frame (weights once per lock-step step + B x KV) over 8 TB/s; the
             # mean talker position is prefill (10 rows: 3 role + 7 codec-prefix

@@ -279,6 +279,12 @@ float *qwen_tts_generate_voice_clone_audio_stream(qwen_tts_ctx_t *ctx, const cha
                                                   const float *ref_wav, int n_ref_samples, const char *language,
                                                   int x_vector_only, int non_streaming, int chunk_frames,
                                                   qwen_tts_audio_cb cb, void *userdata, int *out_samples);
+/* Resample mono PCM from sr_in to sr_out Hz (reference audio at another rate;
+ * the Python reference resamples to 24 kHz with librosa, qwen3_tts_model.py:
+ * 441-444): librosa's "polyphase" method = scipy.signal.resample_poly (Kaiser
+ * windowed-sinc FIR, ceil(n * sr_out / sr_in) samples).  malloc'd, *n_out set;
+ * NULL on error. */
+float *qwen_tts_resample(const float *in, int n_in, int sr_in, int sr_out, int *n_out);
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
     }
 }
 
-// k_conv on the bf16 matrix cores (QTTS_HIP_CONV_BF, default on): same
+// k_conv on the bf16 matrix cores: same
 // tiles, grid, splits and epilogues, fp32-equivalent products.  The weights
 // and the staged input are split exactly into three bf16 planes, w = w1 + w2
 // + w3 and x = x1 + x2 + x3, and the six products with i + j <= 4 are

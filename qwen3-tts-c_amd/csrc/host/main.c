@@ -44,8 +44,8 @@ static void usage(const char *prog) {
             "  --device N (HIP device, default 0)   --batch N (lock-step batch of N copies, default 1)\n"
             "  --stream N (streaming decode, audio chunks every N frames after the first)\n"
             "voice clone (include/qwen_tts.h qwen_tts_generate_voice_clone[_audio]):\n"
-            "  --ref-audio <wav>   reference audio (mono/stereo PCM16 or float WAV at 24 kHz): encoded on\n"
-            "                      the GPU (12 Hz codes + speaker x-vector)\n"
+            "  --ref-audio <wav>   reference audio (mono/stereo PCM16 or float WAV; other rates are resampled\n"
+            "                      to 24 kHz): encoded on the GPU (12 Hz codes + speaker x-vector)\n"
             "  --x-vector-only     with --ref-audio: x-vector only (no reference codes / ref text)\n"
             "  --ref-codes <file>  12 Hz codes of the reference audio, 16 ints per frame (any separators)\n"
             "  --ref-text <ids>    ids of \"<|im_start|>assistant\\n{ref text}<|im_end|>\\n\" (ICL mode)\n"
@@ -258,9 +258,15 @@ int main(int argc, char **argv) {
         int sr = 0;
         if (!(ref_wav = read_wav(ref_audio, &n_ref_wav, &sr))) { free(file_ids); return 1; }
         if (sr != QWEN_TTS_SAMPLE_RATE) {   /* the reference resamples with librosa (qwen3_tts_model.py:441-444) */
-            fprintf(stderr, "Error: --ref-audio must be %d Hz (got %d Hz); resample it first\n", QWEN_TTS_SAMPLE_RATE, sr);
-            free(ref_wav); free(file_ids);
-            return 1;
+            int n24 = 0;
+            float *w24 = qwen_tts_resample(ref_wav, n_ref_wav, sr, QWEN_TTS_SAMPLE_RATE, &n24);
+            free(ref_wav);
+            if (!w24) { fprintf(stderr, "Error: cannot resample --ref-audio from %d Hz\n", sr); free(file_ids); return 1; }
+            if (verbose >= 1)
+                fprintf(stderr, "Reference audio resampled %d -> %d Hz (polyphase): %d -> %d samples\n", sr,
+                        QWEN_TTS_SAMPLE_RATE, n_ref_wav, n24);
+            ref_wav = w24;
+            n_ref_wav = n24;
         }
         if (!xvec_only && !ref_text) {
             fprintf(stderr, "Error: ref_text is required when x_vector_only_mode=False (ICL mode): pass --ref-text or --x-vector-only\n");

@@ -2,6 +2,7 @@
  * clamp to [-1, 1], (int16)(s * 32767) truncation, write to <path>.tmp then
  * rename so a reader never sees a partial file). */
 #include <errno.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -61,4 +62,75 @@ int qwen_tts_write_wav(const char *path, const float *samples, int n_samples, in
         return -1;
     }
     return 0;
+}
+
+/* ------------------------------------------------------------------ resampling
+ * Reference audio at another rate (the Python reference resamples it to 24 kHz
+ * with librosa.resample, qwen_tts/inference/qwen3_tts_model.py:441-444).  This
+ * is librosa's res_type="polyphase" path, i.e. scipy.signal.resample_poly
+ * (up / down = sr_out / sr_in reduced by their gcd): the firwin low-pass of
+ * 2 * 10 * max(up, down) + 1 taps, cutoff 1 / max(up, down), Kaiser window
+ * beta 5, unit DC gain times up, zero padding, upfirdn with scipy's phase
+ * alignment, ceil(n * up / down) samples out; computed in double precision.
+ * (librosa's default res_type is soxr_hq, a different filter: parity with it
+ * is unpinned; tests/test_resample.py pins this to scipy.) */
+static double bessel_i0(double x) {
+    double s = 1.0, t = 1.0;
+    for (int k = 1; k < 200; k++) {
+        t *= (x / (2.0 * k)) * (x / (2.0 * k));
+        s += t;
+        if (t < s * 1e-17) break;
+    }
+    return s;
+}
+
+static long gcd_l(long a, long b) {
+    while (b) { long t = a % b; a = b; b = t; }
+    return a;
+}
+
+float *qwen_tts_resample(const float *in, int n_in, int sr_in, int sr_out, int *n_out) {
+    if (n_out) *n_out = 0;
+    if (!in || n_in < 1 || sr_in < 1 || sr_out < 1 || !n_out) return NULL;
+    const long g = gcd_l(sr_out, sr_in), up = sr_out / g, down = sr_in / g;
+    const long no = (long)n_in * up / down + (((long)n_in * up) % down ? 1 : 0);
+    float *out = (float *)malloc((size_t)(no > 0 ? no : 1) * sizeof(float));
+    if (!out) return NULL;
+    if (up == 1 && down == 1) {
+        memcpy(out, in, (size_t)n_in * sizeof(float));
+        *n_out = n_in;
+        return out;
+    }
+    const long maxr = up > down ? up : down, half = 10 * maxr, taps = 2 * half + 1;
+    /* firwin: cutoff * sinc(cutoff * m) x kaiser(taps, 5), scaled to unit DC gain, times up */
+    const long pre = down - half % down;           /* scipy's n_pre_pad */
+    const long L = pre + taps;                      /* (n_post_pad is never needed for n_out samples) */
+    double *h = (double *)calloc((size_t)L, sizeof(double));
+    if (!h) { free(out); return NULL; }
+    const double fc = 1.0 / (double)maxr, beta = 5.0, i0b = bessel_i0(beta);
+    double sum = 0.0;
+    for (long j = 0; j < taps; j++) {
+        const double m = (double)j - (double)(taps - 1) / 2.0;
+        const double x = fc * m;
+        const double sinc = x == 0.0 ? 1.0 : sin(M_PI * x) / (M_PI * x);
+        const double r = 2.0 * (double)j / (double)(taps - 1) - 1.0;
+        const double w = bessel_i0(beta * sqrt(1.0 - r * r > 0.0 ? 1.0 - r * r : 0.0)) / i0b;
+        h[pre + j] = fc * sinc * w;
+        sum += h[pre + j];
+    }
+    for (long j = 0; j < taps; j++) h[pre + j] = h[pre + j] / sum * (double)up;
+    const long skip = (half + pre) / down;          /* scipy's n_pre_remove */
+    for (long k = 0; k < no; k++) {
+        /* upfirdn output index t = (k + skip) * down: z[t] = sum_i x[i] h[t - i * up] */
+        const long t = (k + skip) * down;
+        long i0 = t - (L - 1) <= 0 ? 0 : (t - (L - 1) + up - 1) / up;
+        long i1 = t / up;
+        if (i1 > n_in - 1) i1 = n_in - 1;
+        double acc = 0.0;
+        for (long i = i0; i <= i1; i++) acc += (double)in[i] * h[t - i * up];
+        out[k] = (float)acc;
+    }
+    free(h);
+    *n_out = (int)no;
+    return out;
 }

@@ -72,7 +72,7 @@ EXPORTS = [
     "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream", "qwen_tts_tokenize",
     "qwen_tts_text_prompt", "qwen_tts_speaker_embedding", "qwen_tts_encode_audio",
     "qwen_tts_generate_voice_clone_audio", "qwen_tts_generate_voice_clone_audio_batch",
-    "qwen_tts_generate_voice_clone_audio_stream", "qtts_dev_codec_timing", "qtts_dev_codec_stage_ms",
+    "qwen_tts_generate_voice_clone_audio_stream", "qtts_dev_codec_timing", "qtts_dev_codec_stage_ms", "qwen_tts_resample",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
     "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
@@ -99,6 +99,19 @@ def tokenize(model_dir, text):
     ids = np.ctypeslib.as_array(C.cast(p, _ip), shape=(n.value,)).tolist() if n.value else []
     _libc.free(C.c_void_p(p))
     return ids
+
+
+def resample(wav, sr_in, sr_out=24000):
+    """qwen_tts_resample (host C, no GPU needed): librosa's polyphase method =
+    scipy.signal.resample_poly."""
+    w = np.ascontiguousarray(wav, np.float32)
+    n = C.c_int(0)
+    p = lib().qwen_tts_resample(w.ctypes.data_as(_fp), w.shape[0], int(sr_in), int(sr_out), C.byref(n))
+    if not p:
+        return None
+    out = np.ctypeslib.as_array(C.cast(p, _fp), shape=(n.value,)).copy()
+    _libc.free(C.c_void_p(p))
+    return out
 
 
 def lib():
@@ -138,6 +151,8 @@ def lib():
     L.qwen_tts_set_progress_callback.argtypes = [C.POINTER(Ctx), PROGRESS_CB, C.c_void_p]
     L.qwen_tts_write_wav.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
     L.qwen_tts_abi_sizeof_ctx.restype = C.c_size_t
+    L.qwen_tts_resample.restype = C.c_void_p
+    L.qwen_tts_resample.argtypes = [_fp, C.c_int, C.c_int, C.c_int, _ip]
     L.qwen_tts_tokenize.restype = C.c_void_p
     L.qwen_tts_tokenize.argtypes = [C.c_char_p, C.c_char_p, _ip]
     L.qwen_tts_text_prompt.restype = C.c_void_p

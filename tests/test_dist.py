@@ -127,3 +127,28 @@ def test_bench_gpus2_self_launch(gpu):
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 2
     assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
     assert all(x["samples"] == 4 * 1920 for x in line["ranks"])
+
+
+@pytest.mark.gpu
+def test_bench_rccl_process_group_one_rank(gpu):
+    """bench.py under torch.distributed.run with an RCCL ("nccl") process group
+    of one rank on cuda:0 (QTTS_BENCH_PG=1): the init with device_id, the
+    barriers around the timed region, the max / sum all-reduces on CUDA tensors
+    and the all_gather_object of the rank records all run through RCCL -- the
+    code the driver's 8-GPU scaling run takes, on the one GPU this box has."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QTTS_BENCH_PG="1")
+    env.pop("QTTS_BENCH_BACKEND", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+                        os.path.join(root, "bench.py"), "--gpus", "1", "--preset", "tiny", "--frames", "4",
+                        "--steps", "2", "--warmup", "0", "--no-cpu-baseline", "--no-profile"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "process group nccl (world 1, device 0)" in r.stderr, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and [x["rank"] for x in line["ranks"]] == [0]
+    assert line["ranks"][0]["samples"] == 2 * 4 * 1920 and line["value"] > 0
