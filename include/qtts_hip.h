@@ -118,6 +118,10 @@ int qtts_dev_frame(qtts_dev_t *dev, int step);
  * (non-fixed mode); n_gen[b] frames stored; stop_step[b] as in the
  * reference's "Stop: eos at step N". */
 int qtts_dev_poll(qtts_dev_t *dev, int *stopped, int *n_gen, int *stop_step);
+/* EOS mode, lagged: waits only until frame `step` has finished (launch frame
+ * step + 1 first) and sets *all_stopped when every slot had drawn EOS by then
+ * (the sampler mirrors the stops into pinned host memory). */
+int qtts_dev_frame_done(qtts_dev_t *dev, int step, int *all_stopped);
 /* Copies slot b's codes [n_gen][G] to host. */
 int qtts_dev_get_codes(qtts_dev_t *dev, int b, int *host_codes, int max_frames);
 /* Codec decode of slot b's generated codes (device-resident) into a malloc'd

@@ -638,7 +638,11 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
     }
     if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok) {
         const int ch = qtts_attn_keys_per_split(a.HD);
-        const int nsplit = (a.S + ch - 1) / ch;
+        // splits launched: the capacity's, or fewer when the caller knows the
+        // live keys stay below a.nsplit * ch (the frame graphs' split buckets;
+        // workgroups past the live length exit at once)
+        const int cap = (a.S + ch - 1) / ch;
+        const int nsplit = a.part && a.nsplit >= 1 && a.nsplit < cap ? a.nsplit : cap;
         if ((nsplit > 1 || a.defer) && (!a.part || !a.cnt || a.nsplit < nsplit)) {
             fprintf(stderr, "qtts_attention: split scratch missing (need %d splits)\n", nsplit);
             return -1;

@@ -145,6 +145,7 @@ struct SampArgs {
     int *counts = nullptr;         // [B][n] occurrences of each generated id
     int fixed = 0;
     int *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr, *stop_step = nullptr;
+    int *host_stopped = nullptr;   // pinned host mirror of `stopped` (set when a slot stops)
     uint32_t *st_rng = nullptr;    // sub-talker state reset per frame
     uint32_t seed_bits = 0;
     // outputs: codes[b*codes_bstride + cur_row[b]*G + g]

@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <set>
 #include <string>
@@ -136,6 +137,12 @@ struct qtts_dev {
     bool have_par = false;
     hipGraphExec_t g0 = nullptr, gN = nullptr;
     int graph_key = -1;
+    // EOS-mode lagged poll: the sampler mirrors each slot's stop into pinned
+    // host memory; an event after every frame lets the host wait for frame
+    // s - 1 while frame s is already queued (qtts_dev_frame_done)
+    int *hstop = nullptr;
+    int hstop_cap = 0;
+    hipEvent_t fev[2] = {nullptr, nullptr};
     // codec overlapped with the decode (qtts_dev_codec_async_*): its own stream,
     // ordered after the frames it decodes by an event; output stays on device
     hipStream_t cst = nullptr;
@@ -382,6 +389,9 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
     codec_destroy(&dv->codec);
     enc_destroy(&dv->enc);
     if (dv->cst) hipStreamSynchronize(dv->cst);
+    if (dv->hstop) hipHostFree(dv->hstop);
+    for (hipEvent_t e : dv->fev)
+        if (e) hipEventDestroy(e);
     if (dv->cwav) hipFree(dv->cwav);
     if (dv->pwav) hipFree(dv->pwav);
     if (dv->push_codes) hipFree(dv->push_codes);
@@ -601,6 +611,19 @@ static uint32_t seed_bits(int seed) {
 static int reset_counters(qtts_dev *dv) {
     const size_t B = dv->nb;
     hipStream_t st = dv->st;
+    if (dv->hstop_cap < (int)B) {   // (a new pointer: the frame graphs are re-captured)
+        if (dv->hstop) CK(hipHostFree(dv->hstop));
+        dv->hstop = nullptr;
+        CK(hipHostMalloc((void **)&dv->hstop, B * sizeof(int), hipHostMallocDefault));
+        dv->hstop_cap = (int)B;
+        dv->graph_key = -1;
+    }
+    if (!dv->fev[0]) {
+        CK(hipEventCreateWithFlags(&dv->fev[0], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&dv->fev[1], hipEventDisableTiming));
+    }
+    CK(hipStreamSynchronize(st));   // no frame of a previous run still writes the mirror
+    memset(dv->hstop, 0, B * sizeof(int));
     CK(hipMemsetAsync(dv->counts, 0, B * dv->d.V * sizeof(int), st));
     CK(hipMemsetAsync(dv->n_gen, 0, B * sizeof(int), st));
     CK(hipMemsetAsync(dv->stopped, 0, B * sizeof(int), st));
@@ -879,6 +902,7 @@ static int talker_head_sample(qtts_dev *dv) {
     s.rng = dv->rng; s.mode = 1; s.suppress_lo = d.V - 1024; s.eos = d.eos_id;
     s.rep = dv->par.repetition_penalty; s.counts = dv->counts; s.fixed = dv->par.fixed_codec_tokens;
     s.n_gen = dv->n_gen; s.stopped = dv->stopped; s.cur_row = dv->cur_row; s.stop_step = dv->stop_step;
+    s.host_stopped = dv->hstop;
     s.st_rng = dv->st_rng; s.seed_bits = seed_bits(dv->par.seed);
     s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G;
     return head_sample(dv, a, s, PK_GEMV_TALKER);
@@ -1050,6 +1074,11 @@ static int capture(qtts_dev *dv, bool with_talker, hipGraphExec_t *out) {
     return 0;
 }
 
+// One graph for step 0 (no talker) and one for every later frame, its talker
+// attention grid sized from the KV capacity (splits past the live length exit
+// at once).  Graphs per power-of-two bucket of the live key count measured no
+// faster, also in EOS mode (4096-frame capacity, 65 splits): 31.0 / 31.3 vs
+// 31.1 / 30.5 audio-s/s (profiles/r03c_eos_ab.txt).
 static int ensure_graphs(qtts_dev *dv) {
     if (dv->g0 && dv->gN && dv->graph_key == 1) return 0;
     if (dv->g0) { hipGraphExecDestroy(dv->g0); dv->g0 = nullptr; }
@@ -1237,6 +1266,23 @@ extern "C" int qtts_dev_frame(qtts_dev_t *dv, int step) {
     CKI(ensure_graphs(dv));
     if (dv->graph_key == 0) return record_frame(dv, step > 0);
     CK(hipGraphLaunch(step == 0 ? dv->g0 : dv->gN, dv->st));
+    CK(hipEventRecord(dv->fev[step & 1], dv->st));
+    return 0;
+}
+
+// EOS mode without a host round trip per frame: wait until frame `step` has
+// finished (the caller has already queued frame step + 1) and report whether
+// every running slot had drawn EOS by then.  At most one frame runs past the
+// last stop, against up to poll_every - 1 with a synchronous poll (which also
+// leaves the GPU idle until the next launch).
+extern "C" int qtts_dev_frame_done(qtts_dev_t *dv, int step, int *all_stopped) {
+    if (!dv || !all_stopped || !dv->hstop) return -1;
+    hipSetDevice(dv->device);
+    if (dv->graph_key == 1) CK(hipEventSynchronize(dv->fev[step & 1]));
+    else CK(hipStreamSynchronize(dv->st));
+    int all = 1;
+    for (int b = 0; b < dv->nrun; ++b) all &= ((volatile int *)dv->hstop)[b] != 0;
+    *all_stopped = all;
     return 0;
 }
 

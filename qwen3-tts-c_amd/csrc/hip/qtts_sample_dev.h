@@ -504,6 +504,7 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
             a.rng[b] = rng;
             if (a.fixed == 0 && tok == a.eos) {
                 a.stopped[b] = 1;
+                if (a.host_stopped) a.host_stopped[b] = 1;   // the host's lagged poll (qtts_dev_frame_done)
                 if (a.stop_step) a.stop_step[b] = ng;
             } else {
                 a.cur_row[b] = ng;

@@ -710,6 +710,9 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     }
     double t_gen = now_ms();
     const int poll_every = fixed > 0 ? 0 : 8;
+    /* EOS mode without streaming: a lagged poll per frame (qtts_dev_frame_done)
+     * instead of a synchronous one every 8 frames */
+    const int lagged = fixed == 0 && !stream;
     int step = 0;
     for (; step < max_tokens; step++) {
         if (qtts_dev_frame(dev, step) != 0) { free(sbuf); free(stopped); free(ngen); free(sstep); goto out; }
@@ -718,6 +721,16 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             ctx->perf_first_frame_ms = now_ms() - t_start;
         }
         if (ctx->progress_cb) ctx->progress_cb(step + 1, max_tokens, ctx->progress_cb_userdata);
+        if (lagged) {   /* EOS mode: frame step is queued; stop once every slot had stopped by frame step - 1 */
+            int done = 0;
+            if (step >= 1 && qtts_dev_frame_done(dev, step - 1, &done) != 0) {
+                free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
+            }
+            if (qwen_tts_verbose >= 1 && step > 0 && step % 10 == 0)
+                fprintf(stderr, "\r  Token %d (%.1f ms/token)...", step, (now_ms() - t_gen) / step);
+            if (done) break;
+            continue;
+        }
         const int want_stream = stream && (step == 0 || step + 1 - streamed >= stream->chunk || step + 1 == max_tokens);
         if (want_stream || (poll_every && ((step + 1) % poll_every == 0 || step + 1 == max_tokens))) {
             qtts_dev_poll(dev, stopped, ngen, sstep);

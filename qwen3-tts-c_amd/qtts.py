@@ -74,7 +74,7 @@ EXPORTS = [
     "qwen_tts_generate_voice_clone_audio", "qwen_tts_generate_voice_clone_audio_batch",
     "qwen_tts_generate_voice_clone_audio_stream", "qtts_dev_codec_timing", "qtts_dev_codec_stage_ms", "qwen_tts_resample",
     "qtts_hip_device_count", "qtts_dev_create", "qtts_dev_destroy", "qtts_dev_put_tensor", "qtts_dev_finalize",
-    "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll",
+    "qtts_dev_bytes", "qtts_dev_begin", "qtts_dev_prompt", "qtts_dev_prompt_ref", "qtts_dev_prefill", "qtts_dev_frame", "qtts_dev_poll", "qtts_dev_frame_done",
     "qtts_dev_get_codes", "qtts_dev_codec_slot", "qtts_dev_talker_prefill_host", "qtts_dev_talker_forward_host",
     "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
     "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_decode_matvec_bf16", "qtts_hip_resident_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
