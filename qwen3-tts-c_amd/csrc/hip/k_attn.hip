@@ -611,8 +611,18 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
 // workgroup.  HD / 32 (64-key splits at HD 128): 16-, 32- and 128-key splits
 // measured 29.3, 28.7, 27.9 vs 29.5 audio-s/s (r02m; the merge of more
 // partials costs more than the shorter splits save)
-static int attn_lpk(int HD) { return HD >= 32 ? HD / 32 : 1; }
-int qtts_attn_keys_per_split(int HD) { return 256 / attn_lpk(HD); }
+// With the merge deferred to the O projection (batch 1) the splits are halved
+// at HD 128: 32-key splits, attention 5.7 -> 4.7 us per layer at <= 138 keys
+// (the consumer merges 5 partials instead of 3; profiles/r03d_attn_split_ab.txt).
+// QTTS_HIP_ATTN_LPK (HD 128: 4, 8 or 16 lanes per key = 64-, 32- or 16-key
+// splits) overrides both for split-size A/B runs.
+static int attn_lpk(int HD, bool defer) {
+    static const int env = [] { const char *e = getenv("QTTS_HIP_ATTN_LPK"); return e ? atoi(e) : 0; }();
+    if (HD == 128 && (env == 4 || env == 8 || env == 16)) return env;
+    if (HD == 128 && defer) return 8;
+    return HD >= 32 ? HD / 32 : 1;
+}
+int qtts_attn_keys_per_split(int HD, bool defer) { return 256 / attn_lpk(HD, defer); }
 
 bool qtts_attn_defer_ok(const AttnArgs &a) {
     const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
@@ -637,7 +647,7 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok) {
-        const int ch = qtts_attn_keys_per_split(a.HD);
+        const int ch = qtts_attn_keys_per_split(a.HD, a.defer);
         // splits launched: the capacity's, or fewer when the caller knows the
         // live keys stay below a.nsplit * ch (the frame graphs' split buckets;
         // workgroups past the live length exit at once)
@@ -648,14 +658,14 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
             return -1;
         }
         const dim3 grid(a.KV, nsplit, a.nrows);
-        const int lpk = attn_lpk(a.HD);
+        const int lpk = attn_lpk(a.HD, a.defer);
 #define QTTS_AD(H, L)                                                                                      \
         if (a.HD == H && lpk == L) {                                                                       \
             hipLaunchKernelGGL((k_attn_dec<H, 2, L>), grid, dim3(256), 0, st, a);                         \
             qtts_last_kernel = "k_attn_dec<" #H ", 2, " #L ">";                                            \
             return hipGetLastError() == hipSuccess ? 0 : -1;                                               \
         }
-        QTTS_AD(128, 4) QTTS_AD(64, 2) QTTS_AD(32, 1) QTTS_AD(16, 1)
+        QTTS_AD(128, 4) QTTS_AD(128, 8) QTTS_AD(128, 16) QTTS_AD(64, 2) QTTS_AD(32, 1) QTTS_AD(16, 1)
 #undef QTTS_AD
         return -1;
         return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -48,10 +48,12 @@ __device__ __forceinline__ float dot8w(const v4u &w, const float *x) {
 // partials (GemvArgs::amerge, AttnArgs::defer) -- the merge the attention's
 // last split would do (k_attn.hip), in the same order and arithmetic:
 // M = max_s m_s, f_s = expf(m_s - M), x = (sum_s f_s acc_s) / (sum_s f_s l_s).
-constexpr int AM_MS = 4;   // splits whose partials are loaded before the weights
+// (AM_MS: splits whose partials are loaded before the weights, >= the live
+// splits of the common case; more come after them, serially)
 // Dynamic LDS: [xs: C floats][red: 4 floats] (16-B aligned, Guideline 17).
-template <int RW, int NV, bool NT, bool AM = false>
+template <int RW, int NV, bool NT, int AM_MS = 0>
 __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
+    constexpr bool AM = AM_MS > 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int C = 512 * NV, XQ = C / 1024 > 0 ? (C + 1023) / 1024 : 1;   // float4 of x per thread
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -81,8 +83,8 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     // AM: the first AM_MS splits' partials of every unit (their addresses need
     // no live length: slots past it hold stale values, masked below), and the
     // position, all in one round trip
-    float4 am_a[AM ? XQ : 1][AM_MS];
-    float am_m[AM ? XQ : 1][AM_MS], am_l[AM ? XQ : 1][AM_MS];
+    float4 am_a[AM ? XQ : 1][AM ? AM_MS : 1];
+    float am_m[AM ? XQ : 1][AM ? AM_MS : 1], am_l[AM ? XQ : 1][AM ? AM_MS : 1];
     int am_p = 0;
     if constexpr (AM) {
         am_p = a.am_pos[0];
@@ -262,13 +264,14 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
         }
         const dim3 grid(a.R / (4 * (a.R / 1024)));
         const size_t smem = (size_t)(a.C + 4) * sizeof(float);
-        if (a.R == 2048) {
-            hipLaunchKernelGGL((k_gemvw<2, 4, true, true>), grid, dim3(256), smem, st, a);
-            qtts_last_kernel = "k_gemvw<2, 4, true, true>";
-        } else {
-            hipLaunchKernelGGL((k_gemvw<1, 4, true, true>), grid, dim3(256), smem, st, a);
-            qtts_last_kernel = "k_gemvw<1, 4, true, true>";
-        }
+        // partials of up to 4 / 8 splits ahead of the weights: the capacity's
+        // splits when they fit (fixed-length decodes), else 8 and the rest after
+#define QTTS_GWA(RW_, MS_)                                                                             \
+        { hipLaunchKernelGGL((k_gemvw<RW_, 4, true, MS_>), grid, dim3(256), smem, st, a);              \
+          qtts_last_kernel = "k_gemvw<" #RW_ ", 4, true, " #MS_ ">"; }
+        if (a.R == 2048) { if (a.am_nsplit <= 4) QTTS_GWA(2, 4) else if (a.am_nsplit <= 6) QTTS_GWA(2, 6) else QTTS_GWA(2, 8) }
+        else { if (a.am_nsplit <= 4) QTTS_GWA(1, 4) else if (a.am_nsplit <= 6) QTTS_GWA(1, 6) else QTTS_GWA(1, 8) }
+#undef QTTS_GWA
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (a.nb != 1 || a.C % 512 || a.R % 1024 || a.ypart) return 1;

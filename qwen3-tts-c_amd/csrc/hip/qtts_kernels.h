@@ -115,7 +115,8 @@ struct AttnArgs {
     // prologue) instead of the last split's
     int defer = 0;
 };
-int qtts_attn_keys_per_split(int HD);
+// keys per split of the talker decode attention (deferred merge or not)
+int qtts_attn_keys_per_split(int HD, bool defer);
 // true when the decode attention takes these arguments on its split kernel,
 // whose merge AttnArgs::defer hands to the consumer
 bool qtts_attn_defer_ok(const AttnArgs &a);

@@ -576,7 +576,9 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(pinv, float, dv->pinv_cap);
     {
         const int gph = d.NH / d.KV;
-        dv->att_nsplit = (dv->S + qtts_attn_keys_per_split(d.HD) - 1) / qtts_attn_keys_per_split(d.HD);
+        // partial slots for the smaller split size of the two launch forms
+        const int ch = std::min(qtts_attn_keys_per_split(d.HD, false), qtts_attn_keys_per_split(d.HD, true));
+        dv->att_nsplit = (dv->S + ch - 1) / ch;
         A(att_part, float, B * d.KV * dv->att_nsplit * (gph * d.HD + 2 * gph));
         const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
         A(att_cnt, int, B * kvmax);
@@ -857,7 +859,7 @@ static int talker_layers(qtts_dev *dv) {
         GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
         if (defer) {
             o.amerge = dv->att_part; o.am_pos = dv->kv_len; o.am_nsplit = dv->att_nsplit;
-            o.am_ch = qtts_attn_keys_per_split(d.HD); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
+            o.am_ch = qtts_attn_keys_per_split(d.HD, true); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
         }
         const bool opend = kzo && split_out(dv, o, dv->bpo, kzo);
         CKI(pgemv(dv, o, PK_GEMV_TALKER));
