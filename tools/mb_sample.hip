@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void k_phase(SampArgs a, float *sink) {
         return;
     }
     uint32_t rng = 0x42280000u;
-    const int t = sample_fast_regs<EM>(fs, v, E, n, a.top_k, rng);
+    const uint64_t etab = kExp2fTab[tid & 31];
+    const int t = sample_fast_regs<EM>(fs, v, E, n, a.top_k, rng, etab);
     if (tid == 0) sink[0] = (float)t;
 }
 
