@@ -19,10 +19,13 @@
 // Sequential sums run on one lane in the reference's order; expf is the
 // glibc-exact replica (qtts_common.h); divisions are correctly rounded.
 //
-// Fast path: each thread keeps its ids in registers; top-k is an MSB radix
-// select over order-preserving u32 keys (per-wave 256-bin LDS histograms, one
-// barrier per pass, early exit), then an exact rank of the k selected (value
-// desc, index asc).  Full path: bitonic sort in LDS.
+// Fast path: each thread keeps its ids in registers.  For k <= 64 (the
+// default 50) one histogram of the key distance from the maximum bounds a
+// candidate set of <= 64 keys that one wave ranks exactly (sample_dist, three
+// barriers); otherwise, or when the candidates overflow, top-k is an MSB
+// radix select over order-preserving u32 keys (per-wave 256-bin LDS
+// histograms, one barrier per pass, early exit), then an exact rank of the k
+// selected (value desc, index asc).  Full path: bitonic sort in LDS.
 #pragma once
 #include <float.h>
 #include "qtts_common.h"
@@ -169,6 +172,7 @@ __device__ __forceinline__ int sample_any(SampSmem &sm, int n, int k, float top_
 // contiguous ids [t*E, t*E + E), E = ceil(n / 256) <= EMAX.
 constexpr int EMAX = NMAX / 256;
 constexpr int KFAST = 1024;   // register path for top_k <= KFAST (the LDS rank buffers are sized by it)
+constexpr int KC = 64;        // candidate cap of the distance-binned path (one wave ranks them)
 
 struct FastSmem {
     int hist[2][4][256];   // per-wave radix histograms, double-buffered by pass
@@ -178,6 +182,14 @@ struct FastSmem {
     float top_v[KFAST];
     int top_i[KFAST];
     int misc[4];
+    // distance-binned path (sample_dist)
+    unsigned long long cand[4][KC];   // per-wave candidate keys (value key << 32 | ~index)
+    unsigned long long rk[KC];        // wave 0: the candidates, one per lane
+    float pv[KC];                     // p in rank order
+    int pi[KC];                       // ids in rank order
+    float red[4];
+    int redn[4];
+    int ncw[4];
 };
 
 // k-th largest eligible key (value desc): 8-bit MSB radix select over
@@ -331,7 +343,146 @@ __device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rn
     return 0;
 }
 
-// Returns the sampled id (all threads).  v[]: logits / temperature.
+// Bin of the key distance d = Kmax - key from the largest eligible key:
+// exact below 32, then 16 bins per octave (the 4 bits under the leading one).
+// Monotone in d, so the bins ascend from the largest value down; 0..463.
+// (8 bins per octave left > KC keys through the k-th key's bin in ~10 % of
+// standard-normal logit rows at k 50; 16 in < 1 %.)
+constexpr int DBINS = 512;
+__device__ __forceinline__ int dist_bin(uint32_t d) {
+    if (d < 32u) return (int)d;
+    const int e = 31 - __builtin_clz(d);
+    return 32 + ((e - 5) << 4) + (int)((d >> (e - 4)) & 15u);
+}
+// okey's inverse (a -0 comes back as +0, which no comparison or difference
+// below tells apart)
+__device__ __forceinline__ float key_val(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// Top-k draw for k <= KC in three barriers, the common case (top-k 50 over
+// 2048 / 3072 logits).  (1) the block max M and the eligible count;
+// (2) one histogram of dist_bin(okey(M) - key): the first bin B at which the
+// running count reaches k bounds a candidate set -- every key in a bin <= B
+// -- that holds the top k; (3) each wave compacts its candidates into LDS.
+// Wave 0 then ranks the <= KC candidates by (value desc, index asc) -- the
+// order the reference's strict '>' insertion list leaves (K.c:436-449) --
+// with p_j = expf(v_j - M) computed beside the rank (M is the list's head,
+// K.c:452), sums the first k in rank order sequentially (K.c:456-463), lane j
+// keeping the running sum through j, and draws the first j whose running sum
+// reaches r = u * sum (K.c:466-474) by a ballot: the same sums, so the same
+// id.  Returns the id in wave 0 (the other waves return 0), or -1 in every
+// thread when more than KC keys share the bins through B (ties, a very dense
+// boundary bin): the caller then runs the radix select after a barrier.
+template <int EM>
+__device__ __forceinline__ int sample_dist(FastSmem &fs, const float (&v)[EM], const uint32_t (&kk)[EM], int E, int k,
+                                           uint32_t &rng, uint64_t etab) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float m = -INFINITY;
+    int ne = 0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j)
+        if (kk[j] != 0u) { m = fmaxf(m, v[j]); ++ne; }
+    m = wave_max(m);
+    ne = __builtin_amdgcn_readlane(wave_incl_scan(ne), 63);
+    int (*dh)[DBINS] = reinterpret_cast<int (*)[DBINS]>(&fs.hist[0][0][0]);   // [wave][bin]
+#pragma unroll
+    for (int i = 0; i < DBINS / 64; ++i) dh[w][lane + 64 * i] = 0;
+    if (lane == 0) { fs.red[w] = m; fs.redn[w] = ne; }
+    __syncthreads();
+    const float M = fmaxf(fmaxf(fs.red[0], fs.red[1]), fmaxf(fs.red[2], fs.red[3]));
+    const int ne_all = fs.redn[0] + fs.redn[1] + fs.redn[2] + fs.redn[3];
+    if (k > ne_all) k = ne_all;
+    if (k == 0) return 0;                     // nothing eligible: the reference returns 0
+    const uint32_t Kmax = okey(M);
+    int bb[EM];
+    int *h = dh[w];
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        bb[j] = DBINS;
+        if (kk[j] != 0u) { bb[j] = dist_bin(Kmax - kk[j]); atomicAdd(&h[bb[j]], 1); }
+    }
+    __syncthreads();
+    // merged histogram, nearest bins first: lane covers bins 8 lane .. 8 lane + 7
+    constexpr int BL = DBINS / 64;
+    int c[BL], tot = 0;
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+        const int bin = BL * lane + i;
+        c[i] = dh[0][bin] + dh[1][bin] + dh[2][bin] + dh[3][bin];
+        tot += c[i];
+    }
+    const int inc = wave_incl_scan(tot), exc = inc - tot;
+    int B = -1, nc = 0;
+    if (exc < k && inc >= k) {
+        int cum = exc;
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            cum += c[i];
+            if (B < 0 && cum >= k) { B = BL * lane + i; nc = cum; }
+        }
+    }
+    const unsigned long long hit = __ballot(B >= 0);   // non-empty: k <= ne_all
+    const int src = __ffsll((long long)hit) - 1;
+    B = __builtin_amdgcn_readlane(B, src);
+    nc = __builtin_amdgcn_readlane(nc, src);
+    if (nc > KC) return -1;
+    int mine = 0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j) mine += bb[j] <= B;
+    const int wi = wave_incl_scan(mine);
+    int pos = wi - mine;
+#pragma unroll
+    for (int j = 0; j < EM; ++j)
+        if (bb[j] <= B) {
+            fs.cand[w][pos] = ((unsigned long long)kk[j] << 32) | (0xFFFFFFFFu - (uint32_t)(tid * E + j));
+            ++pos;
+        }
+    if (lane == 63) fs.ncw[w] = wi;
+    __syncthreads();
+    if (w != 0) return 0;
+    // wave 0: lane l takes candidate l of the concatenated per-wave lists
+    const int n0 = fs.ncw[0], n1 = fs.ncw[1], n2 = fs.ncw[2];
+    int ww = 0, off = lane;
+    if (off >= n0) { off -= n0; ww = 1; if (off >= n1) { off -= n1; ww = 2; if (off >= n2) { off -= n2; ww = 3; } } }
+    if (lane >= nc) { ww = 0; off = 0; }
+    const unsigned long long key = lane < nc ? fs.cand[ww][off] : 0ull;   // 0: below every real key
+    fs.rk[lane] = key;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: LDS is in order once the writes landed
+    const float e = expf_glibc_wave(lane < nc ? key_val((uint32_t)(key >> 32)) - M : 0.f, etab);
+    int rank = 0;
+    for (int t0 = 0; t0 < nc; t0 += 8) {
+        unsigned long long kt[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kt[u] = fs.rk[t0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += kt[u] > key;
+    }
+    if (lane < nc && rank < k) { fs.pv[rank] = e; fs.pi[rank] = (int)(0xFFFFFFFFu - (uint32_t)key); }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float sum = 0.f, cj = 0.f;
+    for (int j0 = 0; j0 < k; j0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p[u] = fs.pv[j0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (j0 + u < k) {
+                sum += p[u];
+                if (lane == j0 + u) cj = sum;
+            }
+    }
+    if (!(sum > 0.0f)) return fs.pi[0];
+    float r = 0.f;
+    if (lane == 0) r = rand_uniform(rng) * sum;
+    r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 0));
+    const unsigned long long hit2 = __ballot(lane < k && cj >= r);
+    return hit2 ? fs.pi[__ffsll((long long)hit2) - 1] : 0;
+}
+
+// Returns the sampled id: in wave 0 (the callers that need it in every wave
+// broadcast it).  v[]: logits / temperature.
 template <int EM>
 __device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[EM], int E, int n, int k, uint32_t &rng,
                                                 uint64_t etab) {
@@ -340,6 +491,11 @@ __device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[E
     uint32_t kk[EM];
 #pragma unroll
     for (int j = 0; j < EM; ++j) kk[j] = (j < E && tid * E + j < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
+    if (k <= KC) {
+        const int t = sample_dist<EM>(fs, v, kk, E, k, rng, etab);
+        if (t != -1) return t;
+        __syncthreads();   // the radix select below rewrites the histograms the other waves read
+    }
     uint32_t T, Tm;
     int take_eq, ne;
     radix_select_regs<EM>(fs, kk, E, k, T, Tm, take_eq, ne);
@@ -434,14 +590,12 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
 #pragma clang fp contract(off)
     KSmem &U = *reinterpret_cast<KSmem *>(smraw);
     const int tid = threadIdx.x, n = a.n;
-    // every global read of this kernel is issued up front (one round trip)
-    int stopped = 0, ng = 0;
+    // every global read of this kernel is issued up front (one round trip);
+    // the row's flags are uniform loads in every thread (no LDS broadcast)
+    const int stopped = a.stopped ? a.stopped[b] : 0;
+    const int ng = a.mode == 1 ? a.n_gen[b] : 0;
     uint32_t rng = 0;
-    if (tid == 0) {
-        stopped = a.stopped ? a.stopped[b] : 0;
-        rng = a.mode == 1 ? a.rng[b] : a.st_rng[b];
-        if (a.mode == 1) ng = a.n_gen[b];
-    }
+    if (tid == 0) rng = a.mode == 1 ? a.rng[b] : a.st_rng[b];
     const int E = (n + 255) / 256;
     const float *lg = a.logits + (size_t)b * a.ld;
     const int i0 = tid * E;
@@ -456,11 +610,7 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
         cnt[j] = (ok && pen) ? a.counts[(size_t)b * n + i] : 0;
     }
     const uint64_t etab = kExp2fTab[tid & 31];   // expf_glibc_wave's table, with the first loads
-    if (tid == 0) { U.fast.misc[1] = stopped; U.fast.misc[2] = ng; }
-    __syncthreads();
-    if (U.fast.misc[1]) return;
-    ng = U.fast.misc[2];
-    __syncthreads();
+    if (stopped) return;
     if (a.mode == 1) {
 #pragma unroll
         for (int j = 0; j < EM; ++j) {
@@ -479,12 +629,17 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
         float v[EM];
 #pragma unroll
         for (int j = 0; j < EM; ++j) v[j] = div_rn(x[j], temp);
-        tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
-        if (a.mode == 1 && a.fixed > 0 && tok == a.eos && ng < a.fixed) {   // Q.c:1315-1321
+        tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);   // (wave 0's)
+        if (a.mode == 1 && a.fixed > 0 && ng < a.fixed) {   // Q.c:1315-1321: an EOS draw is redrawn
+            if (tid == 0) U.fast.misc[3] = tok;
+            __syncthreads();
+            tok = U.fast.misc[3];
+            if (tok == a.eos) {
 #pragma unroll
-            for (int j = 0; j < EM; ++j)
-                if (i0 + j == a.eos) v[j] = div_rn(-1e9f, temp);
-            tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
+                for (int j = 0; j < EM; ++j)
+                    if (i0 + j == a.eos) v[j] = div_rn(-1e9f, temp);
+                tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
+            }
         }
     } else if constexpr (!FAST_ONLY) {
         SampSmem &sm = U.full;

@@ -199,6 +199,45 @@ def test_sampler_random_vs_oracle(gpu, oracle):
             assert st[b] == s.view(np.uint32)[0], (it, b)
 
 
+def test_sampler_candidate_bins_vs_oracle(gpu, oracle):
+    """The k <= 64 distance-binned path (qtts_sample_dev.h sample_dist) and
+    its radix fallback: boundary bins dense with ties (more than 64
+    candidates), every logit equal, +0 / -0 mixtures, ineligible -FLT_MAX
+    entries, values spanning zero, k at the 64 cap and one past it, narrow
+    and wide logit scales; ids and RNG state bit-exact."""
+    rng = np.random.default_rng(7)
+    fmax = np.finfo(np.float32).max
+    cases = []
+    for it in range(48):
+        V = [2048, 3072, 4096, 1500, 100][it % 5]
+        lg = (rng.standard_normal(V) * [0.01, 0.3, 3.0, 40.0][it % 4]).astype(np.float32)
+        kind = it % 8
+        if kind == 1:    # ties straddling the k-th key (fallback: > 64 candidates)
+            srt = np.sort(lg)[::-1]
+            lg[rng.integers(0, V, 80)] = srt[45]
+        elif kind == 2:  # every logit equal
+            lg[:] = np.float32(rng.standard_normal())
+        elif kind == 3:  # +0 / -0 and values around zero
+            lg[rng.integers(0, V, V // 2)] = 0.0
+            lg[rng.integers(0, V, V // 4)] = -0.0
+        elif kind == 4:  # ineligible entries (v <= -FLT_MAX after / T)
+            lg[rng.integers(0, V, V - 20)] = -fmax
+        elif kind == 5:  # a sharp head and a long tail
+            lg[rng.integers(0, V, 5)] += 30.0
+        elif kind == 6:  # many copies of the maximum
+            lg[rng.integers(0, V, 70)] = lg.max()
+        k = int([50, 64, 65, 1, 63, 2, 50, 50][(it // 8 + it) % 8])
+        temp = float([0.9, 1.0, 0.5, 1.7][it % 4])
+        cases.append((lg, V, k, temp))
+    for it, (lg, V, k, temp) in enumerate(cases):
+        st0 = np.array([float(rng.integers(1, 10**6))], np.float32)
+        r, st = sample_gpu(gpu, lg[None, :], V, k, 1.0, temp, st0.view(np.uint32))
+        s = st0.copy()
+        e = oracle.lib.orc_sample(fptr(lg.copy()), V, k, 1.0, temp, fptr(s))
+        assert r[0] == e, (it, r[0], e)
+        assert st[0] == s.view(np.uint32)[0], it
+
+
 @pytest.mark.parametrize("i", range(5))
 def test_causal_conv1d_golden(gpu, i):
     import torch
