@@ -374,7 +374,8 @@ __device__ __forceinline__ float key_val(uint32_t k) {
 // id.  Returns the id in wave 0 (the other waves return 0), or -1 in every
 // thread when more than KC keys share the bins through B (ties, a very dense
 // boundary bin): the caller then runs the radix select after a barrier.
-template <int EM>
+// (STOP < 4: the micro-benchmark's phase cut, tools/mb_sample.hip)
+template <int EM, int STOP = 4>
 __device__ __forceinline__ int sample_dist(FastSmem &fs, const float (&v)[EM], const uint32_t (&kk)[EM], int E, int k,
                                            uint32_t &rng, uint64_t etab) {
 #pragma clang fp contract(off)
@@ -395,6 +396,7 @@ __device__ __forceinline__ int sample_dist(FastSmem &fs, const float (&v)[EM], c
     const int ne_all = fs.redn[0] + fs.redn[1] + fs.redn[2] + fs.redn[3];
     if (k > ne_all) k = ne_all;
     if (k == 0) return 0;                     // nothing eligible: the reference returns 0
+    if constexpr (STOP == 1) return (int)M;
     const uint32_t Kmax = okey(M);
     int bb[EM];
     int *h = dh[w];
@@ -423,6 +425,7 @@ __device__ __forceinline__ int sample_dist(FastSmem &fs, const float (&v)[EM], c
             if (B < 0 && cum >= k) { B = BL * lane + i; nc = cum; }
         }
     }
+    if constexpr (STOP == 2) return tot;
     const unsigned long long hit = __ballot(B >= 0);   // non-empty: k <= ne_all
     const int src = __ffsll((long long)hit) - 1;
     B = __builtin_amdgcn_readlane(B, src);
@@ -442,6 +445,7 @@ __device__ __forceinline__ int sample_dist(FastSmem &fs, const float (&v)[EM], c
     if (lane == 63) fs.ncw[w] = wi;
     __syncthreads();
     if (w != 0) return 0;
+    if constexpr (STOP == 3) return fs.ncw[0];
     // wave 0: lane l takes candidate l of the concatenated per-wave lists
     const int n0 = fs.ncw[0], n1 = fs.ncw[1], n2 = fs.ncw[2];
     int ww = 0, off = lane;

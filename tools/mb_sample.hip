@@ -6,6 +6,11 @@
 //   1 logits loaded            (+ a store of their sum)
 //   2 + radix select           (k-th largest key)
 //   3 + selection, rank, draw  (= the full fast path, qtts_sample_dev.h)
+// and the distance-binned path (sample_dist, k <= 64) cut after its phases:
+//   11 + max / eligible count (barrier 1)
+//   12 + distance histogram (barrier 2), merged-histogram scan
+//   13 + candidate compaction (barrier 3)
+//   14 = the whole draw (wave 0 ranks, sums, draws)
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iqwen3-tts-c_amd/csrc/hip tools/mb_sample.hip -o tools/mb_sample
 #include "qtts_sample_dev.h"
@@ -46,6 +51,14 @@ __global__ __launch_bounds__(256) void k_phase(SampArgs a, float *sink) {
     }
     uint32_t rng = 0x42280000u;
     const uint64_t etab = kExp2fTab[tid & 31];
+    if constexpr (PHASE > 10) {
+        uint32_t kk[EM];
+#pragma unroll
+        for (int j = 0; j < EM; ++j) kk[j] = (j < E && tid * E + j < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
+        const int t = sample_dist<EM, PHASE - 10>(fs, v, kk, E, a.top_k, rng, etab);
+        if (tid == 0) sink[0] = (float)t;
+        return;
+    }
     const int t = sample_fast_regs<EM>(fs, v, E, n, a.top_k, rng, etab);
     if (tid == 0) sink[0] = (float)t;
 }
@@ -95,5 +108,9 @@ int main() {
     printf("phase 1 + logits loaded     %6.2f us\n", time_phase<1>(a, sink, st));
     printf("phase 2 + radix select      %6.2f us\n", time_phase<2>(a, sink, st));
     printf("phase 3 + select/rank/draw  %6.2f us\n", time_phase<3>(a, sink, st));
+    printf("dist 11 + max / count       %6.2f us\n", time_phase<11>(a, sink, st));
+    printf("dist 12 + histogram, scan   %6.2f us\n", time_phase<12>(a, sink, st));
+    printf("dist 13 + compaction        %6.2f us\n", time_phase<13>(a, sink, st));
+    printf("dist 14 = whole draw        %6.2f us\n", time_phase<14>(a, sink, st));
     return 0;
 }
