@@ -57,15 +57,30 @@ __device__ __forceinline__ unsigned gb_row_id(const GemvArgs &a, int b) {
 // split-K partials added to x (0, 2 or 4; n_xadd <= PM); SRC: x source kind
 // (the kernel is specialised on it: a branch between loads of different kinds
 // makes the compiler wait for every outstanding load at the join).
+// diagnostic phase stamps (GemvArgs::dbg, QTTS_HIP_GM_DBG; compiled in only
+// with `make EXTRA=-DQTTS_STAMPS`: the stores cost registers): 100 MHz wall
+// clock, one lane
+__device__ __forceinline__ void gb_stamp(const GemvArgs &a, int k) {
+#ifdef QTTS_STAMPS
+    if (a.dbg && threadIdx.x == 0) a.dbg[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
 template <int SPW, int TPW, int NBC, int PM, int SRC>
 __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
+    gb_stamp(a, 0);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int SC = 32 * SPW;                 // columns of a wave's slice
     constexpr int U4 = SC / 4;                   // float4 units per slice row (8 SPW, divides 64)
     constexpr int XQ = SPW * NBC / 8;            // x units per lane
     constexpr int RPQ = 64 / U4;                 // slice rows per unit index q
     constexpr int LDX = SC + 4;                  // staged row stride (floats; +4: fragment reads spread over banks)
-    constexpr int SA = (SPW + 1) / 2;            // steps whose weights go before the staging
+    // steps whose weights go before the staging (the rest reuse the partials'
+    // registers).  Issuing every step before the staging where the registers
+    // allow measured slower at batch 8 (139.8 / 140.2 vs 142.3 / 142.0
+    // audio-s/s, same box) although the stamps show q|k|v's last wave
+    // finishing 3.5 us after its first (profiles/r03i_batch8_gemvb_stamps.txt)
+    constexpr int SA = (SPW + 1) / 2;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
     const int nb = a.nb;
     const int kz = gridDim.y, Ck = a.C / kz, woff = blockIdx.y * Ck;
@@ -179,6 +194,7 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
         for (int t = 0; t < TPW; ++t)
             wv[t][j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rw, wo[t] + 64u * j, 0, 0));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave writes and reads its rows: LDS is in order
+    gb_stamp(a, 1);
 
     // ---- 3. per step: A fragments (three exact planes) x each tile's weight fragment
     const int tb = lane & 15, kq = 8 * (lane >> 4);
@@ -203,6 +219,7 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
 #pragma unroll
         for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h3, __builtin_bit_cast(bf16x8, wv[t][j]), acc[t], 0, 0, 0);
     }
+    gb_stamp(a, 2);
     // the wave's partial tiles over its own (dead) x rows
     floatx4 *red = reinterpret_cast<floatx4 *>(xs);
 #pragma unroll
@@ -210,6 +227,7 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
 
     // ---- 4. one barrier; tile t: the W partial tiles in wave order, inv, epilogue
     __syncthreads();
+    gb_stamp(a, 3);
     if (copier && norm && a.xcopy_normed) {   // the normalised copy: (x * nw) * inv[b]
 #pragma unroll
         for (int q = 0; q < XQ; ++q) {
@@ -264,6 +282,7 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
         }
         epilogue(a, bb, r, val, up);
     }
+    gb_stamp(a, 4);
 }
 
 }  // namespace

@@ -61,6 +61,7 @@ struct GemvArgs {
     int ldy = 0;
     const float *bias = nullptr;
     int epi = EPI_STORE;
+    unsigned long long *dbg = nullptr;   // diagnostics (k_gemvb): [workgroup][8] phase stamps, 100 MHz clock
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {
         if (xadd && (((uintptr_t)xadd & 15) || ld_xadd % 4 || n_xadd < 1)) return false;

@@ -161,6 +161,10 @@ struct qtts_dev {
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
     bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
+    // QTTS_HIP_GM_DBG=<layer>: phase stamps of that talker layer's batch GEMVs
+    // (q|k|v, O, gate|up, down), printed by qtts_dev_get_codes
+    int gm_dbg_layer = -1;
+    unsigned long long *gm_dbg = nullptr;
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
     int pinv_cap = 0;
 
@@ -375,6 +379,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_defer = !(ad && !atoi(ad));
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
+    const char *gd = getenv("QTTS_HIP_GM_DBG");
+    if (gd) dv->gm_dbg_layer = atoi(gd);
     codec_init(&dv->codec, dims, dv->st);
     dv->enc.st = dv->st;
     dv->enc.device = device;
@@ -585,6 +591,10 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
         A(btick, int, QTTS_GM_TICKS);
         CK(hipMemsetAsync(dv->btick, 0, QTTS_GM_TICKS * sizeof(int), dv->st));
+        if (dv->gm_dbg_layer >= 0) {
+            A(gm_dbg, unsigned long long, 4 * 2048 * 8);
+            CK(hipMemsetAsync(dv->gm_dbg, 0, 4 * 2048 * 8 * 8, dv->st));
+        }
     }
 #undef A
     dv->p_len_h.assign(nb, 0);
@@ -854,9 +864,12 @@ static int talker_layers(qtts_dev *dv) {
         // prologue (one dependent hand-off fewer per layer)
         const bool defer = dv->attn_defer && nb == 1 && qtts_attn_defer_ok(t) && qtts_gemvw_amerge_ok(d.H, AD);
         t.defer = defer;
+        const bool dbg = dv->gm_dbg && l == dv->gm_dbg_layer;
+        if (dbg) a.dbg = dv->gm_dbg;
         CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
         if (pend) { std::swap(xa, xb); pend = nullptr; }
         GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
+        if (dbg) o.dbg = dv->gm_dbg + 2048 * 8;
         if (defer) {
             o.amerge = dv->att_part; o.am_pos = dv->kv_len; o.am_nsplit = dv->att_nsplit;
             o.am_ch = qtts_attn_keys_per_split(d.HD, true); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
@@ -865,10 +878,12 @@ static int talker_layers(qtts_dev *dv) {
         CKI(pgemv(dv, o, PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
+        if (dbg) a.dbg = dv->gm_dbg + 2 * 2048 * 8;
         if (opend) add_in(a, dv->bpo, kzo, d.H, nb, xb);
         CKI(pgemv(dv, a, PK_GEMV_TALKER));
         if (opend) std::swap(xa, xb);
         GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
+        if (dbg) dn.dbg = dv->gm_dbg + 3 * 2048 * 8;
         if (kzd && split_out(dv, dn, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
         CKI(pgemv(dv, dn, PK_GEMV_TALKER));
     }
@@ -1305,6 +1320,26 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
     int n = 0;
     CK(hipMemcpyAsync(&n, dv->n_gen + b, 4, hipMemcpyDeviceToHost, dv->st));
     CK(hipStreamSynchronize(dv->st));
+    if (dv->gm_dbg) {   // QTTS_HIP_GM_DBG: phase spans of the chosen talker layer's GEMVs, last frame
+        std::vector<unsigned long long> h(4 * 2048 * 8);
+        CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+        static const char *op[4] = {"q|k|v", "O", "gate|up", "down"};
+        static const char *ph[5] = {"start", "x staged", "mfma done", "barrier", "end (wg 0)"};
+        for (int g = 0; g < 4; ++g) {
+            const unsigned long long *b = h.data() + (size_t)g * 2048 * 8;
+            unsigned long long t0 = ~0ull;
+            for (int i = 0; i < 2048; ++i) if (b[i * 8] && b[i * 8] < t0) t0 = b[i * 8];
+            for (int k = 0; k < 5; ++k) {
+                std::vector<double> v;
+                for (int i = 0; i < 2048; ++i) if (b[i * 8 + k]) v.push_back((b[i * 8 + k] - t0) * 0.01);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                fprintf(stderr, "[gm_dbg] %-8s %-10s n %4zu  min %6.2f  med %6.2f  max %6.2f us\n", op[g], ph[k], v.size(),
+                        v[0], v[v.size() / 2], v.back());
+            }
+        }
+        hipMemsetAsync(dv->gm_dbg, 0, h.size() * 8, dv->st);
+    }
     if (n > max_frames) n = max_frames;
     CK(hipMemcpyAsync(host_codes, dv->codes + (size_t)b * (dv->max_frames + 1) * dv->d.G, (size_t)n * dv->d.G * 4,
                       hipMemcpyDeviceToHost, dv->st));
