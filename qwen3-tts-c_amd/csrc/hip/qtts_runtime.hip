@@ -844,6 +844,8 @@ static int talker_layers(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     const int nb = dv->nrun, NBA = dv->nb, QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
     hipStream_t st = dv->st;
+    // (the talker's O without split-K at batch 8: 142.0 / 142.6 vs 140.7 / 142.1
+    // audio-s/s, within noise; its down without: 135.9 / 135.6, gpurun_out/tkz)
     const int kzo = bsplit_kz(dv, d.H, AD), kzd = bsplit_kz(dv, d.H, d.I);
     float *xa = dv->x_tk, *xb = dv->x_tk2;
     const float *pend = nullptr;
