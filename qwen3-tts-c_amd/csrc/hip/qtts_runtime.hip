@@ -829,9 +829,9 @@ static int bsplit_kz(const qtts_dev *dv, int R, int C) {
 // again after the loads of both sides were unserialised (gpurun_out ab5, same
 // box): self-reducing at every batch size gave batch 2 38.7 vs 42.6, 4 70.5
 // vs 76.0, 8 123.6 vs 126.3, 16 193.3 vs 189.0.
-static bool split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz) {
+static bool split_out(qtts_dev *dv, GemvArgs &g, float *part, int kz, int self_min = 0) {
     g.ypart = part; g.kz = kz; g.ld_ypart = (size_t)dv->nrun * g.R;
-    if (dv->nrun >= dv->bself_min) { g.tick = dv->btick; return false; }
+    if (dv->nrun >= (self_min > 0 ? self_min : dv->bself_min)) { g.tick = dv->btick; return false; }
     g.y = nullptr;
     return true;
 }
@@ -876,7 +876,13 @@ static int talker_layers(qtts_dev *dv) {
             o.amerge = dv->att_part; o.am_pos = dv->kv_len; o.am_nsplit = dv->att_nsplit;
             o.am_ch = qtts_attn_keys_per_split(d.HD, true); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
         }
-        const bool opend = kzo && split_out(dv, o, dv->bpo, kzo);
+        // the talker's O / down reduce their own partials at every batch size:
+        // its q|k|v and gate|up prologues (2048-wide x rows) then read x alone
+        // (batch 8: 141.1 / 143.1 vs 138.9 / 141.2 audio-s/s adding the partials
+        // there, same box, gpurun_out/bstk; the sub-talker keeps the consumer
+        // add up to 8 rows, where self-reduction measured slower)
+        const int tk_self = 2;
+        const bool opend = kzo && split_out(dv, o, dv->bpo, kzo, tk_self);
         CKI(pgemv(dv, o, PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
@@ -886,7 +892,7 @@ static int talker_layers(qtts_dev *dv) {
         if (opend) std::swap(xa, xb);
         GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
         if (dbg) dn.dbg = dv->gm_dbg + 3 * 2048 * 8;
-        if (kzd && split_out(dv, dn, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
+        if (kzd && split_out(dv, dn, dv->bpd, kzd, tk_self)) { pend = dv->bpd; npend = kzd; }
         CKI(pgemv(dv, dn, PK_GEMV_TALKER));
     }
     dv->tk_xfin = xa; dv->tk_pend = pend; dv->tk_npend = npend;
