@@ -51,8 +51,17 @@ __device__ __forceinline__ float dot8w(const v4u &w, const float *x) {
 // (AM_MS: splits whose partials are loaded before the weights, >= the live
 // splits of the common case; more come after them, serially)
 // Dynamic LDS: [xs: C floats][red: 4 floats] (16-B aligned, Guideline 17).
+// diagnostic phase stamps (GemvArgs::dbg, QTTS_HIP_GM_DBG; compiled in only
+// with `make EXTRA=-DQTTS_STAMPS`): 100 MHz wall clock, one lane per workgroup
+__device__ __forceinline__ void gw_stamp(const GemvArgs &a, int k) {
+#ifdef QTTS_STAMPS
+    if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
 template <int RW, int NV, bool NT, int AM_MS = 0>
 __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
+    gw_stamp(a, 0);
     constexpr bool AM = AM_MS > 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int C = 512 * NV, XQ = C / 1024 > 0 ? (C + 1023) / 1024 : 1;   // float4 of x per thread
@@ -199,6 +208,7 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
         __syncthreads();
         inv = rms_inv(red[0] + red[1] + red[2] + red[3], C, a.eps);
     }
+    gw_stamp(a, 1);
     const bool cp = a.xcopy && blockIdx.x == 0;
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
@@ -225,6 +235,7 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
         for (int k = 0; k < NV; ++k) s += dot8w(wv[i][k], xs + 8 * (lane + 64 * k));
         acc[i] = wave_sum(s);
     }
+    gw_stamp(a, 2);
     if (lane != 0) return;
     float *y = a.y + blockIdx.y * a.ldy_rep;
 #pragma unroll

@@ -981,6 +981,9 @@ static int subtalker(qtts_dev *dv) {
             const bool kv_only = g == 0 && l == d.Ls - 1;
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
+            // QTTS_HIP_GM_DBG at batch 1: stamps of pass 5, layer 2's q|k|v / gate|up / down
+            const bool sdbg = dv->gm_dbg && nb == 1 && g == 5 && l == 2;
+            if (sdbg) a.dbg = dv->gm_dbg;
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
             AttnArgs t;
@@ -1034,6 +1037,7 @@ static int subtalker(qtts_dev *dv) {
             if (kv_only) break;
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
+            if (sdbg) a.dbg = dv->gm_dbg + 2 * 2048 * 8;
             if (tab0) set_src(a);   // the residual is the input table row (x_st was not written)
             if (fused_o) {
                 add_in(a, dv->opart, d.KVs, d.Hs, nb, xb);
@@ -1044,6 +1048,7 @@ static int subtalker(qtts_dev *dv) {
             if (fused_o || opend) std::swap(xa, xb);
             a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xa, d.Hs, nb, EPI_RESID);
             a.nt = 0;
+            if (sdbg) a.dbg = dv->gm_dbg + 3 * 2048 * 8;
             if (kzd && split_out(dv, a, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
         }
@@ -1331,8 +1336,8 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
     if (dv->gm_dbg) {   // QTTS_HIP_GM_DBG: phase spans of the chosen talker layer's GEMVs, last frame
         std::vector<unsigned long long> h(4 * 2048 * 8);
         CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
-        static const char *op[4] = {"q|k|v", "O", "gate|up", "down"};
-        static const char *ph[5] = {"start", "x staged", "mfma done", "barrier", "end (wg 0)"};
+        static const char *op[4] = {"q|k|v", "O / -", "gate|up", "down"};
+        static const char *ph[5] = {"start", "x staged", "dot done", "barrier", "end (wg 0)"};
         for (int g = 0; g < 4; ++g) {
             const unsigned long long *b = h.data() + (size_t)g * 2048 * 8;
             unsigned long long t0 = ~0ull;
