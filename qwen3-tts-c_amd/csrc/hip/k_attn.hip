@@ -617,7 +617,8 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
 // QTTS_HIP_ATTN_LPK (HD 128: 4, 8 or 16 lanes per key = 64-, 32- or 16-key
 // splits) overrides both for split-size A/B runs.
 static int attn_lpk(int HD, bool defer) {
-    static const int env = [] { const char *e = getenv("QTTS_HIP_ATTN_LPK"); return e ? atoi(e) : 0; }();
+    const char *ev = getenv("QTTS_HIP_ATTN_LPK");   // (read per call: tests switch it per model instance)
+    const int env = ev ? atoi(ev) : 0;
     if (HD == 128 && (env == 4 || env == 8 || env == 16)) return env;
     if (HD == 128 && defer) return 8;
     return HD >= 32 ? HD / 32 : 1;

@@ -290,11 +290,10 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
 // Returns 1 when the shape is not covered (the caller uses k_gemvm), 0 ok,
 // -1 launch error.  QTTS_HIP_GEMVB=0 keeps k_gemvm for every shape (A/B).
 int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
-    static const int enabled = [] {
-        const char *e = getenv("QTTS_HIP_GEMVB");
-        return e && !atoi(e) ? 0 : 1;
-    }();
-    if (!enabled) return 1;
+    // (read per call: launches happen at graph capture, and tests switch it
+    // per model instance)
+    const char *ge = getenv("QTTS_HIP_GEMVB");
+    if (ge && !atoi(ge)) return 1;
     const GemvArgs &a = in;
     if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32 || (size_t)a.R * a.C * 2 >= ((size_t)1 << 31)) return 1;
     const bool tab = a.table != nullptr, tabf = !tab && a.table_f32 != nullptr;

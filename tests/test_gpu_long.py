@@ -119,3 +119,23 @@ def test_full_bench_workload_vs_reference(gpu):
         _audio_close(a, g["audio"], "1.7B bench workload waveform")
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("env", [{"QTTS_HIP_ATTN_DEFER": "0"}, {"QTTS_HIP_ATTN_LPK": "4"},
+                                 {"QTTS_HIP_ATTN_LPK": "16"}])
+def test_hd128_attention_switch_paths_vs_reference(gpu, monkeypatch, env):
+    """The talker attention's A/B switches at HD 128, 300 frames (positions
+    to 338: the 1-, 2-8- and > 8-split merges of 64- / 32- / 16-key splits):
+    the merge in the last split instead of the O projection's prologue, and
+    the other split sizes -- codes bit-exact against the reference's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = np.load(os.path.join(GOLDEN, "long_hd128.npz"))
+    man = _man()["hd128"]
+    m = qtts.QwenTTS(model_dir("hd128"))
+    try:
+        m.set_params(max_tokens=4096, fixed=300, seed=man["seed"], **DEFAULT)
+        m.generate(g["prompt_ids"], "aiden", "english")
+        _codes_equal(m.last_codes(), g["decode_codes"][:300], f"hd128 300 frames {env}")
+    finally:
+        m.close()
