@@ -194,14 +194,42 @@ def profile_roofline(m, lib):
                 gemv_ms_per_frame=float(t[(k == 0) | (k == 1)].sum()))
 
 
+def lscpu():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        return {k.strip(): v.strip() for k, v in (l.split(":", 1) for l in out.splitlines() if ":" in l)}
+    except Exception:
+        return {}
+
+
 def physical_cores():
     """Physical cores of this host from lscpu (sockets x cores per socket)."""
     try:
-        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
-        kv = dict(l.split(":", 1) for l in out.splitlines() if ":" in l)
-        return int(kv["Socket(s)"].strip()) * int(kv["Core(s) per socket"].strip())
+        kv = lscpu()
+        return int(kv["Socket(s)"]) * int(kv["Core(s) per socket"])
     except Exception:
         return None
+
+
+def cpu_placement():
+    """What the CPU baseline's threads run on: lscpu's SMT width, the CPUs this
+    process may use, and the OpenMP placement the reference is started with."""
+    kv = lscpu()
+    aff = sorted(os.sched_getaffinity(0))
+    tpc = kv.get("Thread(s) per core")
+    return {"threads_per_core": int(tpc) if tpc and tpc.isdigit() else None,
+            "physical_cores": physical_cores(), "affinity_cpus": len(aff),
+            "affinity": f"{aff[0]}-{aff[-1]}" if aff and aff[-1] - aff[0] + 1 == len(aff) else ",".join(map(str, aff)),
+            "OMP_PLACES": OMP_PLACEMENT["OMP_PLACES"], "OMP_PROC_BIND": OMP_PLACEMENT["OMP_PROC_BIND"]}
+
+
+# one OpenMP thread per physical core, packed (the reference's GEMV threads
+# otherwise float over the share and two can land on one core's SMT pair)
+OMP_PLACEMENT = {"OMP_PLACES": "cores", "OMP_PROC_BIND": "close"}
+# BASELINE.json configs[1]: greedy decode (the reference CLI's flags for it)
+GREEDY_FLAGS = ["--temperature", "1", "--top-k", "1", "--top-p", "1", "--repetition-penalty", "1",
+                "--subtalker-temperature", "1", "--subtalker-top-k", "1", "--subtalker-top-p", "1"]
+GREEDY = dict(temperature=1.0, top_k=1, top_p=1.0, rep=1.0, st_temperature=1.0, st_top_k=1, st_top_p=1.0)
 
 
 def cpu_threads_default():
@@ -218,7 +246,8 @@ def cpu_threads_default():
     return max(1, n)
 
 
-def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128, speaker="aiden", timeout=900):
+def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128, speaker="aiden", timeout=900,
+                 greedy=False):
     """The reference c/ CLI (oracle/_ref/qwen-tts, built unmodified by
     oracle/Makefile) timed as BASELINE.md §2 plans: --benchmark-warmup /
     --benchmark-runs with the [persistent] lines parsed (c/main.c:262-271).
@@ -229,9 +258,11 @@ def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128
     exe = os.path.join(ROOT, "oracle", "_ref", "qwen-tts")
     if not os.path.exists(exe):
         return None
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), **OMP_PLACEMENT)
     cmd = [exe, "-d", md, "-t", ",".join(map(str, ids)), "-s", speaker, "-l", "english", "-o", "/tmp/qtts_cpu.wav",
            "--fixed-codec-tokens", str(frames), "--benchmark-warmup", str(warmup), "--benchmark-runs", str(runs), "-v"]
+    if greedy:
+        cmd += GREEDY_FLAGS
     t = time.time()
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     wall = time.time() - t
@@ -248,10 +279,11 @@ def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128
     ext_ms = fixed_ms + (med["talker_ms"] + med["codec_ms"]) / n * target_frames
     audio_s = target_frames * 0.08
     return dict(value=audio_s / (ext_ms / 1e3), unit="audio-s/s", cores=threads, kind="reference",
-                physical_cores=physical_cores(),
+                physical_cores=physical_cores(), placement=cpu_placement(),
                 runs=runs_,
                 sample=(f"reference c/ (oracle/_ref/qwen-tts: unmodified c/ sources, scalar GEMV + OpenMP, no BLAS in "
-                        f"the image) on the same synthetic model and prompt, {threads} OpenMP threads, "
+                        f"the image) on the same synthetic model and prompt{', greedy' if greedy else ''}, {threads} OpenMP "
+                        f"threads (OMP_PLACES=cores, OMP_PROC_BIND=close), "
                         f"--fixed-codec-tokens {frames} --benchmark-warmup {warmup} --benchmark-runs {runs} "
                         f"([persistent] lines); the {target_frames}-frame workload is extrapolated from the median run: "
                         f"fixed {fixed_ms:.0f} ms (prompt + prefill) + talker {med['talker_ms'] / n:.0f} ms/frame + codec "
@@ -320,6 +352,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--preset", default="1.7b")
     ap.add_argument("--frames", type=int, default=128)
+    ap.add_argument("--greedy", action="store_true",
+                    help="greedy decode (top-k 1, temperature 1, no repetition penalty; BASELINE.json configs[1] "
+                         "with --preset 0.6b)")
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU per step (lock-step batch)")
     ap.add_argument("--cpu-frames", type=int, default=8, help="frames per run of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the physical cores this process may use")
@@ -377,10 +412,11 @@ def main():
     t = time.time()
     m = qtts.QwenTTS(md, device=dev)
     log(f"[bench] rank {rank}: model loaded on HIP device {dev} in {time.time() - t:.1f}s")
+    samp = GREEDY if args.greedy else {}
     if args.eos:   # the reference's defaults: max_new_tokens 4096, EOS stop (Q.c:871-880, 1324-1330)
-        m.set_params(max_tokens=4096, fixed=0, seed=42 + rank)
+        m.set_params(max_tokens=4096, fixed=0, seed=42 + rank, **samp)
     else:
-        m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank)
+        m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank, **samp)
     prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
 
     vc = None
@@ -444,18 +480,25 @@ def main():
         # the same utterances at the same length in fixed-length mode: what the
         # EOS mode itself costs (host polling every 8 frames, the attention grid
         # sized from the 4096-frame KV capacity)
-        n_eos = samples // (1920 * args.steps * args.batch)
-        m.set_params(max_tokens=n_eos, fixed=n_eos, seed=42 + rank)
-        one_step()
-        torch.cuda.synchronize()
-        tf = time.perf_counter()
-        sf = sum(one_step() for _ in range(args.steps))
-        torch.cuda.synchronize()
-        elf = time.perf_counter() - tf
-        m.set_params(max_tokens=4096, fixed=0, seed=42 + rank)
-        eos = dict(eos_gain=EOS_GAIN, frames_per_utterance=n_eos, max_new_tokens=4096,
-                   fixed_same_length_audio_s_per_s=round(sf / 24000.0 / elf, 3),
-                   fixed_same_length_ms_per_step=round(elf / args.steps * 1e3, 2))
+        # (batch 1 only: the slots of a batch stop at different frames, so one
+        # fixed length would be a different workload; there the line reports
+        # the mean frames per utterance alone)
+        if args.batch == 1:
+            n_eos = samples // (1920 * args.steps)
+            m.set_params(max_tokens=n_eos, fixed=n_eos, seed=42 + rank, **samp)
+            one_step()
+            torch.cuda.synchronize()
+            tf = time.perf_counter()
+            sf = sum(one_step() for _ in range(args.steps))
+            torch.cuda.synchronize()
+            elf = time.perf_counter() - tf
+            m.set_params(max_tokens=4096, fixed=0, seed=42 + rank, **samp)
+            eos = dict(eos_gain=EOS_GAIN, frames_per_utterance=n_eos, max_new_tokens=4096,
+                       fixed_same_length_audio_s_per_s=round(sf / 24000.0 / elf, 3),
+                       fixed_same_length_ms_per_step=round(elf / args.steps * 1e3, 2))
+        else:
+            eos = dict(eos_gain=EOS_GAIN, frames_per_utterance_mean=round(samples / (1920 * args.steps * args.batch), 2),
+                       max_new_tokens=4096)
     el_max = reduce_max(ws, el)
     audio_total = reduce_sum(ws, samples / 24000.0)
     value = audio_total / el_max
@@ -524,11 +567,13 @@ def main():
     # baseline in ref_audio_encode instead
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and vc is None and not args.eos:
         thr = args.cpu_threads or cpu_threads_default()
-        cpu = cpu_baseline(md, prompts[0], thr, frames=args.cpu_frames, runs=args.cpu_runs, target_frames=args.frames)
+        cpu = cpu_baseline(md, prompts[0], thr, frames=args.cpu_frames, runs=args.cpu_runs, target_frames=args.frames,
+                           greedy=args.greedy)
         if cpu and not args.no_cpu_1thread:
             # (two measured runs: the reference prints its [persistent] lines only
             # for --benchmark-runs > 1, c/main.c:263-264)
-            one = cpu_baseline(md, prompts[0], 1, frames=2, warmup=0, runs=2, target_frames=args.frames, timeout=3000)
+            one = cpu_baseline(md, prompts[0], 1, frames=2, warmup=0, runs=2, target_frames=args.frames, timeout=3000,
+                               greedy=args.greedy)
             if one:
                 cpu["one_thread"] = {k: one[k] for k in ("value", "unit", "cores", "sample", "runs")}
 
@@ -545,17 +590,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32 activations x bf16 weights (fp32 accumulate)",
-            "data": "synthetic (seeded random-init weights of the 1.7B architecture, tools/synth_model.py)",
+            "data": f"synthetic (seeded random-init weights of the {args.preset.upper()} architecture, tools/synth_model.py)",
             "config": {"workload": f"Qwen3-TTS-{args.preset} synthetic, P128 prompt, fixed {args.frames} frames "
-                                   f"({args.frames * 0.08:.2f} s audio), default sampling, batch {args.batch} per GPU"
+                                   f"({args.frames * 0.08:.2f} s audio), {'greedy' if args.greedy else 'default sampling'}, "
+                                   f"batch {args.batch} per GPU"
                                    + ((", ICL voice clone from 5 s reference audio (12 Hz codes + x-vector encoded "
                                        "on the GPU inside the step) + 20-id reference text, codec over reference ++ "
                                        "generated (reference part cut)") if wavs is not None else
                                       (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, "
                                        "codec over reference ++ generated (reference part cut)") if vc else
                                       (f", EOS mode (max_new_tokens 4096, codec-head EOS row x {EOS_GAIN}: the "
-                                       f"utterance stops at frame {eos['frames_per_utterance']})") if eos else ""),
-                       "global_batch": args.batch * ws, "frames": eos["frames_per_utterance"] if eos else args.frames,
+                                       f"utterances stop at frame {eos.get('frames_per_utterance', eos.get('frames_per_utterance_mean'))}"
+                                       f"{'' if 'frames_per_utterance' in (eos or {}) else ' on average'})") if eos else ""),
+                       "global_batch": args.batch * ws, "frames": (eos.get("frames_per_utterance", eos.get("frames_per_utterance_mean")) if eos
+                                  else args.frames),
                        "parallelism": f"dp{ws} (independent replicas, no collective in the data path)"},
         }
         if fp:

@@ -246,7 +246,8 @@ int qwen_tts_generate_voice_clone_batch(qwen_tts_ctx_t *ctx, int nb, const char 
 /* Voice clone from reference AUDIO (the Python reference's
  * create_voice_clone_prompt, qwen3_tts_model.py:356-458, on the device).
  * Waveforms are mono float PCM at 24 kHz (the reference resamples other rates
- * with librosa first; this library takes 24 kHz only).  The model directory
+ * with librosa first; here the caller resamples with qwen_tts_resample below,
+ * as the CLI's --ref-audio does for other rates).  The model directory
  * must hold the speaker encoder (speaker_encoder.* + speaker_encoder_config)
  * and the 12 Hz tokenizer encoder (speech_tokenizer/ encoder.* +
  * encoder_config).
@@ -288,6 +289,9 @@ float *qwen_tts_resample(const float *in, int n_in, int sr_in, int sr_out, int *
 /* codes of the last generate() (slot 0): copies up to max_frames rows of
  * num_code_groups ints, returns the frame count */
 int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames);
+/* the same for slot `slot` of the last qwen_tts_generate_batch (slot 0 ==
+ * qwen_tts_last_codes); -1 on a bad slot */
+int qwen_tts_last_codes_slot(qwen_tts_ctx_t *ctx, int slot, int *codes, int max_frames);
 /* Streaming generation (the reference has only a per-step
  * progress callback, c/qwen_tts.h:356): audio is decoded incrementally and
  * exactly (qtts_hip.h codec stream) and handed to `cb` as it is produced --

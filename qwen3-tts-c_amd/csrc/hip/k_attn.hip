@@ -615,15 +615,15 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
 // at HD 128: 32-key splits, attention 5.7 -> 4.7 us per layer at <= 138 keys
 // (the consumer merges 5 partials instead of 3; profiles/r03d_attn_split_ab.txt).
 // QTTS_HIP_ATTN_LPK (HD 128: 4, 8 or 16 lanes per key = 64-, 32- or 16-key
-// splits) overrides both for split-size A/B runs.
-static int attn_lpk(int HD, bool defer) {
-    const char *ev = getenv("QTTS_HIP_ATTN_LPK");   // (read per call: tests switch it per model instance)
-    const int env = ev ? atoi(ev) : 0;
+// splits) overrides both for split-size A/B runs.  The model latches it ONCE
+// at creation (qtts_dev::attn_lpk) and passes it in AttnArgs::lpk, so the
+// split scratch it sizes at allocation always covers the launch.
+static int attn_lpk(int HD, bool defer, int env) {
     if (HD == 128 && (env == 4 || env == 8 || env == 16)) return env;
     if (HD == 128 && defer) return 8;
     return HD >= 32 ? HD / 32 : 1;
 }
-int qtts_attn_keys_per_split(int HD, bool defer) { return 256 / attn_lpk(HD, defer); }
+int qtts_attn_keys_per_split(int HD, bool defer, int lpk) { return 256 / attn_lpk(HD, defer, lpk); }
 
 bool qtts_attn_defer_ok(const AttnArgs &a) {
     const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
@@ -648,18 +648,18 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok) {
-        const int ch = qtts_attn_keys_per_split(a.HD, a.defer);
-        // splits launched: the capacity's, or fewer when the caller knows the
-        // live keys stay below a.nsplit * ch (the frame graphs' split buckets;
-        // workgroups past the live length exit at once)
-        const int cap = (a.S + ch - 1) / ch;
-        const int nsplit = a.part && a.nsplit >= 1 && a.nsplit < cap ? a.nsplit : cap;
+        const int ch = qtts_attn_keys_per_split(a.HD, a.defer, a.lpk);
+        // one split per ch keys of the cache's capacity (workgroups past the
+        // live length exit at once); the scratch must hold all of them, or
+        // keys past a.nsplit * ch would never be attended
+        const int nsplit = (a.S + ch - 1) / ch;
         if ((nsplit > 1 || a.defer) && (!a.part || !a.cnt || a.nsplit < nsplit)) {
-            fprintf(stderr, "qtts_attention: split scratch missing (need %d splits)\n", nsplit);
+            fprintf(stderr, "qtts_attention: split scratch missing (need %d splits of %d keys, have %d)\n",
+                    nsplit, ch, a.part ? a.nsplit : 0);
             return -1;
         }
         const dim3 grid(a.KV, nsplit, a.nrows);
-        const int lpk = attn_lpk(a.HD, a.defer);
+        const int lpk = attn_lpk(a.HD, a.defer, a.lpk);
 #define QTTS_AD(H, L)                                                                                      \
         if (a.HD == H && lpk == L) {                                                                       \
             hipLaunchKernelGGL((k_attn_dec<H, 2, L>), grid, dim3(256), 0, st, a);                         \
@@ -668,8 +668,8 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
         }
         QTTS_AD(128, 4) QTTS_AD(128, 8) QTTS_AD(128, 16) QTTS_AD(64, 2) QTTS_AD(32, 1) QTTS_AD(16, 1)
 #undef QTTS_AD
+        fprintf(stderr, "qtts_attention: no decode kernel for HD=%d lpk=%d\n", a.HD, lpk);
         return -1;
-        return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     size_t smem = (size_t)(128 * 3 + 256 + 8 + 8 * 128 + a.S + 4) * sizeof(float);
     hipLaunchKernelGGL(k_attn, dim3(a.NH, a.nrows), dim3(256), smem, st, a);

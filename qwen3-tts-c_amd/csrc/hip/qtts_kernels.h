@@ -115,9 +115,13 @@ struct AttnArgs {
     // and the merge is the consumer's (GemvArgs::amerge, the O projection's
     // prologue) instead of the last split's
     int defer = 0;
+    // lanes per key of the split kernel at HD 128 (4 / 8 / 16), latched by the
+    // model at creation (QTTS_HIP_ATTN_LPK); 0 = the default for HD / defer
+    int lpk = 0;
 };
-// keys per split of the talker decode attention (deferred merge or not)
-int qtts_attn_keys_per_split(int HD, bool defer);
+// keys per split of the talker decode attention (deferred merge or not; lpk
+// as AttnArgs::lpk)
+int qtts_attn_keys_per_split(int HD, bool defer, int lpk);
 // true when the decode attention takes these arguments on its split kernel,
 // whose merge AttnArgs::defer hands to the consumer
 bool qtts_attn_defer_ok(const AttnArgs &a);

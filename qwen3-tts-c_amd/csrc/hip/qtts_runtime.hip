@@ -161,6 +161,7 @@ struct qtts_dev {
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
     bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
+    int attn_lpk = 0;        // QTTS_HIP_ATTN_LPK=4|8|16 (HD 128 split size), latched here: sizes att_part
     // QTTS_HIP_GM_DBG=<layer>: phase stamps of that talker layer's batch GEMVs
     // (q|k|v, O, gate|up, down), printed by qtts_dev_get_codes
     int gm_dbg_layer = -1;
@@ -377,6 +378,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     if (bm) dv->bself_min = atoi(bm);
     const char *ad = getenv("QTTS_HIP_ATTN_DEFER");
     dv->attn_defer = !(ad && !atoi(ad));
+    const char *lk = getenv("QTTS_HIP_ATTN_LPK");
+    dv->attn_lpk = lk ? atoi(lk) : 0;
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
     const char *gd = getenv("QTTS_HIP_GM_DBG");
@@ -583,7 +586,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     {
         const int gph = d.NH / d.KV;
         // partial slots for the smaller split size of the two launch forms
-        const int ch = std::min(qtts_attn_keys_per_split(d.HD, false), qtts_attn_keys_per_split(d.HD, true));
+        const int ch = std::min(qtts_attn_keys_per_split(d.HD, false, dv->attn_lpk),
+                                qtts_attn_keys_per_split(d.HD, true, dv->attn_lpk));
         dv->att_nsplit = (dv->S + ch - 1) / ch;
         A(att_part, float, B * d.KV * dv->att_nsplit * (gph * d.HD + 2 * gph));
         const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
@@ -861,7 +865,7 @@ static int talker_layers(qtts_dev *dv) {
         t.kc = dv->kc + (size_t)l * NBA * dv->S * KVD; t.vc = dv->vc + (size_t)l * NBA * dv->S * KVD; t.S = dv->S;
         t.pos = dv->kv_len; t.NH = d.NH; t.KV = d.KV; t.HD = d.HD; t.out = dv->att; t.ld_out = AD; t.nrows = nb;
         t.skip = dv->stopped;
-        t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit;
+        t.part = dv->att_part; t.cnt = dv->att_cnt; t.nsplit = dv->att_nsplit; t.lpk = dv->attn_lpk;
         // batch 1: the attention's split merge moves into the O projection's
         // prologue (one dependent hand-off fewer per layer)
         const bool defer = dv->attn_defer && nb == 1 && qtts_attn_defer_ok(t) && qtts_gemvw_amerge_ok(d.H, AD);
@@ -874,7 +878,7 @@ static int talker_layers(qtts_dev *dv) {
         if (dbg) o.dbg = dv->gm_dbg + 2048 * 8;
         if (defer) {
             o.amerge = dv->att_part; o.am_pos = dv->kv_len; o.am_nsplit = dv->att_nsplit;
-            o.am_ch = qtts_attn_keys_per_split(d.HD, true); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
+            o.am_ch = qtts_attn_keys_per_split(d.HD, true, dv->attn_lpk); o.am_hd = d.HD; o.am_gph = d.NH / d.KV;
         }
         // the talker's O / down reduce their own partials at every batch size:
         // its q|k|v and gate|up prologues (2048-wide x rows) then read x alone

@@ -1154,6 +1154,12 @@ int qwen_tts_last_codes(qwen_tts_ctx_t *ctx, int *codes, int max_frames) {
     return n;
 }
 
+int qwen_tts_last_codes_slot(qwen_tts_ctx_t *ctx, int slot, int *codes, int max_frames) {
+    if (!ctx || !ctx->hip || slot < 0 || max_frames < 0) return -1;
+    if (slot == 0) return qwen_tts_last_codes(ctx, codes, max_frames);
+    return qtts_dev_get_codes((qtts_dev_t *)ctx->hip, slot, codes, max_frames);
+}
+
 /* -------------------------------------------------- stage functions (host) */
 void qwen_tts_talker_prefill(qwen_tts_ctx_t *ctx, const float *input_embeds, int seq_len) {
     if (qtts_dev_talker_prefill_host((qtts_dev_t *)ctx->hip, input_embeds, seq_len, ctx->tk_x) != 0) {

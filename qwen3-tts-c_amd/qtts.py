@@ -66,7 +66,7 @@ class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
 EXPORTS = [
     "qwen_tts_load", "qwen_tts_free", "qwen_tts_set_progress_callback", "qwen_tts_generate", "qwen_tts_write_wav",
     "qwen_tts_talker_prefill", "qwen_tts_talker_forward", "qwen_tts_subtalker_generate", "qwen_tts_codec_decode",
-    "qwen_tts_talker_hidden", "qwen_tts_load_on", "qwen_tts_generate_batch", "qwen_tts_last_codes",
+    "qwen_tts_talker_hidden", "qwen_tts_load_on", "qwen_tts_generate_batch", "qwen_tts_last_codes", "qwen_tts_last_codes_slot",
     "qwen_tts_abi_sizeof_ctx", "qwen_tts_verbose", "qwen_tts_generate_stream", "qwen_tts_codec_stream_begin",
     "qwen_tts_codec_stream_push", "qwen_tts_generate_voice_clone",
     "qwen_tts_generate_voice_clone_batch", "qwen_tts_generate_voice_clone_stream", "qwen_tts_tokenize",
@@ -140,6 +140,8 @@ def lib():
                                           C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), _ip]
     L.qwen_tts_last_codes.restype = C.c_int
     L.qwen_tts_last_codes.argtypes = [C.POINTER(Ctx), _ip, C.c_int]
+    L.qwen_tts_last_codes_slot.restype = C.c_int
+    L.qwen_tts_last_codes_slot.argtypes = [C.POINTER(Ctx), C.c_int, _ip, C.c_int]
     L.qwen_tts_talker_prefill.argtypes = [C.POINTER(Ctx), _fp, C.c_int]
     L.qwen_tts_talker_forward.argtypes = [C.POINTER(Ctx), _fp, _fp]
     L.qwen_tts_subtalker_generate.argtypes = [C.POINTER(Ctx), _fp, C.c_int, _ip]
@@ -235,6 +237,7 @@ class QwenTTS:
             raise RuntimeError(f"qwen_tts_load({model_dir}) failed")
         self.c = self.ctx.contents
         self.cfg = self.c.config
+        self._last_nb = 1
 
     def close(self):
         if self.ctx:
@@ -426,6 +429,7 @@ class QwenTTS:
         out = (C.c_void_p * nb)()
         ns = (C.c_int * nb)()
         rc = lib().qwen_tts_generate_batch(self.ctx, nb, tx, sp, lg, out, ns)
+        self._last_nb = nb
         audio = [_take_audio(out[i], ns[i]) for i in range(nb)]
         return rc, audio
 
@@ -484,6 +488,17 @@ class QwenTTS:
         buf = np.zeros((max(n, 1), G), np.int32)
         k = lib().qwen_tts_last_codes(self.ctx, buf.ctypes.data_as(_ip), n)
         return buf[:k].copy()
+
+    def last_codes_slot(self, slot, max_frames=4096):
+        """codes of batch slot `slot` of the last generate_batch (frames x groups)"""
+        buf = np.zeros((max_frames, self.cfg.num_code_groups), np.int32)
+        k = lib().qwen_tts_last_codes_slot(self.ctx, int(slot), buf.ctypes.data_as(_ip), max_frames)
+        if k < 0:
+            raise ValueError(f"no batch slot {slot}")
+        return buf[:k].copy()
+
+    def last_codes_batch(self, nb=None, max_frames=4096):
+        return [self.last_codes_slot(b, max_frames) for b in range(nb if nb is not None else self._last_nb)]
 
     # stage functions (host pointers)
     def prefill(self, embeds):

@@ -10,6 +10,12 @@ Fixtures (tests/golden/make_golden_long.py, from the reference c/ build):
   way.  A 600-row prefill (> 512 rows) and 4 decode steps over 600+ keys.
 * `long_17b.npz` -- the benchmark workload itself (bench.py): synthetic 1.7B,
   P128 prompt, fixed 128 frames, default sampling, seed 42.
+* `long_06b.npz` -- BASELINE configs[1] (C2): synthetic 0.6B (H = H_s = 1024,
+  no sub-talker input projection), P128, GREEDY, fixed 128 frames.
+* `long_17b_b8.npz` -- BASELINE C4's per-GPU shape: 8 prompts, default
+  sampling, 32 frames, each slot one reference run; decoded here as ONE
+  lock-step batch on the batch GEMV (`k_gemvb`, RMS scale applied after the
+  dot product, split-K O / down), codes compared slot by slot.
 
 Bars: codes bit-exact (the first divergent frame / group is reported if not);
 waveform MSE < 1e-4 and max |d| < 1e-3 (north star); hidden / logits
@@ -23,7 +29,7 @@ import pytest
 
 from conftest import GOLDEN, model_dir
 from make_golden_long import prefill_inputs
-from oracle_py import DEFAULT, Oracle
+from oracle_py import DEFAULT, GREEDY, Oracle
 
 import qtts
 
@@ -117,6 +123,52 @@ def test_full_bench_workload_vs_reference(gpu):
         a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
         _codes_equal(m.last_codes(), g["codes"], "1.7B bench workload")
         _audio_close(a, g["audio"], "1.7B bench workload waveform")
+    finally:
+        m.close()
+
+
+def test_c2_06b_greedy_128_frames_vs_reference(gpu):
+    """BASELINE configs[1] (0.6B, batch 1, greedy, P128), the whole 128-frame
+    utterance: codes bit-exact against the reference, waveform MSE < 1e-4."""
+    g = np.load(os.path.join(GOLDEN, "long_06b.npz"))
+    man = _man()["0.6b"]
+    m = qtts.QwenTTS(model_dir("0.6b"))
+    try:
+        m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **GREEDY)
+        a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
+        _codes_equal(m.last_codes(), g["codes"], "0.6B greedy 128 frames")
+        _audio_close(a, g["audio"], "0.6B greedy waveform")
+    finally:
+        m.close()
+
+
+def _b8_prompts(g):
+    return [g["prompt_ids"][b, :int(g["prompt_len"][b])] for b in range(g["prompt_ids"].shape[0])]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"}])
+def test_c4_batch8_lock_step_vs_reference(gpu, monkeypatch, env):
+    """C4's per-GPU shape: the 8 reference utterances (32 frames, default
+    sampling) decoded as ONE lock-step batch -- the batch GEMV with its RMS
+    scale after the dot product, split-K O / down -- every slot's codes
+    bit-exact against its own reference run, audio against the reference's
+    samples.  Also on the staged-plane batch GEMV (GEMVB=0) and with the
+    split-K producers reducing their own partials from 2 rows."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = np.load(os.path.join(GOLDEN, "long_17b_b8.npz"))
+    man = _man()["b8"]
+    m = qtts.QwenTTS(model_dir("1.7b"))
+    try:
+        m.set_params(max_tokens=4096, fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        rc, audio = m.generate_batch(_b8_prompts(g), man["speakers"], [man["language"]] * 8)
+        assert rc == 0
+        codes = m.last_codes_batch()
+        for b in range(8):
+            _codes_equal(codes[b], g["codes"][b], f"batch-8 slot {b} {env}")
+            _audio_close(audio[b][::man["audio_stride"]], g["audio_sub"][b], f"slot {b} every 16th sample")
+            _audio_close(audio[b][-1920:], g["audio_last"][b], f"slot {b} last frame")
     finally:
         m.close()
 
