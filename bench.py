@@ -124,13 +124,13 @@ def _latest_profile(pattern):
     return fs[-1] if fs else None
 
 
-def _rocprof_lookup(kname):
+def _rocprof_lookup(kname, variant=""):
     """Average duration (us) of `kname` in the newest committed rocprofv3
     --stats summary and its HBM bytes per launch in the newest PMC summary
     (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/prof_summary.py)."""
     avg_us = traffic = None
     src = {}
-    f = _latest_profile("*kernel_stats.csv")
+    f = _latest_profile(f"*{variant}kernel_stats.csv")
     if f:
         import csv
         with open(f) as fh:
@@ -139,7 +139,7 @@ def _rocprof_lookup(kname):
                     avg_us = float(row["AverageNs"]) / 1e3
                     src["stats"] = os.path.relpath(f, ROOT)
                     break
-    f = _latest_profile("*pmc.json")
+    f = _latest_profile(f"*{variant}pmc.json")
     if f:
         with open(f) as fh:
             pm = json.load(fh)
@@ -151,7 +151,7 @@ def _rocprof_lookup(kname):
     return avg_us, traffic, src
 
 
-def profile_roofline(m, lib):
+def profile_roofline(m, lib, variant=""):
     """One eager frame with HIP events around every kernel launch on the
     context stream (qtts_dev_profile_frame); the dominant kernel is the GEMV
     instantiation with the largest share of the frame."""
@@ -183,7 +183,7 @@ def profile_roofline(m, lib):
     dom = max(gemv, key=lambda x: gemv[x][1])
     cnt, tot_ms, tot_b = gemv[dom]
     avg_ms, avg_bytes = tot_ms / cnt, tot_b / cnt
-    rp_us, traffic, src = _rocprof_lookup(dom)
+    rp_us, traffic, src = _rocprof_lookup(dom, variant)
     kind_of = {nm[i]: int(k[i]) for i in range(n)}
     return dict(kernel=dom, kind=kind_of[dom], launches_per_frame=cnt, avg_bytes=avg_bytes, avg_ms=avg_ms,
                 achieved_GBs=avg_bytes / (avg_ms * 1e-3) / 1e9, rocprof_avg_us=rp_us, traffic=traffic,
@@ -558,7 +558,9 @@ def main():
             for _ in range(2):
                 m.generate_voice_clone_audio_stream(prompts[0], wavs[0], vc[0][0], "english", chunk_frames=8)
             fp["first_packet_from_audio_ms"] = m.c.perf_first_packet_ms
-    roof = None if args.no_profile or vc is not None else profile_roofline(m, qtts.lib())
+    # (the 0.6B line reads the 0.6B profile passes: <tag>_06b_kernel_stats.csv / _pmc.json)
+    roof = None if args.no_profile or vc is not None else profile_roofline(
+        m, qtts.lib(), "" if args.preset == "1.7b" else args.preset.replace(".", "") + "_")
     m.close()
 
     cpu = None

@@ -59,8 +59,18 @@ __device__ __forceinline__ void gw_stamp(const GemvArgs &a, int k) {
 #endif
 }
 
+// The first arguments are what the kernel's first loads need -- the x (or
+// table) base, the weights, the id pointer (ids + ids_off) and the source
+// kind (0 x, 1 bf16 table, 2 fp32 table, + 4: a.row_sel set) -- ahead of the
+// GemvArgs block: the Makefile builds this file with kernarg preloading, so
+// the CP hands them over in SGPRs and the x / id / weight loads issue
+// without waiting for a kernarg round trip (the rest of `a` arrives by
+// s_load meanwhile).
+enum { GW_SRC_X = 0, GW_SRC_TAB = 1, GW_SRC_TABF = 2, GW_SRC_ROWSEL = 4 };
+
 template <int RW, int NV, bool NT, int AM_MS = 0>
-__global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
+__global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W, const int *ids, int src_kind,
+                                               GemvArgs a) {
     gw_stamp(a, 0);
     constexpr bool AM = AM_MS > 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -73,13 +83,13 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     //    them do not hold back the prologue (vmcnt retires loads in issue
     //    order, so x issued behind 12 weight loads would wait for all of them)
     const bf16_t *trow = nullptr;
-    const float *xrow = a.x;
-    if (a.table || a.table_f32) {
-        const int *ip = a.ids + a.ids_off + blockIdx.y;
-        if (a.row_sel) ip += (size_t)a.row_sel[0] * a.ids_rstride;
+    const float *xrow = reinterpret_cast<const float *>(src);
+    if (src_kind & 3) {
+        const int *ip = ids + blockIdx.y;
+        if (src_kind & GW_SRC_ROWSEL) ip += (size_t)a.row_sel[0] * a.ids_rstride;
         const size_t off = (size_t)(*ip) * C;
-        if (a.table) trow = a.table + off;
-        else xrow = a.table_f32 + off;
+        if ((src_kind & 3) == GW_SRC_TAB) trow = reinterpret_cast<const bf16_t *>(src) + off;
+        else xrow += off;
     }
     // partials held in registers (the sub-talker's 8 per-head O partials at
     // C = 1024); wider rows sum them from memory below
@@ -126,11 +136,22 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
         if (a.norm_w) nwv[q] = *reinterpret_cast<const float4 *>(a.norm_w + cc);
     }
 
+    // 1b. the residual rows of an EPI_RESID epilogue, also ahead of the weights
+    //     (read after the dot they were one more dependent round trip at the
+    //     end of every O / down projection); rows are owned by this workgroup,
+    //     so the early read sees the same values.  Unconditional load from a
+    //     clamped address: a branch here would make the compiler wait for it.
+    float *y = a.y + blockIdx.y * a.ldy_rep;
+    const bool resid = a.epi == EPI_RESID;
+    float yres[RW];
+#pragma unroll
+    for (int i = 0; i < RW; ++i) yres[i] = y[resid ? row0 + w + 4 * i : 0];
+
     // 2. the whole weight slice of this lane in flight
     v4u wv[RW][NV];
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-        const v4u *p = reinterpret_cast<const v4u *>(a.W + (size_t)(row0 + w + 4 * i) * C) + lane;
+        const v4u *p = reinterpret_cast<const v4u *>(W + (size_t)(row0 + w + 4 * i) * C) + lane;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             if constexpr (NT) wv[i][k] = __builtin_nontemporal_load(p + 64 * k);
@@ -237,7 +258,6 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
     }
     gw_stamp(a, 2);
     if (lane != 0) return;
-    float *y = a.y + blockIdx.y * a.ldy_rep;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         const int r = row0 + w + 4 * i;
@@ -250,7 +270,7 @@ __global__ __launch_bounds__(256) void k_gemvw(GemvArgs a) {
                 y[r] = z / (1.0f + expf(-z));
                 break;
             }
-            case EPI_RESID: y[r] += v; break;
+            case EPI_RESID: y[r] = yres[i] + v; break;
             case EPI_SWIGLU:
                 if ((i & 1) == 0 && i + 1 < RW) y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * acc[i + 1];
                 break;
@@ -278,7 +298,8 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
         // partials of up to 4 / 8 splits ahead of the weights: the capacity's
         // splits when they fit (fixed-length decodes), else 8 and the rest after
 #define QTTS_GWA(RW_, MS_)                                                                             \
-        { hipLaunchKernelGGL((k_gemvw<RW_, 4, true, MS_>), grid, dim3(256), smem, st, a);              \
+        { hipLaunchKernelGGL((k_gemvw<RW_, 4, true, MS_>), grid, dim3(256), smem, st, (const void *)a.x, a.W,   \
+                             (const int *)nullptr, (int)GW_SRC_X, a);                                   \
           qtts_last_kernel = "k_gemvw<" #RW_ ", 4, true, " #MS_ ">"; }
         if (a.R == 2048) { if (a.am_nsplit <= 4) QTTS_GWA(2, 4) else if (a.am_nsplit <= 6) QTTS_GWA(2, 6) else QTTS_GWA(2, 8) }
         else { if (a.am_nsplit <= 4) QTTS_GWA(1, 4) else if (a.am_nsplit <= 6) QTTS_GWA(1, 6) else QTTS_GWA(1, 8) }
@@ -302,13 +323,17 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
     if (RW * NV > 24 || (a.epi == EPI_SWIGLU && (RW & 1))) return 1;
     const dim3 grid(a.R / (4 * RW), a.reps);
     const size_t smem = (size_t)(a.C + 4) * sizeof(float);
+    const void *src = a.table ? (const void *)a.table : a.table_f32 ? (const void *)a.table_f32 : (const void *)a.x;
+    const int kind = (a.table ? GW_SRC_TAB : a.table_f32 ? GW_SRC_TABF : GW_SRC_X) |
+                     ((a.table || a.table_f32) && a.row_sel ? GW_SRC_ROWSEL : 0);
+    const int *ids = (a.table || a.table_f32) ? a.ids + a.ids_off : nullptr;
 #define QTTS_GW(RW_, NV_)                                                                              \
     if (RW == RW_ && NV == NV_) {                                                                      \
         if (a.nt) {                                                                                    \
-            hipLaunchKernelGGL((k_gemvw<RW_, NV_, true>), grid, dim3(256), smem, st, a);               \
+            hipLaunchKernelGGL((k_gemvw<RW_, NV_, true>), grid, dim3(256), smem, st, src, a.W, ids, kind, a); \
             qtts_last_kernel = "k_gemvw<" #RW_ ", " #NV_ ", true>";                                    \
         } else {                                                                                       \
-            hipLaunchKernelGGL((k_gemvw<RW_, NV_, false>), grid, dim3(256), smem, st, a);              \
+            hipLaunchKernelGGL((k_gemvw<RW_, NV_, false>), grid, dim3(256), smem, st, src, a.W, ids, kind, a); \
             qtts_last_kernel = "k_gemvw<" #RW_ ", " #NV_ ", false>";                                   \
         }                                                                                              \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                               \

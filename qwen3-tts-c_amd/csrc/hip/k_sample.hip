@@ -13,6 +13,14 @@ __global__ __launch_bounds__(256) void k_sample(SampArgs a) {
     qtts_samp::sample_row<FAST, EM>(a, blockIdx.x, smraw);
 }
 
+// the fast path on 1024 threads (qtts_sample_dev.h sample_fast_nt): EM ids per
+// thread (2 up to 2048 logits, 4 up to 4096)
+template <int EM>
+__global__ __launch_bounds__(1024) void k_sample_w(SampArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    qtts_samp::sample_row<true, EM, 1024>(a, blockIdx.x, smraw);
+}
+
 }  // namespace
 
 int qtts_sample(const SampArgs &a, hipStream_t st) {
@@ -20,7 +28,19 @@ int qtts_sample(const SampArgs &a, hipStream_t st) {
         fprintf(stderr, "qtts_sample: vocab %d unsupported (max %d)\n", a.n, qtts_samp::NMAX);
         return -1;
     }
-    if (qtts_samp::fast_path(a)) {
+    // QTTS_HIP_SAMPLE_W=0: the 256-thread fast path (A/B; read per call so a
+    // test's setting applies to its own launches)
+    const char *sw = getenv("QTTS_HIP_SAMPLE_W");
+    if (qtts_samp::fast_path(a) && !(sw && !atoi(sw))) {
+        const size_t sm = sizeof(qtts_samp::FastSmemNT<1024>);
+        if (a.n <= 2 * 1024) {
+            hipLaunchKernelGGL((k_sample_w<2>), dim3(a.nb), dim3(1024), sm, st, a);
+            qtts_last_kernel = "k_sample_w<2>";
+        } else {
+            hipLaunchKernelGGL((k_sample_w<4>), dim3(a.nb), dim3(1024), sm, st, a);
+            qtts_last_kernel = "k_sample_w<4>";
+        }
+    } else if (qtts_samp::fast_path(a)) {
         const size_t sm = sizeof(qtts_samp::FastSmem);
         if (a.n <= 8 * 256) {
             hipLaunchKernelGGL((k_sample<true, 8>), dim3(a.nb), dim3(256), sm, st, a);

@@ -118,6 +118,10 @@ struct qtts_dev {
     float *x_st = nullptr, *qkv_s = nullptr, *att_s = nullptr, *h_s = nullptr, *logits_s = nullptr;
     float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
     int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
+    // [B] the id each slot's last draw produced (every sampler's out_tok): the
+    // next sub-talker pass reads its input row by it -- one dependent load
+    // where codes[b][cur_row[b]][g-1] took two (cur_row, then the code)
+    int *last_tok = nullptr;
     int *stop_step = nullptr, *kv_len = nullptr, *n_trailing = nullptr;
     float *att_part = nullptr;   // split-K decode attention partials (talker)
     int *att_cnt = nullptr, att_nsplit = 0;
@@ -563,6 +567,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(n_gen, int, B);
     A(stopped, int, B);
     A(cur_row, int, B);
+    A(last_tok, int, B);
+    CK(hipMemsetAsync(dv->last_tok, 0, B * sizeof(int), dv->st));
     A(stop_step, int, B);
     A(kv_len, int, B);
     A(n_trailing, int, B);
@@ -933,7 +939,7 @@ static int talker_head_sample(qtts_dev *dv) {
     s.n_gen = dv->n_gen; s.stopped = dv->stopped; s.cur_row = dv->cur_row; s.stop_step = dv->stop_step;
     s.host_stopped = dv->hstop;
     s.st_rng = dv->st_rng; s.seed_bits = seed_bits(dv->par.seed);
-    s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G;
+    s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G; s.out_tok = dv->last_tok;
     return head_sample(dv, a, s, PK_GEMV_TALKER);
 }
 
@@ -954,8 +960,9 @@ static int subtalker(qtts_dev *dv) {
         else {
             if (ptab) src.table_f32 = g == 1 ? dv->codec_ptab : dv->st_ptab + (size_t)(g - 2) * d.Vs * d.Hs;
             else src.table = g == 1 ? dv->codec_emb : dv->st_emb + (size_t)(g - 2) * d.Vs * d.H;
-            src.ids = dv->codes; src.ids_bstride = cstride; src.row_sel = dv->cur_row; src.ids_rstride = d.G;
-            src.ids_off = g - 1;
+            // the previous draw's id (group g - 1: the talker's for g = 1)
+            src.ids = dv->last_tok; src.ids_bstride = 1; src.row_sel = nullptr; src.ids_rstride = 0;
+            src.ids_off = 0;
         }
         auto set_src = [&](GemvArgs &a) {
             a.x = src.x; a.ldx = src.ldx; a.table = src.table; a.table_f32 = src.table_f32; a.ids = src.ids;
@@ -1065,7 +1072,7 @@ static int subtalker(qtts_dev *dv) {
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
         s.mode = 0; s.st_rng = dv->st_rng; s.stopped = dv->stopped; s.cur_row = dv->cur_row;
-        s.codes = dv->codes; s.codes_bstride = cstride; s.G = d.G; s.g = g;
+        s.codes = dv->codes; s.codes_bstride = cstride; s.G = d.G; s.g = g; s.out_tok = dv->last_tok;
         CKI(head_sample(dv, a, s, PK_GEMV_SUB));
     }
     return 0;
@@ -1589,6 +1596,7 @@ extern "C" int qtts_dev_subtalker_host(qtts_dev_t *dv, const float *hidden, int 
     CK(hipMemcpy(dv->stopped, &zero, 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dv->st_rng, &sb, 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dv->codes, &first_code, 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dv->last_tok, &first_code, 4, hipMemcpyHostToDevice));
     dv->nrun = 1;
     int rc = subtalker(dv);
     dv->nrun = dv->nb;

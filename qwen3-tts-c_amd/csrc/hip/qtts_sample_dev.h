@@ -278,7 +278,8 @@ __device__ __forceinline__ void block_scan2(FastSmem &fs, int x, int y, int &ex,
 // and the first j whose running sum reaches r (K.c:451-477), every lane
 // walking the same broadcast values.  Lane 0 owns the RNG.  Returns the id
 // (all lanes).  (v_readlane per step measured 2-3x slower than the LDS reads.)
-__device__ __forceinline__ int wave_sort_draw(FastSmem &fs, int ke, uint32_t &rng, uint64_t etab) {
+template <class FS>
+__device__ __forceinline__ int wave_sort_draw(FS &fs, int ke, uint32_t &rng, uint64_t etab) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     unsigned long long *keys = reinterpret_cast<unsigned long long *>(fs.top_v);   // 64 x 8 B scratch
@@ -577,6 +578,328 @@ __device__ __forceinline__ int sample_fast_regs(FastSmem &fs, const float (&v)[E
     return out;
 }
 
+// ---------------------------------------------------------------------------
+// The same fast path on NT = 1024 threads (16 waves, <= 4 ids per thread):
+// a quarter of the per-thread work of every phase, one SHARED distance
+// histogram, candidate slots by one LDS atomic per wave, and the rank of the
+// <= 64 candidates split over the 16 waves (4 comparisons each) instead of
+// one wave's 64.  Wave 0 then holds p_j for rank j in lane j and sums them
+// sequentially in rank order with v_readlane (the reference's order,
+// K.c:456-463), and draws by ballot -- the same sums, so the same id as the
+// 256-thread path and the reference.  Dense ties (> 64 candidates) fall back
+// to the radix select over a shared three-buffer histogram.
+template <int NT>
+struct FastSmemNT {
+    static constexpr int NW = NT / 64;
+    int hist[3][256];                  // radix fallback, rotating buffers
+    int scan[NW];
+    float sel_v[KFAST];
+    int sel_i[KFAST];
+    float top_v[KFAST];
+    int top_i[KFAST];
+    int misc[4];
+    int dh[DBINS];                     // distance histogram (shared)
+    unsigned long long cand[KC];       // candidate keys (value key << 32 | ~index), slots by atomic
+    int crank[KC];                     // candidate ranks, summed over the waves' slices
+    float pv[KC];
+    int pi[KC];
+    float red[NW];
+    int redn[NW];
+    int ncand;
+};
+
+// block-wide exclusive scans of two small per-thread counts (16 | 16 bits)
+template <int NT>
+__device__ __forceinline__ void block_scan2_nt(FastSmemNT<NT> &fs, int x, int y, int &ex, int &ey) {
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int v = x | (y << 16);
+    const int inc = wave_incl_scan(v);
+    if (l == 63) fs.scan[w] = inc;
+    __syncthreads();
+    int base = 0;
+    for (int i = 0; i < w; ++i) base += fs.scan[i];
+    const int e = base + inc - v;
+    ex = e & 0xFFFF;
+    ey = e >> 16;
+}
+
+// radix_select_regs over one shared histogram per pass; buffers 0 and 1 are
+// zeroed by the caller before a barrier, buffer (p + 2) % 3 after pass p's
+// barrier (its readers were pass p - 1, its writers come after pass p + 1's)
+template <int NT, int EM>
+__device__ __forceinline__ void radix_select_nt(FastSmemNT<NT> &fs, const uint32_t (&kk)[EM], int E, int k,
+                                                uint32_t &T, uint32_t &Tmask, int &take_eq, int &ne) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t prefix = 0, mask = 0;
+    int rem = k;
+    ne = -1;
+    int p = 0;
+    for (int shift = 24; shift >= 0; shift -= 8, ++p) {
+        int *h = fs.hist[p % 3];
+#pragma unroll
+        for (int j = 0; j < EM; ++j)
+            if (j < E && kk[j] != 0u && (kk[j] & mask) == prefix) atomicAdd(&h[(kk[j] >> shift) & 255u], 1);
+        __syncthreads();
+        int c[4], tot = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            c[i] = h[255 - 4 * lane - i];
+            tot += c[i];
+        }
+        const int inc = wave_incl_scan(tot);
+        if (ne < 0) {
+            ne = __builtin_amdgcn_readlane(inc, 63);
+            if (k > ne) k = ne;
+            rem = k;
+        }
+        const int exc = inc - tot;
+        int bin = -1, nrem = 0, cbin = 0;
+        if (exc < rem && inc >= rem) {
+            int cum = exc;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (bin < 0 && cum + c[i] >= rem) { bin = 255 - 4 * lane - i; nrem = rem - cum; cbin = c[i]; }
+                cum += c[i];
+            }
+        }
+        const unsigned long long hit = __ballot(bin >= 0);
+        const int src = hit ? __ffsll((long long)hit) - 1 : 0;
+        bin = __builtin_amdgcn_readlane(bin, src);
+        nrem = __builtin_amdgcn_readlane(nrem, src);
+        cbin = __builtin_amdgcn_readlane(cbin, src);
+        if (tid < 256) fs.hist[(p + 2) % 3][tid] = 0;
+        if (k == 0) { T = 0xFFFFFFFFu; Tmask = 0xFFFFFFFFu; take_eq = 0; return; }
+        prefix |= (uint32_t)bin << shift;
+        mask |= 255u << shift;
+        rem = nrem;
+        if (cbin == nrem || shift == 0) {
+            T = prefix; Tmask = mask; take_eq = nrem;
+            return;
+        }
+    }
+}
+
+// Top-k draw for k <= KC (see sample_dist): returns the id in wave 0 (0 in
+// the other waves), or -1 in every thread when more than KC keys share the
+// bins through the k-th key's.  Four barriers.
+template <int NT, int EM, int STOP = 5>
+__device__ __forceinline__ int sample_dist_nt(FastSmemNT<NT> &fs, const float (&v)[EM], const uint32_t (&kk)[EM],
+                                              const int (&id)[EM], int k, uint32_t &rng, uint64_t etab) {
+#pragma clang fp contract(off)
+    constexpr int NW = NT / 64;
+    static_assert(NW * 4 >= KC, "the rank slices cover KC candidates");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float m = -INFINITY;
+    int ne = 0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j)
+        if (kk[j] != 0u) { m = fmaxf(m, v[j]); ++ne; }
+    m = wave_max(m);
+    ne = __builtin_amdgcn_readlane(wave_incl_scan(ne), 63);
+    for (int i = tid; i < DBINS; i += NT) fs.dh[i] = 0;
+    if (tid < 256) { fs.hist[0][tid] = 0; fs.hist[1][tid] = 0; }   // (the radix fallback's first buffers)
+    if (tid < KC) fs.crank[tid] = 0;
+    if (tid == 0) fs.ncand = 0;
+    if (lane == 0) { fs.red[w] = m; fs.redn[w] = ne; }
+    __syncthreads();                                                   // 1
+    const float M = wave_max(lane < NW ? fs.red[lane] : -INFINITY);
+    const int ne_all = __builtin_amdgcn_readlane(wave_incl_scan(lane < NW ? fs.redn[lane] : 0), 63);
+    if (k > ne_all) k = ne_all;
+    if (k == 0) return 0;                     // nothing eligible: the reference returns 0
+    if constexpr (STOP == 1) return (int)M;
+    const uint32_t Kmax = okey(M);
+    int bb[EM];
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        bb[j] = DBINS;
+        if (kk[j] != 0u) { bb[j] = dist_bin(Kmax - kk[j]); atomicAdd(&fs.dh[bb[j]], 1); }
+    }
+    __syncthreads();                                                   // 2
+    constexpr int BL = DBINS / 64;
+    int c[BL], tot = 0;
+    {
+        const int4 h0 = *reinterpret_cast<const int4 *>(&fs.dh[BL * lane]);
+        const int4 h1 = *reinterpret_cast<const int4 *>(&fs.dh[BL * lane + 4]);
+        c[0] = h0.x; c[1] = h0.y; c[2] = h0.z; c[3] = h0.w; c[4] = h1.x; c[5] = h1.y; c[6] = h1.z; c[7] = h1.w;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) tot += c[i];
+    const int inc = wave_incl_scan(tot), exc = inc - tot;
+    int B = -1, nc = 0;
+    if (exc < k && inc >= k) {
+        int cum = exc;
+#pragma unroll
+        for (int i = 0; i < BL; ++i) {
+            cum += c[i];
+            if (B < 0 && cum >= k) { B = BL * lane + i; nc = cum; }
+        }
+    }
+    if constexpr (STOP == 2) return tot;
+    const unsigned long long hit = __ballot(B >= 0);   // non-empty: k <= ne_all
+    const int src = __ffsll((long long)hit) - 1;
+    B = __builtin_amdgcn_readlane(B, src);
+    nc = __builtin_amdgcn_readlane(nc, src);
+    if (nc > KC) return -1;
+    // candidates (bin <= B) to slots: one returning LDS atomic per wave
+    int mine = 0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j) mine += bb[j] <= B;
+    const int wi = wave_incl_scan(mine);
+    const int wtot = __builtin_amdgcn_readlane(wi, 63);
+    int base = 0;
+    if (wtot > 0) {
+        if (lane == 0) base = atomicAdd(&fs.ncand, wtot);
+        base = __builtin_amdgcn_readlane(base, 0);
+    }
+    int pos = base + wi - mine;
+#pragma unroll
+    for (int j = 0; j < EM; ++j)
+        if (bb[j] <= B) {
+            fs.cand[pos] = ((unsigned long long)kk[j] << 32) | (0xFFFFFFFFu - (uint32_t)id[j]);
+            ++pos;
+        }
+    __syncthreads();                                                   // 3
+    if constexpr (STOP == 3) return nc;
+    // rank: candidate `lane` against the 4 of this wave's slice (value desc, index asc)
+    const unsigned long long key = lane < nc ? fs.cand[lane] : 0ull;   // 0: below every real key
+    {
+        // (unconditional reads of the slice -- slots past nc hold stale keys,
+        // masked after -- so the four LDS reads are in flight together)
+        unsigned long long kt[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) kt[u] = fs.cand[4 * w + u];
+        int r = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r += (4 * w + u < nc) && kt[u] > key;
+        if (lane < nc && r > 0) atomicAdd(&fs.crank[lane], r);
+    }
+    float e = 0.f;
+    if (w == 0) e = expf_glibc_wave(lane < nc ? key_val((uint32_t)(key >> 32)) - M : 0.f, etab);
+    __syncthreads();                                                   // 4
+    if (w != 0) return 0;
+    if constexpr (STOP == 4) return fs.crank[lane];
+    const int rank = fs.crank[lane];
+    if (lane < nc && rank < k) { fs.pv[rank] = e; fs.pi[rank] = (int)(0xFFFFFFFFu - (uint32_t)key); }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: LDS is in order once the writes landed
+    const float p = lane < k ? fs.pv[lane] : 0.f;
+    const int pid = fs.pi[lane];
+    // sequential sum in rank order; lane j keeps the running sum through j
+    float sum = 0.f, cj = 0.f;
+    for (int j0 = 0; j0 < k; j0 += 8) {
+        float q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), j0 + u));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (j0 + u < k) {
+                sum += q[u];
+                if (lane == j0 + u) cj = sum;
+            }
+    }
+    if (!(sum > 0.0f)) return __builtin_amdgcn_readlane(pid, 0);
+    float r = 0.f;
+    if (lane == 0) r = rand_uniform(rng) * sum;
+    r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 0));
+    const unsigned long long hit2 = __ballot(lane < k && cj >= r);
+    return hit2 ? __builtin_amdgcn_readlane(pid, __ffsll((long long)hit2) - 1) : 0;
+}
+
+// sample_fast_regs on NT threads: thread t owns ids id[j] = t*E + j (j < E).
+template <int NT, int EM>
+__device__ __forceinline__ int sample_fast_nt(FastSmemNT<NT> &fs, const float (&v)[EM], int E, int n, int k,
+                                              uint32_t &rng, uint64_t etab) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x;
+    uint32_t kk[EM];
+    int id[EM];
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        id[j] = tid * E + j;
+        kk[j] = (j < E && id[j] < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
+    }
+    if (k <= KC) {
+        const int t = sample_dist_nt<NT, EM>(fs, v, kk, id, k, rng, etab);
+        if (t != -1) return t;
+        __syncthreads();   // (every thread returned -1 at the same point; hist 0 / 1 were zeroed before barrier 1)
+    } else {
+        if (threadIdx.x < 256) { fs.hist[0][threadIdx.x] = 0; fs.hist[1][threadIdx.x] = 0; }
+        __syncthreads();
+    }
+    uint32_t T, Tm;
+    int take_eq, ne;
+    radix_select_nt<NT, EM>(fs, kk, E, k, T, Tm, take_eq, ne);
+    const int ke = k < ne ? k : ne;
+    if (ke == 0) return 0;
+    int ngt = 0, neq = 0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        if (j < E && kk[j] != 0u) {
+            const uint32_t m = kk[j] & Tm;
+            ngt += m > T;
+            neq += m == T;
+        }
+    }
+    int gt0, eq0;
+    block_scan2_nt<NT>(fs, ngt, neq, gt0, eq0);
+    int pos = gt0 + min(eq0, take_eq);
+    int eqc = eq0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        if (j < E && kk[j] != 0u) {
+            const uint32_t m = kk[j] & Tm;
+            bool take = m > T;
+            if (m == T) { take = eqc < take_eq; ++eqc; }
+            if (take) { fs.sel_v[pos] = v[j]; fs.sel_i[pos] = id[j]; ++pos; }
+        }
+    }
+    __syncthreads();
+    if (ke <= 64) {
+        if (tid < 64) {
+            const int t = wave_sort_draw(fs, ke, rng, etab);
+            if (tid == 0) fs.misc[0] = t;
+        }
+        __syncthreads();
+        const int out = fs.misc[0];
+        __syncthreads();   // fs is reused by a second draw (fixed-mode EOS re-sample)
+        return out;
+    }
+    for (int s2 = tid; s2 < ke; s2 += NT) {
+        const float vs = fs.sel_v[s2];
+        const uint32_t ks = okey(vs);
+        int rk = 0;
+        for (int t = 0; t < ke; ++t) {
+            const uint32_t kt = okey(fs.sel_v[t]);
+            rk += (kt > ks) || (kt == ks && t < s2);
+        }
+        fs.top_v[rk] = vs;
+        fs.top_i[rk] = fs.sel_i[s2];
+    }
+    __syncthreads();
+    const float mx = fs.top_v[0];
+    for (int j = tid; j < ke; j += NT) fs.sel_v[j] = expf_glibc(fs.top_v[j] - mx);
+    __syncthreads();
+    if (tid == 0) {
+        float sum = 0.0f;
+        for (int j = 0; j < ke; ++j) sum += fs.sel_v[j];
+        int out = 0;
+        if (sum > 0.0f) {
+            const float r = rand_uniform(rng) * sum;
+            float c = 0.0f;
+            for (int j = 0; j < ke; ++j) {
+                c += fs.sel_v[j];
+                if (c >= r) { out = fs.top_i[j]; break; }
+            }
+        } else {
+            out = fs.top_i[0];
+        }
+        fs.misc[0] = out;
+    }
+    __syncthreads();
+    const int out = fs.misc[0];
+    __syncthreads();
+    return out;
+}
+
 union KSmem {
     SampSmem full;
     FastSmem fast;
@@ -586,34 +909,55 @@ __host__ __device__ inline bool fast_path(const SampArgs &a) {
     return a.top_p >= 1.0f && a.top_k > 0 && a.top_k < a.n && a.top_k <= KFAST && a.n <= NMAX;
 }
 
-// One row's draw (all 256 threads of the workgroup).  `smraw` >= sizeof(KSmem),
-// or sizeof(FastSmem) with FAST_ONLY (the caller guarantees fast_path(a)).
-// Used by k_sample and, FAST_ONLY, as the tail of the logit-head GEMV.
-template <bool FAST_ONLY, int EM = EMAX>
+// One row's draw (all NT threads of the workgroup).  `smraw` >= sizeof(KSmem),
+// or sizeof(FastSmem) / sizeof(FastSmemNT<NT>) with FAST_ONLY (the caller
+// guarantees fast_path(a)).  Used by k_sample.
+template <bool FAST_ONLY, int EM = EMAX, int NT = 256>
 __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned char *smraw) {
 #pragma clang fp contract(off)
+    static_assert(NT == 256 || FAST_ONLY, "the full path runs on 256 threads");
     KSmem &U = *reinterpret_cast<KSmem *>(smraw);
+    int *misc = NT == 256 ? U.fast.misc : reinterpret_cast<FastSmemNT<NT> *>(smraw)->misc;
     const int tid = threadIdx.x, n = a.n;
-    // every global read of this kernel is issued up front (one round trip);
-    // the row's flags are uniform loads in every thread (no LDS broadcast)
-    const int stopped = a.stopped ? a.stopped[b] : 0;
-    const int ng = a.mode == 1 ? a.n_gen[b] : 0;
-    uint32_t rng = 0;
-    if (tid == 0) rng = a.mode == 1 ? a.rng[b] : a.st_rng[b];
-    const int E = (n + 255) / 256;
+    // every global read of this kernel is issued up front, as VECTOR loads
+    // from unconditional (clamped) addresses: the logits, the repetition
+    // counts, then the row's flags and RNG state (through an opaque zero
+    // offset: as scalar loads they were waited for one after another --
+    // stopped, then the RNG state -- before the first logit load issued)
+    const int E = (n + NT - 1) / NT;
     const float *lg = a.logits + (size_t)b * a.ld;
     const int i0 = tid * E;
     float x[EM];
     int cnt[EM];
     const bool pen = a.mode == 1 && a.rep != 1.0f && a.counts;
+    const int *cbase = pen ? a.counts + (size_t)b * n : reinterpret_cast<const int *>(lg);
 #pragma unroll
     for (int j = 0; j < EM; ++j) {
-        const int i = i0 + j;
-        const bool ok = j < E && i < n;
-        x[j] = ok ? (FAST_ONLY ? ld_sc1(lg + i) : lg[i]) : -INFINITY;   // FAST_ONLY = GEMV tail: sc1 hand-off
-        cnt[j] = (ok && pen) ? a.counts[(size_t)b * n + i] : 0;
+        const int i = i0 + j < n ? i0 + j : n - 1;
+        x[j] = lg[i];
+        cnt[j] = cbase[i];
     }
+    int z0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+    // (an absent flag reads a logit word instead, and is replaced by 0 below)
+    const int *sp = a.stopped ? a.stopped + b : reinterpret_cast<const int *>(lg);
+    const int *np = a.mode == 1 ? a.n_gen + b : reinterpret_cast<const int *>(lg);
+    const uint32_t *rp = (a.mode == 1 ? a.rng : a.st_rng) + b;
+    int stopped = sp[z0];
+    int ng = np[z0];
+    uint32_t rng = rp[z0];
     const uint64_t etab = kExp2fTab[tid & 31];   // expf_glibc_wave's table, with the first loads
+    // one wait for all of them here (the compiler would otherwise sink the
+    // flag loads into the branches that use them: another round trip each)
+    asm volatile("" :: "v"(stopped), "v"(ng), "v"(rng));
+    if (!a.stopped) stopped = 0;
+    if (a.mode != 1) ng = 0;
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        const bool ok = j < E && i0 + j < n;
+        if (!ok) x[j] = -INFINITY;
+        if (!(ok && pen)) cnt[j] = 0;
+    }
     if (stopped) return;
     if (a.mode == 1) {
 #pragma unroll
@@ -633,16 +977,20 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
         float v[EM];
 #pragma unroll
         for (int j = 0; j < EM; ++j) v[j] = div_rn(x[j], temp);
-        tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);   // (wave 0's)
+        auto draw = [&]() {   // (wave 0's id)
+            if constexpr (NT == 256) return sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
+            else return sample_fast_nt<NT, EM>(*reinterpret_cast<FastSmemNT<NT> *>(smraw), v, E, n, a.top_k, rng, etab);
+        };
+        tok = draw();
         if (a.mode == 1 && a.fixed > 0 && ng < a.fixed) {   // Q.c:1315-1321: an EOS draw is redrawn
-            if (tid == 0) U.fast.misc[3] = tok;
+            if (tid == 0) misc[3] = tok;
             __syncthreads();
-            tok = U.fast.misc[3];
+            tok = misc[3];
             if (tok == a.eos) {
 #pragma unroll
                 for (int j = 0; j < EM; ++j)
                     if (i0 + j == a.eos) v[j] = div_rn(-1e9f, temp);
-                tok = sample_fast_regs<EM>(U.fast, v, E, n, a.top_k, rng, etab);
+                tok = draw();
             }
         }
     } else if constexpr (!FAST_ONLY) {

@@ -175,9 +175,12 @@ def test_sampler_golden_bit_exact(gpu, V):
         assert st[0] == rs[i, 1], i
 
 
-def test_sampler_random_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("sw", ["1", "0"])
+def test_sampler_random_vs_oracle(gpu, oracle, monkeypatch, sw):
     """Many draws, ties, -inf, top_p cut, k=0/1/large, batched rows with their
-    own RNG states: ids and RNG state bit-exact."""
+    own RNG states: ids and RNG state bit-exact.  On the 1024-thread fast path
+    (k_sample_w) and the 256-thread one (QTTS_HIP_SAMPLE_W=0)."""
+    monkeypatch.setenv("QTTS_HIP_SAMPLE_W", sw)
     rng = np.random.default_rng(123)
     for it in range(40):
         V = [2048, 3072, 1500, 64][it % 4]
@@ -199,12 +202,15 @@ def test_sampler_random_vs_oracle(gpu, oracle):
             assert st[b] == s.view(np.uint32)[0], (it, b)
 
 
-def test_sampler_candidate_bins_vs_oracle(gpu, oracle):
-    """The k <= 64 distance-binned path (qtts_sample_dev.h sample_dist) and
-    its radix fallback: boundary bins dense with ties (more than 64
-    candidates), every logit equal, +0 / -0 mixtures, ineligible -FLT_MAX
-    entries, values spanning zero, k at the 64 cap and one past it, narrow
-    and wide logit scales; ids and RNG state bit-exact."""
+@pytest.mark.parametrize("sw", ["1", "0"])
+def test_sampler_candidate_bins_vs_oracle(gpu, oracle, monkeypatch, sw):
+    """The k <= 64 distance-binned path (qtts_sample_dev.h sample_dist /
+    sample_dist_nt) and its radix fallback: boundary bins dense with ties
+    (more than 64 candidates), every logit equal, +0 / -0 mixtures,
+    ineligible -FLT_MAX entries, values spanning zero, k at the 64 cap and
+    one past it, narrow and wide logit scales; ids and RNG state bit-exact.
+    On the 1024-thread fast path and the 256-thread one (QTTS_HIP_SAMPLE_W=0)."""
+    monkeypatch.setenv("QTTS_HIP_SAMPLE_W", sw)
     rng = np.random.default_rng(7)
     fmax = np.finfo(np.float32).max
     cases = []

@@ -4,9 +4,12 @@ Fixtures (tests/golden/make_golden_long.py, from the reference c/ build):
 
 * `long_hd128.npz` -- the `hd128` synthetic model (the talker's real attention
   shape NH 16 / KV 8 / HD 128, 2 narrow layers): a 640-frame default-sampling
-  decode.  `k_attn_dec` takes 64-key splits at HD 128, so the talker positions
-  (38 .. 678) run through the 1-split path, the 2-8-split merge and the
-  > 8-split serial merge (k_attn.hip); the codes must be bit-exact all the
+  decode, talker positions 38 .. 678.  At batch 1 `k_attn_dec` takes 32-key
+  splits whose merge runs in the O projection's prologue (up to 22 splits
+  here); the batch-3 test runs the 64-key splits the kernel merges itself,
+  through the 1-split, 2-8-split and > 8-split merges.  QTTS_HIP_ATTN_DEFER=0
+  (batch 1 merging its own 64-key splits) runs all 640 frames, so batch 1
+  also reaches > 8 splits of 64 keys.  The codes must be bit-exact all the
   way.  A 600-row prefill (> 512 rows) and 4 decode steps over 600+ keys.
 * `long_17b.npz` -- the benchmark workload itself (bench.py): synthetic 1.7B,
   P128 prompt, fixed 128 frames, default sampling, seed 42.
@@ -173,21 +176,23 @@ def test_c4_batch8_lock_step_vs_reference(gpu, monkeypatch, env):
         m.close()
 
 
-@pytest.mark.parametrize("env", [{"QTTS_HIP_ATTN_DEFER": "0"}, {"QTTS_HIP_ATTN_LPK": "4"},
-                                 {"QTTS_HIP_ATTN_LPK": "16"}])
-def test_hd128_attention_switch_paths_vs_reference(gpu, monkeypatch, env):
-    """The talker attention's A/B switches at HD 128, 300 frames (positions
-    to 338: the 1-, 2-8- and > 8-split merges of 64- / 32- / 16-key splits):
-    the merge in the last split instead of the O projection's prologue, and
-    the other split sizes -- codes bit-exact against the reference's."""
+@pytest.mark.parametrize("env,frames", [({"QTTS_HIP_ATTN_DEFER": "0"}, 640), ({"QTTS_HIP_ATTN_LPK": "4"}, 300),
+                                        ({"QTTS_HIP_ATTN_LPK": "16"}, 300)])
+def test_hd128_attention_switch_paths_vs_reference(gpu, monkeypatch, env, frames):
+    """The talker attention's A/B switches at HD 128: the merge in the last
+    split instead of the O projection's prologue (64-key splits, all 640
+    frames: positions to 678, so batch 1 runs the 1-, 2-8- and > 8-split
+    merges), and the other split sizes of the deferred merge (64- / 16-key
+    splits, 300 frames) -- codes bit-exact against the reference's.  The
+    split size is latched at model creation (the scratch is sized by it)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = np.load(os.path.join(GOLDEN, "long_hd128.npz"))
     man = _man()["hd128"]
     m = qtts.QwenTTS(model_dir("hd128"))
     try:
-        m.set_params(max_tokens=4096, fixed=300, seed=man["seed"], **DEFAULT)
+        m.set_params(max_tokens=4096, fixed=frames, seed=man["seed"], **DEFAULT)
         m.generate(g["prompt_ids"], "aiden", "english")
-        _codes_equal(m.last_codes(), g["decode_codes"][:300], f"hd128 300 frames {env}")
+        _codes_equal(m.last_codes(), g["decode_codes"][:frames], f"hd128 {frames} frames {env}")
     finally:
         m.close()

@@ -38,7 +38,16 @@ python3 $R/tools/prof_summary.py $O
 cp $O/kernel_stats.csv $R/profiles/${TAG}_kernel_stats.csv
 cp $O/pmc.json $R/profiles/${TAG}_pmc.json
 echo $TAG > $R/profiles/LATEST
+# BASELINE configs[1] (C2): 0.6B, batch 1, greedy -- its own profile passes
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/c2/prof -o run -- python3 $R/bench.py --preset 0.6b --greedy --no-cpu-baseline > $O/prof_bench_06b.json 2> $O/prof_bench_06b.err
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/c2/pmc_fetch -o run -- python3 $R/bench.py --preset 0.6b --greedy --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch_06b.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $O/c2/pmc_write -o run -- python3 $R/bench.py --preset 0.6b --greedy --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_write_06b.log 2>&1
+python3 $R/tools/prof_summary.py $O/c2
+cp $O/c2/kernel_stats.csv $R/profiles/${TAG}_06b_kernel_stats.csv
+cp $O/c2/pmc.json $R/profiles/${TAG}_06b_pmc.json
 cd $R
+timeout -k 10 900 python bench.py --preset 0.6b --greedy > $O/bench_06b.json 2> $O/bench_06b.err
+cp $O/bench_06b.json $R/profiles/${TAG}_bench_06b.json
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
 # BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8
 timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 > $O/bench_vc8.json 2> $O/bench_vc8.err

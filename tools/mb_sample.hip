@@ -11,6 +11,10 @@
 //   12 + distance histogram (barrier 2), merged-histogram scan
 //   13 + candidate compaction (barrier 3)
 //   14 = the whole draw (wave 0 ranks, sums, draws)
+// and the same on 1024 threads (sample_dist_nt, 2 ids per thread):
+//   21 + max / count (barrier 1)   22 + shared histogram, scan (barrier 2)
+//   23 + candidate slots (barrier 3)  24 + rank slices (barrier 4)
+//   25 = the whole draw              26 = k_sample_w's sample_fast_nt
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iqwen3-tts-c_amd/csrc/hip tools/mb_sample.hip -o tools/mb_sample
 #include "qtts_sample_dev.h"
@@ -64,12 +68,45 @@ __global__ __launch_bounds__(256) void k_phase(SampArgs a, float *sink) {
 }
 
 template <int PHASE>
+__global__ __launch_bounds__(1024) void k_phase_w(SampArgs a, float *sink) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    FastSmemNT<1024> &fs = *reinterpret_cast<FastSmemNT<1024> *>(smraw);
+    const int tid = threadIdx.x;
+    constexpr int EM = 2;
+    const int n = a.n, E = (n + 1023) / 1024;
+    float v[EM];
+    uint32_t kk[EM];
+    int id[EM];
+    float raw[EM];
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        id[j] = tid * E + j;
+        raw[j] = a.logits[id[j] < n ? id[j] : n - 1];   // every load in flight at once
+    }
+#pragma unroll
+    for (int j = 0; j < EM; ++j) {
+        v[j] = (j < E && id[j] < n) ? div_rn(raw[j], a.temp) : -INFINITY;
+        kk[j] = (j < E && id[j] < n && v[j] > -FLT_MAX) ? okey(v[j]) : 0u;
+    }
+    uint32_t rng = 0x42280000u;
+    const uint64_t etab = kExp2fTab[tid & 31];
+    int t;
+    if constexpr (PHASE == 26) t = sample_fast_nt<1024, EM>(fs, v, E, n, a.top_k, rng, etab);
+    else t = sample_dist_nt<1024, EM, PHASE - 20>(fs, v, kk, id, a.top_k, rng, etab);
+    if (tid == 0) sink[0] = (float)t;
+}
+
+template <int PHASE>
 static float time_phase(const SampArgs &a, float *sink, hipStream_t st) {
     hipGraph_t g;
     hipGraphExec_t ge;
     CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
-    for (int i = 0; i < 200; ++i)
-        hipLaunchKernelGGL((k_phase<PHASE>), dim3(1), dim3(256), sizeof(FastSmem), st, a, sink);
+    for (int i = 0; i < 200; ++i) {
+        if constexpr (PHASE > 20)
+            hipLaunchKernelGGL((k_phase_w<PHASE>), dim3(1), dim3(1024), sizeof(FastSmemNT<1024>), st, a, sink);
+        else
+            hipLaunchKernelGGL((k_phase<PHASE>), dim3(1), dim3(256), sizeof(FastSmem), st, a, sink);
+    }
     CK(hipStreamEndCapture(st, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     CK(hipGraphLaunch(ge, st));
@@ -112,5 +149,11 @@ int main() {
     printf("dist 12 + histogram, scan   %6.2f us\n", time_phase<12>(a, sink, st));
     printf("dist 13 + compaction        %6.2f us\n", time_phase<13>(a, sink, st));
     printf("dist 14 = whole draw        %6.2f us\n", time_phase<14>(a, sink, st));
+    printf("w1024 21 + max / count      %6.2f us\n", time_phase<21>(a, sink, st));
+    printf("w1024 22 + histogram, scan  %6.2f us\n", time_phase<22>(a, sink, st));
+    printf("w1024 23 + candidate slots  %6.2f us\n", time_phase<23>(a, sink, st));
+    printf("w1024 24 + rank slices      %6.2f us\n", time_phase<24>(a, sink, st));
+    printf("w1024 25 = whole draw       %6.2f us\n", time_phase<25>(a, sink, st));
+    printf("w1024 26 sample_fast_nt     %6.2f us\n", time_phase<26>(a, sink, st));
     return 0;
 }
