@@ -18,6 +18,7 @@
 #include "qtts_attn_dev.h"
 #include "qtts_common.h"
 #include "qtts_kernels.h"
+#include "qtts_l2pf.h"
 
 namespace {
 
@@ -561,9 +562,11 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     // issued right behind the attention's own loads
     v4u wv[NJ];
     const bf16_t *wr = Wo + (size_t)rowc * AD + W2 * kvh + 8 * sub;
+    L2PfRegs pfr;   // the next launch's weight slice (AttnArgs::pf), behind the W_o fragment
     auto issue = [&]() {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
+        qtts_l2pf_issue<256>(t.pf, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), pfr, Wo);
     };
     attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0, issue);
     __syncthreads();
@@ -582,6 +585,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
     }
     acc = group_sum<LPS>(acc);
     if (sub == 0 && row < R) part[((size_t)kvh * gridDim.z + b) * R + row] = acc;
+    qtts_l2pf_sink(t.pf, pfr);
 }
 
 }  // namespace

@@ -30,6 +30,7 @@
 // its up row (r + 4), so the product is formed in registers.
 #include "qtts_common.h"
 #include "qtts_kernels.h"
+#include "qtts_l2pf.h"
 
 namespace {
 
@@ -158,6 +159,9 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
             else wv[i][k] = p[64 * k];
         }
     }
+    // 2b. the next launch's weight slice into this XCD's L2 (GemvArgs::pf)
+    L2PfRegs pfr;
+    qtts_l2pf_issue<256>(a.pf, blockIdx.x + gridDim.x * blockIdx.y, pfr, W);
 
     if constexpr (AM) {   // 3a. the attention merge, split order (k_attn_dec's last-split merge)
         const int HDm = a.am_hd, GP = a.am_gph, NO = GP * HDm, stride = NO + 2 * GP;
@@ -257,25 +261,27 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
         acc[i] = wave_sum(s);
     }
     gw_stamp(a, 2);
-    if (lane != 0) return;
+    if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
-        const int r = row0 + w + 4 * i;
-        const float v = acc[i];
-        switch (a.epi) {
-            case EPI_STORE: y[r] = v; break;
-            case EPI_BIAS: y[r] = v + a.bias[r]; break;
-            case EPI_BIAS_SILU: {
-                const float z = v + a.bias[r];
-                y[r] = z / (1.0f + expf(-z));
-                break;
+        for (int i = 0; i < RW; ++i) {
+            const int r = row0 + w + 4 * i;
+            const float v = acc[i];
+            switch (a.epi) {
+                case EPI_STORE: y[r] = v; break;
+                case EPI_BIAS: y[r] = v + a.bias[r]; break;
+                case EPI_BIAS_SILU: {
+                    const float z = v + a.bias[r];
+                    y[r] = z / (1.0f + expf(-z));
+                    break;
+                }
+                case EPI_RESID: y[r] = yres[i] + v; break;
+                case EPI_SWIGLU:
+                    if ((i & 1) == 0 && i + 1 < RW) y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * acc[i + 1];
+                    break;
             }
-            case EPI_RESID: y[r] = yres[i] + v; break;
-            case EPI_SWIGLU:
-                if ((i & 1) == 0 && i + 1 < RW) y[(r >> 3) * 4 + (r & 3)] = (v / (1.0f + expf(-v))) * acc[i + 1];
-                break;
         }
     }
+    qtts_l2pf_sink(a.pf, pfr);   // (after the stores: the prefetch is off this launch's own path)
 }
 
 }  // namespace

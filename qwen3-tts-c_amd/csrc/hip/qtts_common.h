@@ -209,3 +209,4 @@ __device__ __forceinline__ void st_sc1(float *p, float v) {
 __device__ __forceinline__ float ld_sc1(const float *p) {
     return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+

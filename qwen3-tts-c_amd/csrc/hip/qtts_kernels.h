@@ -9,6 +9,23 @@ constexpr int QTTS_GM_TICKS = 1024;   // self-reducing split-K tickets (row bloc
 
 enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SILU = 2, EPI_RESID = 3, EPI_SWIGLU = 4 };
 
+// The next launch's weight slice, loaded by the SAME workgroup index of this
+// launch right after its own weights (qtts_l2pf below): workgroup b of every
+// decode launch runs on XCD b % 8, so the slice lands in the L2 that the next
+// launch's workgroup b reads from.  For linear workgroup id b:
+//   start = base + (b % pm) * pa + (b / pm) * pb,
+//   `chunks` 64-B chunks: chunk c at start + (c >> lg) * ld + (c & (2^lg - 1)) * 64
+// (rows of 2^lg chunks at stride ld; chunks <= threads x QTTS_PF_LOADS).  One
+// 4-B load per chunk brings its line in.
+constexpr int QTTS_PF_LOADS = 4;
+struct L2Prefetch {
+    const unsigned char *base = nullptr;   // nullptr: none
+    int pm = 1 << 30;
+    long long pa = 0, pb = 0;
+    int chunks = 0, lg = 30, ld = 0;
+    unsigned *sink = nullptr;              // never written (the loads' values are folded into a test)
+};
+
 struct GemvArgs {
     const bf16_t *W = nullptr;  // [R, C] bf16 row-major
     int R = 0, C = 0;
@@ -62,6 +79,7 @@ struct GemvArgs {
     const float *bias = nullptr;
     int epi = EPI_STORE;
     unsigned long long *dbg = nullptr;   // diagnostics (k_gemvb): [workgroup][8] phase stamps, 100 MHz clock
+    L2Prefetch pf;                      // batch-1 lean kernel (k_gemvw): the next launch's weights
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {
         if (xadd && (((uintptr_t)xadd & 15) || ld_xadd % 4 || n_xadd < 1)) return false;
@@ -115,6 +133,7 @@ struct AttnArgs {
     // and the merge is the consumer's (GemvArgs::amerge, the O projection's
     // prologue) instead of the last split's
     int defer = 0;
+    L2Prefetch pf;                 // k_attn_o: the next launch's weights
     // lanes per key of the split kernel at HD 128 (4 / 8 / 16), latched by the
     // model at creation (QTTS_HIP_ATTN_LPK); 0 = the default for HD / defer
     int lpk = 0;

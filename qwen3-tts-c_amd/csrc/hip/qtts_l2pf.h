@@ -1,0 +1,35 @@
+// qtts_l2pf.h - device side of L2Prefetch (qtts_kernels.h).
+#pragma once
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+// The next launch's weight slice into this XCD's L2 (L2Prefetch,
+// qtts_kernels.h): QTTS_PF_LOADS 4-B loads per thread (one per 64-B chunk), issued right after
+// the kernel's own weight loads, every one unconditional (an absent or short
+// slice re-reads its first chunk: a branch between loads would make the
+// compiler wait for all of them).  The values are folded into `acc`, which
+// qtts_l2pf_sink tests at the end of the kernel.
+struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
+template <int NT>
+__device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
+    const unsigned char *st = p.base ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
+                                     : reinterpret_cast<const unsigned char *>(fallback);
+    const unsigned m = (1u << p.lg) - 1u, n = (unsigned)p.chunks;
+    // offsets first (selects, no exec-masked branches: those made the compiler
+    // reuse an in-flight load's registers and wait for every load), then the loads
+    unsigned off[QTTS_PF_LOADS];
+#pragma unroll
+    for (int j = 0; j < QTTS_PF_LOADS; ++j) {
+        const unsigned c0 = threadIdx.x + NT * j;
+        const unsigned c = c0 < n ? c0 : 0u;
+        off[j] = (c >> p.lg) * (unsigned)p.ld + ((c & m) << 6);
+    }
+#pragma unroll
+    for (int j = 0; j < QTTS_PF_LOADS; ++j) r.v[j] = *reinterpret_cast<const unsigned *>(st + off[j]);
+}
+__device__ __forceinline__ void qtts_l2pf_sink(const L2Prefetch &p, const L2PfRegs &r) {
+    unsigned acc = 0;
+#pragma unroll
+    for (int j = 0; j < QTTS_PF_LOADS; ++j) acc ^= r.v[j];
+    if (acc == 0x9E3779B9u && p.sink) p.sink[0] = acc;
+}

@@ -164,6 +164,8 @@ struct qtts_dev {
     std::vector<Prof> prof;
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
+    bool l2pf = true;        // QTTS_HIP_L2PF=0: no next-launch weight prefetch in the batch-1 sub-talker chain
+    unsigned *pf_sink = nullptr;
     bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
     int attn_lpk = 0;        // QTTS_HIP_ATTN_LPK=4|8|16 (HD 128 split size), latched here: sizes att_part
     // QTTS_HIP_GM_DBG=<layer>: phase stamps of that talker layer's batch GEMVs
@@ -386,6 +388,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_lpk = lk ? atoi(lk) : 0;
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
+    const char *pf = getenv("QTTS_HIP_L2PF");
+    dv->l2pf = !(pf && !atoi(pf));
     const char *gd = getenv("QTTS_HIP_GM_DBG");
     if (gd) dv->gm_dbg_layer = atoi(gd);
     codec_init(&dv->codec, dims, dv->st);
@@ -599,6 +603,7 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         const int kvmax = d.KV > d.KVs ? d.KV : d.KVs;
         A(att_cnt, int, B * kvmax);
         CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
+        A(pf_sink, unsigned, 1);
         A(btick, int, QTTS_GM_TICKS);
         CK(hipMemsetAsync(dv->btick, 0, QTTS_GM_TICKS * sizeof(int), dv->st));
         if (dv->gm_dbg_layer >= 0) {
@@ -943,6 +948,31 @@ static int talker_head_sample(qtts_dev *dv) {
     return head_sample(dv, a, s, PK_GEMV_TALKER);
 }
 
+// Next-launch weight slices (L2Prefetch): what workgroup b of the NEXT launch
+// reads, for the two launch shapes of the batch-1 sub-talker chain
+//   k_gemvw (grid 256): rows [b R / 256, (b + 1) R / 256), contiguous
+static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C) {
+    L2Prefetch p;
+    if (!dv->l2pf || R % 256) return p;
+    const long long bytes = (long long)(R / 256) * C * 2;
+    if (bytes % 64 || bytes / 64 > 256 * QTTS_PF_LOADS) return p;
+    p.base = reinterpret_cast<const unsigned char *>(W);
+    p.pa = bytes; p.pb = 0; p.chunks = (int)(bytes / 64); p.lg = 30; p.ld = 0; p.sink = dv->pf_sink;
+    return p;
+}
+//   k_attn_o (grid (R / RPW, KV), linear b = rb + (R / RPW) kvh): rows
+//   [RPW rb, +RPW) x columns [2 HD kvh, +2 HD) of W_o [R][NH HD]
+static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH, int HD) {
+    L2Prefetch p;
+    const int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
+    const int cpr = W2 * 2 / 64;   // 64-B chunks per row slice
+    if (!dv->l2pf || R % RPW || (cpr & (cpr - 1)) || cpr < 1 || RPW * cpr > 256 * QTTS_PF_LOADS) return p;
+    p.base = reinterpret_cast<const unsigned char *>(Wo);
+    p.pm = R / RPW; p.pa = (long long)RPW * NH * HD * 2; p.pb = W2 * 2;
+    p.chunks = RPW * cpr; p.lg = __builtin_ctz(cpr); p.ld = NH * HD * 2; p.sink = dv->pf_sink;
+    return p;
+}
+
 // 16 sub-talker passes (T.c:539-736)
 static int subtalker(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
@@ -950,6 +980,15 @@ static int subtalker(qtts_dev *dv) {
     const int cstride = (dv->max_frames + 1) * d.G;
     hipStream_t st = dv->st;
     const bool proj = dv->st_proj != nullptr;
+    // batch 1, fused attention + O: each launch also pulls the next launch's
+    // weight slice into its XCD's L2 (GemvArgs::pf / AttnArgs::pf)
+    const bool pfon = nb == 1 && dv->attn_o && dv->l2pf;
+    const bool tab0_ok = nb == 1 && dv->attn_o && dv->qkv0_tab && (!proj || dv->st_ptab);
+    auto first_op_pf = [&](int gn) {   // pass gn's first launch (layer 0: the table attention or q|k|v)
+        if (!pfon || gn >= d.G) return L2Prefetch();
+        if (gn >= 1 && tab0_ok) return pf_attn_o(dv, dv->sl[0].wo, d.Hs, d.NHs, d.HDs);
+        return pf_gemvw(dv, dv->sl[0].wqkv, QKV, d.Hs);
+    };
     for (int g = 0; g < d.G; ++g) {
         // input source for this pass
         GemvArgs src;  // x / table description only
@@ -1023,6 +1062,10 @@ static int subtalker(qtts_dev *dv) {
                 t.tab_ids = src.ids; t.tab_bstride = src.ids_bstride; t.tab_row_sel = src.row_sel;
                 t.tab_rstride = src.ids_rstride; t.tab_off = src.ids_off;
             }
+            if (pfon) {
+                a.pf = pf_attn_o(dv, ly.wo, d.Hs, d.NHs, d.HDs);
+                t.pf = kv_only ? first_op_pf(g + 1) : pf_gemvw(dv, ly.wgu, 2 * d.Is, d.Hs);
+            }
             if (dv->attn_o && nb == 1) {
                 if (!tab0) CKI(pgemv(dv, a, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
@@ -1048,6 +1091,7 @@ static int subtalker(qtts_dev *dv) {
             if (kv_only) break;
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
+            if (pfon) a.pf = pf_gemvw(dv, ly.wdown, d.Hs, d.Is);
             if (sdbg) a.dbg = dv->gm_dbg + 2 * 2048 * 8;
             if (tab0) set_src(a);   // the residual is the input table row (x_st was not written)
             if (fused_o) {
@@ -1059,6 +1103,10 @@ static int subtalker(qtts_dev *dv) {
             if (fused_o || opend) std::swap(xa, xb);
             a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xa, d.Hs, nb, EPI_RESID);
             a.nt = 0;
+            if (pfon) {
+                if (l + 1 < d.Ls) a.pf = pf_gemvw(dv, dv->sl[l + 1].wqkv, QKV, d.Hs);
+                else if (g >= 1) a.pf = pf_gemvw(dv, dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs);
+            }
             if (sdbg) a.dbg = dv->gm_dbg + 3 * 2048 * 8;
             if (kzd && split_out(dv, a, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
@@ -1068,6 +1116,7 @@ static int subtalker(qtts_dev *dv) {
                         EPI_STORE);
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
         if (pend) add_in(a, pend, npend, d.Hs, nb, nullptr);
+        a.pf = first_op_pf(g + 1);   // (two launches ahead: the sampler runs in between)
         SampArgs s;
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
