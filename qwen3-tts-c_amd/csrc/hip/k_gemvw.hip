@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
     }
     // 2b. the next launch's weight slice into this XCD's L2 (GemvArgs::pf)
     L2PfRegs pfr;
-    qtts_l2pf_issue<256>(a.pf, blockIdx.x + gridDim.x * blockIdx.y, pfr, W);
+    qtts_l2pf_issue<256, NT>(a.pf, blockIdx.x + gridDim.x * blockIdx.y, pfr, W);
 
     if constexpr (AM) {   // 3a. the attention merge, split order (k_attn_dec's last-split merge)
         const int HDm = a.am_hd, GP = a.am_gph, NO = GP * HDm, stride = NO + 2 * GP;

@@ -10,7 +10,9 @@
 // compiler wait for all of them).  The values are folded into `acc`, which
 // qtts_l2pf_sink tests at the end of the kernel.
 struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
-template <int NT>
+// NTL: non-temporal loads (the talker's read-once weights: they must not
+// displace the sub-talker's weights from the Infinity Cache)
+template <int NT, bool NTL = false>
 __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
     const unsigned char *st = p.base ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
                                      : reinterpret_cast<const unsigned char *>(fallback);
@@ -25,7 +27,11 @@ __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2Pf
         off[j] = (c >> p.lg) * (unsigned)p.ld + ((c & m) << 6);
     }
 #pragma unroll
-    for (int j = 0; j < QTTS_PF_LOADS; ++j) r.v[j] = *reinterpret_cast<const unsigned *>(st + off[j]);
+    for (int j = 0; j < QTTS_PF_LOADS; ++j) {
+        const unsigned *q = reinterpret_cast<const unsigned *>(st + off[j]);
+        if constexpr (NTL) r.v[j] = __builtin_nontemporal_load(q);
+        else r.v[j] = *q;
+    }
 }
 __device__ __forceinline__ void qtts_l2pf_sink(const L2Prefetch &p, const L2PfRegs &r) {
     unsigned acc = 0;

@@ -165,6 +165,7 @@ struct qtts_dev {
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
     bool l2pf = true;        // QTTS_HIP_L2PF=0: no next-launch weight prefetch in the batch-1 sub-talker chain
+    int l2pf_tk = 0;         // QTTS_HIP_L2PF_TK bits (batch-1 talker, non-temporal): 1 q|k|v -> O's W_o, 2 O -> gate|up
     unsigned *pf_sink = nullptr;
     bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
     int attn_lpk = 0;        // QTTS_HIP_ATTN_LPK=4|8|16 (HD 128 split size), latched here: sizes att_part
@@ -390,6 +391,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_o = !(ao && !atoi(ao));
     const char *pf = getenv("QTTS_HIP_L2PF");
     dv->l2pf = !(pf && !atoi(pf));
+    const char *pft = getenv("QTTS_HIP_L2PF_TK");
+    if (pft) dv->l2pf_tk = atoi(pft);
     const char *gd = getenv("QTTS_HIP_GM_DBG");
     if (gd) dv->gm_dbg_layer = atoi(gd);
     codec_init(&dv->codec, dims, dv->st);
@@ -855,6 +858,36 @@ static void add_in(GemvArgs &g, const float *part, int n, int R, int nrun, float
     if (xnew) { g.xcopy = xnew; g.ldxc = R; g.xcopy_normed = 0; }
 }
 
+// Next-launch weight slices (L2Prefetch): what workgroup b of the NEXT launch
+// reads, for the two launch shapes of the batch-1 sub-talker chain
+//   k_gemvw (grid 256): rows [b R / 256, (b + 1) R / 256), contiguous
+//   (a next launch of `grid` workgroups, 256 or 512: this launch's workgroup b
+//   < 256 takes the first cap bytes of the next one's workgroup b -- b and
+//   b + 256 share an XCD, so a 512 grid is half covered)
+static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C, int grid = 256, bool on = true) {
+    L2Prefetch p;
+    if (!on || R % grid) return p;
+    long long bytes = (long long)(R / grid) * C * 2;
+    if (bytes > 64LL * 256 * QTTS_PF_LOADS) bytes = 64LL * 256 * QTTS_PF_LOADS;
+    if (bytes % 64) return p;
+    p.base = reinterpret_cast<const unsigned char *>(W);
+    p.pa = (long long)(R / grid) * C * 2; p.pb = 0; p.chunks = (int)(bytes / 64); p.lg = 30; p.ld = 0;
+    p.sink = dv->pf_sink;
+    return p;
+}
+//   k_attn_o (grid (R / RPW, KV), linear b = rb + (R / RPW) kvh): rows
+//   [RPW rb, +RPW) x columns [2 HD kvh, +2 HD) of W_o [R][NH HD]
+static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH, int HD) {
+    L2Prefetch p;
+    const int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
+    const int cpr = W2 * 2 / 64;   // 64-B chunks per row slice
+    if (!dv->l2pf || R % RPW || (cpr & (cpr - 1)) || cpr < 1 || RPW * cpr > 256 * QTTS_PF_LOADS) return p;
+    p.base = reinterpret_cast<const unsigned char *>(Wo);
+    p.pm = R / RPW; p.pa = (long long)RPW * NH * HD * 2; p.pb = W2 * 2;
+    p.chunks = RPW * cpr; p.lg = __builtin_ctz(cpr); p.ld = NH * HD * 2; p.sink = dv->pf_sink;
+    return p;
+}
+
 static int talker_layers(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     const int nb = dv->nrun, NBA = dv->nb, QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
@@ -883,6 +916,8 @@ static int talker_layers(qtts_dev *dv) {
         t.defer = defer;
         const bool dbg = dv->gm_dbg && l == dv->gm_dbg_layer;
         if (dbg) a.dbg = dv->gm_dbg;
+        // (batch 1: the O projection's slices two launches ahead, the attention in between)
+        if (nb == 1 && (dv->l2pf_tk & 1)) a.pf = pf_gemvw(dv, ly.wo, d.H, AD);
         CKI(qkv_attn(dv, a, t, PK_GEMV_TALKER));
         if (pend) { std::swap(xa, xb); pend = nullptr; }
         GemvArgs o = gv(ly.wo, d.H, AD, dv->att, AD, xa, d.H, nb, EPI_RESID);
@@ -898,6 +933,7 @@ static int talker_layers(qtts_dev *dv) {
         // add up to 8 rows, where self-reduction measured slower)
         const int tk_self = 2;
         const bool opend = kzo && split_out(dv, o, dv->bpo, kzo, tk_self);
+        if (nb == 1 && (dv->l2pf_tk & 2)) o.pf = pf_gemvw(dv, ly.wgu, 2 * d.I, d.H, 512);
         CKI(pgemv(dv, o, PK_GEMV_TALKER));
         a = gv(ly.wgu, 2 * d.I, d.H, xa, d.H, dv->hbuf, d.I, nb, EPI_SWIGLU);
         a.norm_w = ly.post; a.eps = d.eps;
@@ -946,31 +982,6 @@ static int talker_head_sample(qtts_dev *dv) {
     s.st_rng = dv->st_rng; s.seed_bits = seed_bits(dv->par.seed);
     s.codes = dv->codes; s.codes_bstride = (dv->max_frames + 1) * d.G; s.G = d.G; s.out_tok = dv->last_tok;
     return head_sample(dv, a, s, PK_GEMV_TALKER);
-}
-
-// Next-launch weight slices (L2Prefetch): what workgroup b of the NEXT launch
-// reads, for the two launch shapes of the batch-1 sub-talker chain
-//   k_gemvw (grid 256): rows [b R / 256, (b + 1) R / 256), contiguous
-static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C) {
-    L2Prefetch p;
-    if (!dv->l2pf || R % 256) return p;
-    const long long bytes = (long long)(R / 256) * C * 2;
-    if (bytes % 64 || bytes / 64 > 256 * QTTS_PF_LOADS) return p;
-    p.base = reinterpret_cast<const unsigned char *>(W);
-    p.pa = bytes; p.pb = 0; p.chunks = (int)(bytes / 64); p.lg = 30; p.ld = 0; p.sink = dv->pf_sink;
-    return p;
-}
-//   k_attn_o (grid (R / RPW, KV), linear b = rb + (R / RPW) kvh): rows
-//   [RPW rb, +RPW) x columns [2 HD kvh, +2 HD) of W_o [R][NH HD]
-static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH, int HD) {
-    L2Prefetch p;
-    const int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
-    const int cpr = W2 * 2 / 64;   // 64-B chunks per row slice
-    if (!dv->l2pf || R % RPW || (cpr & (cpr - 1)) || cpr < 1 || RPW * cpr > 256 * QTTS_PF_LOADS) return p;
-    p.base = reinterpret_cast<const unsigned char *>(Wo);
-    p.pm = R / RPW; p.pa = (long long)RPW * NH * HD * 2; p.pb = W2 * 2;
-    p.chunks = RPW * cpr; p.lg = __builtin_ctz(cpr); p.ld = NH * HD * 2; p.sink = dv->pf_sink;
-    return p;
 }
 
 // 16 sub-talker passes (T.c:539-736)

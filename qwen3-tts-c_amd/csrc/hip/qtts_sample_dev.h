@@ -682,7 +682,7 @@ __device__ __forceinline__ void radix_select_nt(FastSmemNT<NT> &fs, const uint32
 // Top-k draw for k <= KC (see sample_dist): returns the id in wave 0 (0 in
 // the other waves), or -1 in every thread when more than KC keys share the
 // bins through the k-th key's.  Four barriers.
-template <int NT, int EM, int STOP = 5>
+template <int NT, int EM, int STOP = 9>
 __device__ __forceinline__ int sample_dist_nt(FastSmemNT<NT> &fs, const float (&v)[EM], const uint32_t (&kk)[EM],
                                               const int (&id)[EM], int k, uint32_t &rng, uint64_t etab) {
 #pragma clang fp contract(off)
@@ -780,28 +780,33 @@ __device__ __forceinline__ int sample_dist_nt(FastSmemNT<NT> &fs, const float (&
     if constexpr (STOP == 4) return fs.crank[lane];
     const int rank = fs.crank[lane];
     if (lane < nc && rank < k) { fs.pv[rank] = e; fs.pi[rank] = (int)(0xFFFFFFFFu - (uint32_t)key); }
+    if (lane >= k) fs.pv[lane] = 0.f;   // (adding +0 leaves every running sum as it is)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: LDS is in order once the writes landed
-    const float p = lane < k ? fs.pv[lane] : 0.f;
-    const int pid = fs.pi[lane];
-    // sequential sum in rank order; lane j keeps the running sum through j
-    float sum = 0.f, cj = 0.f;
-    for (int j0 = 0; j0 < k; j0 += 8) {
-        float q[8];
+    // every lane holds all 64 p_j (broadcast reads) and walks them in rank
+    // order: the sum, then the running sum to the first j with c_j >= r --
+    // plain dependent adds in registers (a v_readlane per step cost ~30 ns)
+    float4 q[KC / 4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) q[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), j0 + u));
+    for (int i = 0; i < KC / 4; ++i) q[i] = reinterpret_cast<const float4 *>(fs.pv)[i];
+    if constexpr (STOP == 5) return (int)q[0].x;
+    float sum = 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (j0 + u < k) {
-                sum += q[u];
-                if (lane == j0 + u) cj = sum;
-            }
-    }
-    if (!(sum > 0.0f)) return __builtin_amdgcn_readlane(pid, 0);
+    for (int i = 0; i < KC / 4; ++i) { sum += q[i].x; sum += q[i].y; sum += q[i].z; sum += q[i].w; }
+    if constexpr (STOP == 6) return (int)sum;
+    if (!(sum > 0.0f)) return fs.pi[0];
     float r = 0.f;
     if (lane == 0) r = rand_uniform(rng) * sum;
     r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 0));
-    const unsigned long long hit2 = __ballot(lane < k && cj >= r);
-    return hit2 ? __builtin_amdgcn_readlane(pid, __ffsll((long long)hit2) - 1) : 0;
+    float cs = 0.f;
+    int jf = -1;
+#pragma unroll
+    for (int i = 0; i < KC / 4; ++i) {
+        cs += q[i].x; jf = (jf < 0 && cs >= r) ? 4 * i : jf;
+        cs += q[i].y; jf = (jf < 0 && cs >= r) ? 4 * i + 1 : jf;
+        cs += q[i].z; jf = (jf < 0 && cs >= r) ? 4 * i + 2 : jf;
+        cs += q[i].w; jf = (jf < 0 && cs >= r) ? 4 * i + 3 : jf;
+    }
+    return jf >= 0 ? fs.pi[jf] : 0;
 }
 
 // sample_fast_regs on NT threads: thread t owns ids id[j] = t*E + j (j < E).

@@ -331,12 +331,14 @@ def test_cli_stream_flag(tiny_dir):
     assert re.search(r"First packet: [\d.]+ ms", r.stderr)
 
 
-@pytest.mark.parametrize("env", [{"QTTS_HIP_PTAB": "0"}, {"QTTS_HIP_ATTN_O": "0"}, {"QTTS_HIP_NO_GRAPH": "1"}])
+@pytest.mark.parametrize("env", [{"QTTS_HIP_PTAB": "0"}, {"QTTS_HIP_ATTN_O": "0"}, {"QTTS_HIP_NO_GRAPH": "1"},
+                                 {"QTTS_HIP_L2PF": "0"}, {"QTTS_HIP_SAMPLE_W": "0"}])
 def test_e2e_debug_switch_paths(tiny_dir, monkeypatch, env):
     """The debug switches' paths stay bit-exact: the per-pass input projection
     instead of the projected tables, sub-talker attention and O projection as
-    two kernels, eager launches instead of the frame graphs (the default path
-    is covered by test_e2e_codes_bit_exact_and_audio)."""
+    two kernels, eager launches instead of the frame graphs, no next-launch
+    L2 prefetch, the 256-thread sampler (the default path is covered by
+    test_e2e_codes_bit_exact_and_audio)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     m = qtts.QwenTTS(tiny_dir)

@@ -14,7 +14,8 @@
 // and the same on 1024 threads (sample_dist_nt, 2 ids per thread):
 //   21 + max / count (barrier 1)   22 + shared histogram, scan (barrier 2)
 //   23 + candidate slots (barrier 3)  24 + rank slices (barrier 4)
-//   25 = the whole draw              26 = k_sample_w's sample_fast_nt
+//   25 + scatter to rank order, read back   26 + sequential sum
+//   29 = the whole draw              30 = k_sample_w's sample_fast_nt
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Iqwen3-tts-c_amd/csrc/hip tools/mb_sample.hip -o tools/mb_sample
 #include "qtts_sample_dev.h"
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(1024) void k_phase_w(SampArgs a, float *sink) {
     uint32_t rng = 0x42280000u;
     const uint64_t etab = kExp2fTab[tid & 31];
     int t;
-    if constexpr (PHASE == 26) t = sample_fast_nt<1024, EM>(fs, v, E, n, a.top_k, rng, etab);
+    if constexpr (PHASE == 30) t = sample_fast_nt<1024, EM>(fs, v, E, n, a.top_k, rng, etab);
     else t = sample_dist_nt<1024, EM, PHASE - 20>(fs, v, kk, id, a.top_k, rng, etab);
     if (tid == 0) sink[0] = (float)t;
 }
@@ -153,7 +154,9 @@ int main() {
     printf("w1024 22 + histogram, scan  %6.2f us\n", time_phase<22>(a, sink, st));
     printf("w1024 23 + candidate slots  %6.2f us\n", time_phase<23>(a, sink, st));
     printf("w1024 24 + rank slices      %6.2f us\n", time_phase<24>(a, sink, st));
-    printf("w1024 25 = whole draw       %6.2f us\n", time_phase<25>(a, sink, st));
-    printf("w1024 26 sample_fast_nt     %6.2f us\n", time_phase<26>(a, sink, st));
+    printf("w1024 25 + scatter, read    %6.2f us\n", time_phase<25>(a, sink, st));
+    printf("w1024 26 + sequential sum   %6.2f us\n", time_phase<26>(a, sink, st));
+    printf("w1024 29 = whole draw       %6.2f us\n", time_phase<29>(a, sink, st));
+    printf("w1024 30 sample_fast_nt     %6.2f us\n", time_phase<30>(a, sink, st));
     return 0;
 }
