@@ -536,7 +536,8 @@ template <int HD>
 __global__ __launch_bounds__(256) void k_attn_short(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) float lq[4 * HD];   // rotated q0 | q1 | k, raw v
     __shared__ float sc[2 * 16];
-    attn_short_wg<HD, false>(a, blockIdx.x, blockIdx.y, lq, sc);
+    attn_short_wg<HD, false>(a, blockIdx.x, blockIdx.y, lq, sc, nullptr, true, NoIssue(),
+                             a.qkv_tab ? a.qkv_tab : a.qkv, a.qkv_tab ? a.tab_ids + a.tab_off : nullptr);
 }
 
 // Short-context attention + the O projection split by kv head (the
@@ -548,8 +549,10 @@ __global__ __launch_bounds__(256) void k_attn_short(AttnArgs a) {
 // partials in head order and adds the residual: x + o_proj(attn) of
 // T.c:667-676 with o_proj's dot split by head.
 // Lanes: LPS per row slot, 8 columns (16 B of bf16) per lane per load.
+// (rsrc / ids lead the arguments: the Makefile preloads them into SGPRs)
 template <int HD>
-__global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, int R, float *part) {
+__global__ __launch_bounds__(256) void k_attn_o(const float *rsrc, const int *ids, AttnArgs t, const bf16_t *Wo,
+                                                int R, float *part) {
     constexpr int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, NJ = W2 / (8 * LPS), RPW = 256 / LPS;
     __shared__ __attribute__((aligned(16))) float lq[4 * HD];
     __shared__ __attribute__((aligned(16))) float att[W2];
@@ -568,7 +571,7 @@ __global__ __launch_bounds__(256) void k_attn_o(AttnArgs t, const bf16_t *Wo, in
         for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const v4u *>(wr + 8 * LPS * j);
         qtts_l2pf_issue<256>(t.pf, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), pfr, Wo);
     };
-    attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0, issue);
+    attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0, issue, rsrc, ids);
     __syncthreads();
     float acc = 0.f;
 #pragma unroll
@@ -602,11 +605,13 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
     if (!qtts_attn_o_covers(a, Wo)) return 1;
     const int W2 = 2 * a.HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
     const dim3 grid((R + RPW - 1) / RPW, a.KV, a.nrows);
+    const float *rsrc = a.qkv_tab ? a.qkv_tab : a.qkv;
+    const int *ids = a.qkv_tab ? a.tab_ids + a.tab_off : nullptr;
     switch (a.HD) {
-        case 128: hipLaunchKernelGGL((k_attn_o<128>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<128>"; break;
-        case 64: hipLaunchKernelGGL((k_attn_o<64>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<64>"; break;
-        case 32: hipLaunchKernelGGL((k_attn_o<32>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<32>"; break;
-        default: hipLaunchKernelGGL((k_attn_o<16>), grid, dim3(256), 0, st, a, Wo, R, part); qtts_last_kernel = "k_attn_o<16>"; break;
+        case 128: hipLaunchKernelGGL((k_attn_o<128>), grid, dim3(256), 0, st, rsrc, ids, a, Wo, R, part); qtts_last_kernel = "k_attn_o<128>"; break;
+        case 64: hipLaunchKernelGGL((k_attn_o<64>), grid, dim3(256), 0, st, rsrc, ids, a, Wo, R, part); qtts_last_kernel = "k_attn_o<64>"; break;
+        case 32: hipLaunchKernelGGL((k_attn_o<32>), grid, dim3(256), 0, st, rsrc, ids, a, Wo, R, part); qtts_last_kernel = "k_attn_o<32>"; break;
+        default: hipLaunchKernelGGL((k_attn_o<16>), grid, dim3(256), 0, st, rsrc, ids, a, Wo, R, part); qtts_last_kernel = "k_attn_o<16>"; break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

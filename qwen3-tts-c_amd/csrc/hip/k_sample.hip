@@ -10,15 +10,18 @@ namespace {
 template <bool FAST, int EM>
 __global__ __launch_bounds__(256) void k_sample(SampArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    qtts_samp::sample_row<FAST, EM>(a, blockIdx.x, smraw);
+    qtts_samp::sample_row<FAST, EM>(a, blockIdx.x, smraw, a.logits, a.stopped, a.mode == 1 ? a.rng : a.st_rng,
+                                    a.n_gen, a.counts);
 }
 
 // the fast path on 1024 threads (qtts_sample_dev.h sample_fast_nt): EM ids per
-// thread (2 up to 2048 logits, 4 up to 4096)
+// thread (2 up to 2048 logits, 4 up to 4096); the row's input pointers lead the
+// arguments (preloaded into SGPRs, Makefile)
 template <int EM>
-__global__ __launch_bounds__(1024) void k_sample_w(SampArgs a) {
+__global__ __launch_bounds__(1024) void k_sample_w(const float *logits, const int *stopped, const uint32_t *rng,
+                                                   const int *n_gen, const int *counts, SampArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    qtts_samp::sample_row<true, EM, 1024>(a, blockIdx.x, smraw);
+    qtts_samp::sample_row<true, EM, 1024>(a, blockIdx.x, smraw, logits, stopped, rng, n_gen, counts);
 }
 
 }  // namespace
@@ -33,11 +36,14 @@ int qtts_sample(const SampArgs &a, hipStream_t st) {
     const char *sw = getenv("QTTS_HIP_SAMPLE_W");
     if (qtts_samp::fast_path(a) && !(sw && !atoi(sw))) {
         const size_t sm = sizeof(qtts_samp::FastSmemNT<1024>);
+        const uint32_t *rng = a.mode == 1 ? a.rng : a.st_rng;
         if (a.n <= 2 * 1024) {
-            hipLaunchKernelGGL((k_sample_w<2>), dim3(a.nb), dim3(1024), sm, st, a);
+            hipLaunchKernelGGL((k_sample_w<2>), dim3(a.nb), dim3(1024), sm, st, a.logits, (const int *)a.stopped, rng,
+                               (const int *)a.n_gen, (const int *)a.counts, a);
             qtts_last_kernel = "k_sample_w<2>";
         } else {
-            hipLaunchKernelGGL((k_sample_w<4>), dim3(a.nb), dim3(1024), sm, st, a);
+            hipLaunchKernelGGL((k_sample_w<4>), dim3(a.nb), dim3(1024), sm, st, a.logits, (const int *)a.stopped, rng,
+                               (const int *)a.n_gen, (const int *)a.counts, a);
             qtts_last_kernel = "k_sample_w<4>";
         }
     } else if (qtts_samp::fast_path(a)) {

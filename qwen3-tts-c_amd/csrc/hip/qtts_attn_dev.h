@@ -30,19 +30,23 @@ struct NoIssue { __device__ __forceinline__ void operator()() const {} };
 // `issue` runs right after the attention's own loads are issued (k_attn_o
 // issues its O-weight fragment there: loads retire in issue order, so the
 // attention's inputs must not queue behind the weights)
+// rsrc: the q|k|v rows (a.qkv) or the table (a.qkv_tab); ids: a.tab_ids +
+// a.tab_off, or nullptr (no table) -- passed separately so a kernel can take
+// them as preloaded kernel arguments (k_attn_o)
 template <int HD, bool SC1, class Issue = NoIssue>
 __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r, float *lq, float *scs,
-                                              float *lout = nullptr, bool wcache = true, Issue issue = Issue()) {
+                                              float *lout, bool wcache, Issue issue, const float *rsrc,
+                                              const int *ids) {
     constexpr int D4 = HD / 4, LPK = HD / 16, NK = 16;
     float (*sc)[NK] = reinterpret_cast<float (*)[NK]>(scs);
     const int tid = threadIdx.x;
     const int KVD = a.KV * HD;
     const int p = a.pos ? a.pos[r] : a.pos_const, n = p + 1;
-    const float *row = a.qkv + (size_t)r * a.ld_qkv;
-    if (a.qkv_tab) {
-        const int *ip = a.tab_ids + (size_t)r * a.tab_bstride + a.tab_off;
+    const float *row = rsrc + (size_t)r * a.ld_qkv;
+    if (ids) {
+        const int *ip = ids + (size_t)r * a.tab_bstride;
         if (a.tab_row_sel) ip += (size_t)a.tab_row_sel[r] * a.tab_rstride;
-        row = a.qkv_tab + (size_t)(*ip) * a.ld_qkv;
+        row = rsrc + (size_t)(*ip) * a.ld_qkv;
     }
     const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
     const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;

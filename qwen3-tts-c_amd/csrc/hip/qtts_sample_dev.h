@@ -789,24 +789,29 @@ __device__ __forceinline__ int sample_dist_nt(FastSmemNT<NT> &fs, const float (&
 #pragma unroll
     for (int i = 0; i < KC / 4; ++i) q[i] = reinterpret_cast<const float4 *>(fs.pv)[i];
     if constexpr (STOP == 5) return (int)q[0].x;
+    // running sums c_j in rank order (the reference's sequential sum); p_j >= 0,
+    // so c_j never decreases and the first j with c_j >= r is the number of
+    // j with c_j < r -- counted with independent compares (a uniform
+    // first-match chain compiled to ~15 dependent VALU -> SALU steps per j)
+    float run[KC];
     float sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < KC / 4; ++i) { sum += q[i].x; sum += q[i].y; sum += q[i].z; sum += q[i].w; }
+    for (int i = 0; i < KC / 4; ++i) {
+        sum += q[i].x; run[4 * i] = sum;
+        sum += q[i].y; run[4 * i + 1] = sum;
+        sum += q[i].z; run[4 * i + 2] = sum;
+        sum += q[i].w; run[4 * i + 3] = sum;
+    }
     if constexpr (STOP == 6) return (int)sum;
     if (!(sum > 0.0f)) return fs.pi[0];
     float r = 0.f;
     if (lane == 0) r = rand_uniform(rng) * sum;
     r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 0));
-    float cs = 0.f;
-    int jf = -1;
+    int n4[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < KC / 4; ++i) {
-        cs += q[i].x; jf = (jf < 0 && cs >= r) ? 4 * i : jf;
-        cs += q[i].y; jf = (jf < 0 && cs >= r) ? 4 * i + 1 : jf;
-        cs += q[i].z; jf = (jf < 0 && cs >= r) ? 4 * i + 2 : jf;
-        cs += q[i].w; jf = (jf < 0 && cs >= r) ? 4 * i + 3 : jf;
-    }
-    return jf >= 0 ? fs.pi[jf] : 0;
+    for (int j = 0; j < KC; ++j) n4[j & 3] += run[j] < r ? 1 : 0;
+    const int jf = n4[0] + n4[1] + n4[2] + n4[3];   // k..KC: no j reached r (the reference returns 0)
+    return jf < k ? fs.pi[jf] : 0;
 }
 
 // sample_fast_regs on NT threads: thread t owns ids id[j] = t*E + j (j < E).
@@ -917,8 +922,13 @@ __host__ __device__ inline bool fast_path(const SampArgs &a) {
 // One row's draw (all NT threads of the workgroup).  `smraw` >= sizeof(KSmem),
 // or sizeof(FastSmem) / sizeof(FastSmemNT<NT>) with FAST_ONLY (the caller
 // guarantees fast_path(a)).  Used by k_sample.
+// The row's input pointers come as parameters (a.logits, a.stopped, the RNG
+// state array of the mode, a.n_gen, a.counts) so that k_sample_w can take
+// them as preloaded kernel arguments.
 template <bool FAST_ONLY, int EM = EMAX, int NT = 256>
-__device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned char *smraw) {
+__device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned char *smraw, const float *logits,
+                                           const int *stopped_p, const uint32_t *rng_p, const int *ngen_p,
+                                           const int *counts_p) {
 #pragma clang fp contract(off)
     static_assert(NT == 256 || FAST_ONLY, "the full path runs on 256 threads");
     KSmem &U = *reinterpret_cast<KSmem *>(smraw);
@@ -930,12 +940,12 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     // offset: as scalar loads they were waited for one after another --
     // stopped, then the RNG state -- before the first logit load issued)
     const int E = (n + NT - 1) / NT;
-    const float *lg = a.logits + (size_t)b * a.ld;
+    const float *lg = logits + (size_t)b * a.ld;
     const int i0 = tid * E;
     float x[EM];
     int cnt[EM];
-    const bool pen = a.mode == 1 && a.rep != 1.0f && a.counts;
-    const int *cbase = pen ? a.counts + (size_t)b * n : reinterpret_cast<const int *>(lg);
+    const bool pen = a.mode == 1 && a.rep != 1.0f && counts_p;
+    const int *cbase = pen ? counts_p + (size_t)b * n : reinterpret_cast<const int *>(lg);
 #pragma unroll
     for (int j = 0; j < EM; ++j) {
         const int i = i0 + j < n ? i0 + j : n - 1;
@@ -945,9 +955,9 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     int z0;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
     // (an absent flag reads a logit word instead, and is replaced by 0 below)
-    const int *sp = a.stopped ? a.stopped + b : reinterpret_cast<const int *>(lg);
-    const int *np = a.mode == 1 ? a.n_gen + b : reinterpret_cast<const int *>(lg);
-    const uint32_t *rp = (a.mode == 1 ? a.rng : a.st_rng) + b;
+    const int *sp = stopped_p ? stopped_p + b : reinterpret_cast<const int *>(lg);
+    const int *np = a.mode == 1 ? ngen_p + b : reinterpret_cast<const int *>(lg);
+    const uint32_t *rp = rng_p + b;
     int stopped = sp[z0];
     int ng = np[z0];
     uint32_t rng = rp[z0];
@@ -955,7 +965,7 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
     // one wait for all of them here (the compiler would otherwise sink the
     // flag loads into the branches that use them: another round trip each)
     asm volatile("" :: "v"(stopped), "v"(ng), "v"(rng));
-    if (!a.stopped) stopped = 0;
+    if (!stopped_p) stopped = 0;
     if (a.mode != 1) ng = 0;
 #pragma unroll
     for (int j = 0; j < EM; ++j) {
