@@ -235,8 +235,11 @@ __global__ __launch_bounds__(256) void k_qk_prep_w(AttnArgs a) {
 // (agent-scope acq_rel ticket) merges them in split order and resets the
 // ticket.  Grid size is fixed at graph capture (nsplit from the cache
 // capacity); splits past the live length exit at once.
+// (qkv / pos / kc / vc lead the arguments: preloaded into SGPRs, Makefile --
+// the position load and the cache loads behind it need no kernarg round trip)
 template <int HD, int GPH, int LPK>
-__global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
+__global__ __launch_bounds__(256) void k_attn_dec(const float *qkv_, const int *pos_, float *kc_, float *vc_,
+                                                  AttnArgs a) {
     // LPK lanes per key
     constexpr int DPL = HD / LPK;                  // dims per lane
     constexpr int CH = 256 / LPK;                  // keys per workgroup
@@ -254,16 +257,16 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kvh = blockIdx.x, split = blockIdx.y, r = blockIdx.z;
     const int KVD = a.KV * HD;
-    const int p = a.pos ? a.pos[r] : a.pos_const;
+    const int p = pos_ ? pos_[r] : a.pos_const;
     const int n = p + 1;
     const int nact = (n + CH - 1) / CH;
     if (split >= nact) return;
     const int t0 = split * CH;
     const int t1 = min(n, t0 + CH);
     const bool owner = (split == nact - 1);        // holds the current token
-    const float *row = a.qkv + (size_t)r * a.ld_qkv;
-    const float *Kc = a.kc + (size_t)r * a.S * KVD + kvh * HD;
-    const float *Vc = a.vc + (size_t)r * a.S * KVD + kvh * HD;
+    const float *row = qkv_ + (size_t)r * a.ld_qkv;
+    const float *Kc = kc_ + (size_t)r * a.S * KVD + kvh * HD;
+    const float *Vc = vc_ + (size_t)r * a.S * KVD + kvh * HD;
 
     // ---- the token's own inputs first (q / k head values, norm weights, RoPE
     // rows, v): issued behind the cache loads they would wait for all of them
@@ -358,8 +361,8 @@ __global__ __launch_bounds__(256) void k_attn_dec(AttnArgs a) {
         __syncthreads();
     }
     if (owner && tid < HD && !(a.skip && a.skip[r])) {
-        a.kc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = qk[GPH * HD + tid];
-        a.vc[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = vv[tid];
+        kc_[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = qk[GPH * HD + tid];
+        vc_[((size_t)r * a.S + p) * KVD + kvh * HD + tid] = vv[tid];
     }
 
     // ---- scores ----
@@ -671,7 +674,7 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
         const int lpk = attn_lpk(a.HD, a.defer, a.lpk);
 #define QTTS_AD(H, L)                                                                                      \
         if (a.HD == H && lpk == L) {                                                                       \
-            hipLaunchKernelGGL((k_attn_dec<H, 2, L>), grid, dim3(256), 0, st, a);                         \
+            hipLaunchKernelGGL((k_attn_dec<H, 2, L>), grid, dim3(256), 0, st, a.qkv, a.pos, a.kc, a.vc, a); \
             qtts_last_kernel = "k_attn_dec<" #H ", 2, " #L ">";                                            \
             return hipGetLastError() == hipSuccess ? 0 : -1;                                               \
         }

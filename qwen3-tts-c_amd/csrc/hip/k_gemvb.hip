@@ -45,9 +45,9 @@ using namespace qtts_gm;
 
 enum { GB_SRC_X = 0, GB_SRC_XADD = 1, GB_SRC_TAB = 2, GB_SRC_TABF = 3 };
 
-// id of the table row that batch row b reads
-__device__ __forceinline__ unsigned gb_row_id(const GemvArgs &a, int b) {
-    const int *p = a.ids + (size_t)b * a.ids_bstride + a.ids_off;
+// id of the table row that batch row b reads (ids: a.ids + a.ids_off)
+__device__ __forceinline__ unsigned gb_row_id(const GemvArgs &a, const int *ids, int b) {
+    const int *p = ids + (size_t)b * a.ids_bstride;
     if (a.row_sel) p += (size_t)a.row_sel[b] * a.ids_rstride;
     return (unsigned)*p;
 }
@@ -66,8 +66,11 @@ __device__ __forceinline__ void gb_stamp(const GemvArgs &a, int k) {
 #endif
 }
 
+// (src -- a.x, a.table or a.table_f32 by SRC --, ids, W and xadd lead the
+// arguments: preloaded into SGPRs, Makefile)
 template <int SPW, int TPW, int NBC, int PM, int SRC>
-__global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
+__global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids, const bf16_t *Wt, const float *xadd,
+                                                GemvArgs a) {
     gb_stamp(a, 0);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int SC = 32 * SPW;                 // columns of a wave's slice
@@ -109,25 +112,25 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
     if constexpr (SRC == GB_SRC_TAB || SRC == GB_SRC_TABF) {
         unsigned id[XQ];
 #pragma unroll
-        for (int q = 0; q < XQ; ++q) id[q] = gb_row_id(a, urow[q]);
+        for (int q = 0; q < XQ; ++q) id[q] = gb_row_id(a, ids, urow[q]);
         if constexpr (SRC == GB_SRC_TAB) {
-            const auto rt = rsrc(a.table);
+            const auto rt = rsrc(src);
 #pragma unroll
             for (int q = 0; q < XQ; ++q) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b64(rt, (id[q] * (unsigned)a.C + (unsigned)(c0 + ucol)) * 2u, 0, 0);
                 tq[q] = make_uint2(v[0], v[1]);
             }
         } else {
-            const auto rt = rsrc(a.table_f32);
+            const auto rt = rsrc(src);
 #pragma unroll
             for (int q = 0; q < XQ; ++q) xv[q] = ld4(rt, id[q] * (unsigned)a.C + (unsigned)(c0 + ucol));
         }
     } else {
-        const auto rx = rsrc(a.x);
+        const auto rx = rsrc(src);
 #pragma unroll
         for (int q = 0; q < XQ; ++q) xv[q] = ld4(rx, (unsigned)urow[q] * (unsigned)a.ldx + (unsigned)(c0 + ucol));
         if constexpr (SRC == GB_SRC_XADD) {
-            const auto rp = rsrc(a.xadd);
+            const auto rp = rsrc(xadd);
             const int np = a.n_xadd;
 #pragma unroll
             for (int p = 0; p < PM; ++p) {
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(1024) void k_gemvb(GemvArgs a) {
     float4 nwv = make_float4(1.f, 1.f, 1.f, 1.f);
     if (norm) nwv = ld4(rsrc(a.norm_w), (unsigned)(c0 + ucol));
     // weight fragments: tile t, step j -> W[r0 + 16 t + (lane & 15)][c0 + 32 j + 8 (lane >> 4) .. +7]
-    const auto rw = rsrc(a.W);
+    const auto rw = rsrc(Wt);
     v4u wv[TPW][SPW];
     unsigned wo[TPW];
 #pragma unroll
@@ -348,10 +351,12 @@ int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
     const dim3 grid((T + TPW - 1) / TPW, kz);
     if (a.tick && (int)grid.x > QTTS_GM_TICKS) return 1;
     const int src = tab ? GB_SRC_TAB : tabf ? GB_SRC_TABF : xadd ? GB_SRC_XADD : GB_SRC_X;
+    const void *srcp = tab ? (const void *)a.table : tabf ? (const void *)a.table_f32 : (const void *)a.x;
+    const int *idsp = (tab || tabf) ? a.ids + a.ids_off : nullptr;
     const dim3 block(64 * W);
 #define QTTS_GB(SP, TP, NC, PP, SS)                                                                    \
     {                                                                                                  \
-        hipLaunchKernelGGL((k_gemvb<SP, TP, NC, PP, SS>), grid, block, smem, st, a);                   \
+        hipLaunchKernelGGL((k_gemvb<SP, TP, NC, PP, SS>), grid, block, smem, st, srcp, idsp, a.W, a.xadd, a); \
         qtts_last_kernel = "k_gemvb<" #SP ", " #TP ", " #NC ", " #PP ", " #SS ">";                      \
     }
 #define QTTS_GB_SRC(SP, TP, NC)                                                                        \

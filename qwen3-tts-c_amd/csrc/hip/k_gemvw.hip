@@ -106,15 +106,17 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
     float4 am_a[AM ? XQ : 1][AM ? AM_MS : 1];
     float am_m[AM ? XQ : 1][AM ? AM_MS : 1], am_l[AM ? XQ : 1][AM ? AM_MS : 1];
     int am_p = 0;
+    // (AM: src / ids carry the preloaded amerge / am_pos pointers)
+    const float *amerge = AM ? reinterpret_cast<const float *>(src) : nullptr;
     if constexpr (AM) {
-        am_p = a.am_pos[0];
+        am_p = ids[0];
         const int HDm = a.am_hd, GP = a.am_gph, NO = GP * HDm, stride = NO + 2 * GP;
 #pragma unroll
         for (int q = 0; q < XQ; ++q) {
             const int c = 4 * (tid + 256 * q);
             const int cc = c < C ? c : 0;
             const int h = cc / HDm, kvh = h / GP, g = h - kvh * GP;
-            const float *mb = a.amerge + (size_t)kvh * a.am_nsplit * stride;
+            const float *mb = amerge + (size_t)kvh * a.am_nsplit * stride;
 #pragma unroll
             for (int s2 = 0; s2 < AM_MS; ++s2) {
                 const int sc = s2 < a.am_nsplit ? s2 : 0;
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
             const int c = 4 * (tid + 256 * q);
             const int cc = c < C ? c : 0;
             const int h = cc / HDm, kvh = h / GP, g = h - kvh * GP, eo = (cc - h * HDm) + g * HDm;
-            const float *mb = a.amerge + (size_t)kvh * a.am_nsplit * stride;
+            const float *mb = amerge + (size_t)kvh * a.am_nsplit * stride;
             float M = -INFINITY;
 #pragma unroll
             for (int s2 = 0; s2 < AM_MS; ++s2)
@@ -304,8 +306,8 @@ int qtts_gemvw(const GemvArgs &a, hipStream_t st) {
         // partials of up to 4 / 8 splits ahead of the weights: the capacity's
         // splits when they fit (fixed-length decodes), else 8 and the rest after
 #define QTTS_GWA(RW_, MS_)                                                                             \
-        { hipLaunchKernelGGL((k_gemvw<RW_, 4, true, MS_>), grid, dim3(256), smem, st, (const void *)a.x, a.W,   \
-                             (const int *)nullptr, (int)GW_SRC_X, a);                                   \
+        { hipLaunchKernelGGL((k_gemvw<RW_, 4, true, MS_>), grid, dim3(256), smem, st, (const void *)a.amerge, \
+                             a.W, a.am_pos, (int)GW_SRC_X, a);                                          \
           qtts_last_kernel = "k_gemvw<" #RW_ ", 4, true, " #MS_ ">"; }
         if (a.R == 2048) { if (a.am_nsplit <= 4) QTTS_GWA(2, 4) else if (a.am_nsplit <= 6) QTTS_GWA(2, 6) else QTTS_GWA(2, 8) }
         else { if (a.am_nsplit <= 4) QTTS_GWA(1, 4) else if (a.am_nsplit <= 6) QTTS_GWA(1, 6) else QTTS_GWA(1, 8) }

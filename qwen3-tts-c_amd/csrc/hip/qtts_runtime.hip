@@ -164,7 +164,11 @@ struct qtts_dev {
     std::vector<Prof> prof;
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
-    bool l2pf = true;        // QTTS_HIP_L2PF=0: no next-launch weight prefetch in the batch-1 sub-talker chain
+    // QTTS_HIP_L2PF=<mask>: which edges of the batch-1 sub-talker chain carry
+    // the next-launch weight prefetch (0 none): 1 q|k|v -> attention + O,
+    // 2 attention + O -> gate|up, 4 gate|up -> down, 8 down -> next q|k|v or
+    // head, 16 head -> the next pass's first launch (two launches ahead)
+    int l2pf = 31;
     int l2pf_tk = 0;         // QTTS_HIP_L2PF_TK bits (batch-1 talker, non-temporal): 1 q|k|v -> O's W_o, 2 O -> gate|up
     unsigned *pf_sink = nullptr;
     bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
@@ -390,7 +394,7 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
     const char *pf = getenv("QTTS_HIP_L2PF");
-    dv->l2pf = !(pf && !atoi(pf));
+    if (pf) dv->l2pf = atoi(pf);
     const char *pft = getenv("QTTS_HIP_L2PF_TK");
     if (pft) dv->l2pf_tk = atoi(pft);
     const char *gd = getenv("QTTS_HIP_GM_DBG");
@@ -881,7 +885,7 @@ static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH,
     L2Prefetch p;
     const int W2 = 2 * HD, LPS = W2 / 8 < 8 ? W2 / 8 : 8, RPW = 256 / LPS;
     const int cpr = W2 * 2 / 64;   // 64-B chunks per row slice
-    if (!dv->l2pf || R % RPW || (cpr & (cpr - 1)) || cpr < 1 || RPW * cpr > 256 * QTTS_PF_LOADS) return p;
+    if (R % RPW || (cpr & (cpr - 1)) || cpr < 1 || RPW * cpr > 256 * QTTS_PF_LOADS) return p;
     p.base = reinterpret_cast<const unsigned char *>(Wo);
     p.pm = R / RPW; p.pa = (long long)RPW * NH * HD * 2; p.pb = W2 * 2;
     p.chunks = RPW * cpr; p.lg = __builtin_ctz(cpr); p.ld = NH * HD * 2; p.sink = dv->pf_sink;
@@ -994,9 +998,10 @@ static int subtalker(qtts_dev *dv) {
     // batch 1, fused attention + O: each launch also pulls the next launch's
     // weight slice into its XCD's L2 (GemvArgs::pf / AttnArgs::pf)
     const bool pfon = nb == 1 && dv->attn_o && dv->l2pf;
+    const int pfm = pfon ? dv->l2pf : 0;
     const bool tab0_ok = nb == 1 && dv->attn_o && dv->qkv0_tab && (!proj || dv->st_ptab);
     auto first_op_pf = [&](int gn) {   // pass gn's first launch (layer 0: the table attention or q|k|v)
-        if (!pfon || gn >= d.G) return L2Prefetch();
+        if (gn >= d.G) return L2Prefetch();
         if (gn >= 1 && tab0_ok) return pf_attn_o(dv, dv->sl[0].wo, d.Hs, d.NHs, d.HDs);
         return pf_gemvw(dv, dv->sl[0].wqkv, QKV, d.Hs);
     };
@@ -1073,10 +1078,8 @@ static int subtalker(qtts_dev *dv) {
                 t.tab_ids = src.ids; t.tab_bstride = src.ids_bstride; t.tab_row_sel = src.row_sel;
                 t.tab_rstride = src.ids_rstride; t.tab_off = src.ids_off;
             }
-            if (pfon) {
-                a.pf = pf_attn_o(dv, ly.wo, d.Hs, d.NHs, d.HDs);
-                t.pf = kv_only ? first_op_pf(g + 1) : pf_gemvw(dv, ly.wgu, 2 * d.Is, d.Hs);
-            }
+            if (pfm & 1) a.pf = pf_attn_o(dv, ly.wo, d.Hs, d.NHs, d.HDs);
+            if (pfm & 2) t.pf = kv_only ? first_op_pf(g + 1) : pf_gemvw(dv, ly.wgu, 2 * d.Is, d.Hs);
             if (dv->attn_o && nb == 1) {
                 if (!tab0) CKI(pgemv(dv, a, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
@@ -1102,7 +1105,7 @@ static int subtalker(qtts_dev *dv) {
             if (kv_only) break;
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
-            if (pfon) a.pf = pf_gemvw(dv, ly.wdown, d.Hs, d.Is);
+            if (pfm & 4) a.pf = pf_gemvw(dv, ly.wdown, d.Hs, d.Is);
             if (sdbg) a.dbg = dv->gm_dbg + 2 * 2048 * 8;
             if (tab0) set_src(a);   // the residual is the input table row (x_st was not written)
             if (fused_o) {
@@ -1114,7 +1117,7 @@ static int subtalker(qtts_dev *dv) {
             if (fused_o || opend) std::swap(xa, xb);
             a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xa, d.Hs, nb, EPI_RESID);
             a.nt = 0;
-            if (pfon) {
+            if (pfm & 8) {
                 if (l + 1 < d.Ls) a.pf = pf_gemvw(dv, dv->sl[l + 1].wqkv, QKV, d.Hs);
                 else if (g >= 1) a.pf = pf_gemvw(dv, dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs);
             }
@@ -1127,7 +1130,7 @@ static int subtalker(qtts_dev *dv) {
                         EPI_STORE);
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
         if (pend) add_in(a, pend, npend, d.Hs, nb, nullptr);
-        a.pf = first_op_pf(g + 1);   // (two launches ahead: the sampler runs in between)
+        if (pfm & 16) a.pf = first_op_pf(g + 1);   // (two launches ahead: the sampler runs in between)
         SampArgs s;
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;
