@@ -598,7 +598,7 @@ struct FastSmemNT {
     float top_v[KFAST];
     int top_i[KFAST];
     int misc[4];
-    int dh[DBINS];                     // distance histogram (shared)
+    int dh[DBINS];                     // distance histogram (shared; 4 copies by wave measured slower, 5.21 vs 4.98 us)
     unsigned long long cand[KC];       // candidate keys (value key << 32 | ~index), slots by atomic
     int crank[KC];                     // candidate ranks, summed over the waves' slices
     float pv[KC];

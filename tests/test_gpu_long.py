@@ -115,9 +115,14 @@ def test_hd128_600_row_prefill_and_steps_vs_reference(hd128):
 
 
 @pytest.mark.slow
-def test_full_bench_workload_vs_reference(gpu):
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_L2PF": "0"}, {"QTTS_HIP_L2PF_TK": "3"}, {"QTTS_HIP_L2PF": "5"}])
+def test_full_bench_workload_vs_reference(gpu, monkeypatch, env):
     """BASELINE's workload as bench.py runs it (1.7B, P128, fixed 128 frames,
-    default sampling, seed 42): codes bit-exact, waveform MSE < 1e-4."""
+    default sampling, seed 42): codes bit-exact, waveform MSE < 1e-4 -- also
+    without the next-launch L2 prefetch, with part of its edges, and with the
+    talker's prefetch edges on (these loads never change a value)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     g = np.load(os.path.join(GOLDEN, "long_17b.npz"))
     man = _man()["1.7b"]
     m = qtts.QwenTTS(model_dir("1.7b"))

@@ -4,10 +4,12 @@
 # voice-clone batch bench (prefill GEMM, batch decode GEMV, codec convs), then
 # the bench line itself -- after the summaries are in the box's profiles/ so
 # the line's roofline.rocprof_avg_us / traffic come from the same code.
-# Usage (via gpurun): bash tools/gpu_round.sh <tag> [all|prof|dist]
+# Usage (via gpurun): bash tools/gpu_round.sh <tag> [all|core|prof|extra|dist]
+#   core  = tests + profiles + the 1.7B and 0.6B (C2) bench lines (fits one call)
+#   extra = C5 voice clone batch 8, batch 8 / 16 lines, encoders, MFMA pass
 set -eo pipefail
 TAG=${1:-r02}
-MODE=${2:-all}   # all | prof (no tests) | dist (2-rank gloo rehearsal)
+MODE=${2:-all}   # all | core | prof (no tests) | extra | dist (2-rank gloo rehearsal)
 R=$GRAFT_REPO_ROOT
 [ -z "$R" ] && R=$(pwd)
 O=$R/gpurun_out/$TAG
@@ -23,12 +25,18 @@ if [ "$MODE" = dist ]; then
     --no-profile > $O/dist2.json 2> $O/dist2.err
   echo done; exit 0
 fi
-if [ "$MODE" = all ]; then
+if [ "$MODE" = extra ]; then
+  for b in 8 16; do
+    timeout -k 10 600 python bench.py --batch $b --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_b$b.json 2> $O/bench_b$b.err
+  done
+fi
+if [ "$MODE" = all ] || [ "$MODE" = core ]; then
   rc=0
   timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || rc=$?
   # 1 = some test failed (keep measuring); anything else (timeout, abort, crash) ends the call
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc"; exit $rc; fi
 fi
+if [ "$MODE" != extra ]; then
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch.log 2>&1
@@ -46,9 +54,11 @@ python3 $R/tools/prof_summary.py $O/c2
 cp $O/c2/kernel_stats.csv $R/profiles/${TAG}_06b_kernel_stats.csv
 cp $O/c2/pmc.json $R/profiles/${TAG}_06b_pmc.json
 cd $R
-timeout -k 10 900 python bench.py --preset 0.6b --greedy > $O/bench_06b.json 2> $O/bench_06b.err
+timeout -k 10 900 python bench.py --preset 0.6b --greedy --no-cpu-1thread > $O/bench_06b.json 2> $O/bench_06b.err
 cp $O/bench_06b.json $R/profiles/${TAG}_bench_06b.json
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
+fi
+[ "$MODE" = core ] && { echo done; exit 0; }
 # BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8
 timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 > $O/bench_vc8.json 2> $O/bench_vc8.err
 cp $O/bench_vc8.json $R/profiles/${TAG}_bench_vc8.json
