@@ -38,6 +38,7 @@
 #include <algorithm>
 
 #include "qtts_gemvm_dev.h"
+#include "qtts_l2pf.h"
 
 namespace {
 
@@ -196,6 +197,9 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
 #pragma unroll
         for (int t = 0; t < TPW; ++t)
             wv[t][j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rw, wo[t] + 64u * j, 0, 0));
+    // the next launch's weight slices into this XCD's L2 (GemvArgs::pf)
+    L2PfRegs pfr;
+    qtts_l2pf_issue<1024, false, 2>(a.pf, blockIdx.x + gridDim.x * blockIdx.y, pfr, Wt, (int)blockDim.x);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave writes and reads its rows: LDS is in order
     gb_stamp(a, 1);
 
@@ -269,9 +273,10 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
             }
         }
         reduce_last(a, 16 * TPW, reinterpret_cast<int *>(ssq));
+        qtts_l2pf_sink(a.pf, pfr);
         return;
     }
-    if (!tile_wave) return;
+    if (!tile_wave) { qtts_l2pf_sink(a.pf, pfr); return; }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int bb = 4 * (lane >> 4) + i;
@@ -286,43 +291,40 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
         epilogue(a, bb, r, val, up);
     }
     gb_stamp(a, 4);
+    qtts_l2pf_sink(a.pf, pfr);
 }
 
 }  // namespace
 
 // Returns 1 when the shape is not covered (the caller uses k_gemvm), 0 ok,
 // -1 launch error.  QTTS_HIP_GEMVB=0 keeps k_gemvm for every shape (A/B).
-int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
-    // (read per call: launches happen at graph capture, and tests switch it
-    // per model instance)
-    const char *ge = getenv("QTTS_HIP_GEMVB");
-    if (ge && !atoi(ge)) return 1;
-    const GemvArgs &a = in;
-    if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32 || (size_t)a.R * a.C * 2 >= ((size_t)1 << 31)) return 1;
+struct GbGeom { int SPW, TPW, W, NBC, PM, src; size_t smem; dim3 grid; };
+static bool gemvb_geom(const GemvArgs &a, GbGeom &g) {
+    if (a.nb < 2 || a.nb > 16 || a.R % 16 || a.C % 32 || (size_t)a.R * a.C * 2 >= ((size_t)1 << 31)) return false;
     const bool tab = a.table != nullptr, tabf = !tab && a.table_f32 != nullptr;
     if (tab) {
-        if (a.C % 4) return 1;
+        if (a.C % 4) return false;
     } else if (tabf) {
-        if ((uintptr_t)a.table_f32 & 15 || a.C % 4) return 1;
+        if ((uintptr_t)a.table_f32 & 15 || a.C % 4) return false;
     } else if (!a.x || a.ldx % 4 || ((uintptr_t)a.x & 15)) {
-        return 1;
+        return false;
     }
-    if (a.norm_w && ((uintptr_t)a.norm_w & 15)) return 1;
-    if (a.xcopy && (a.ldxc % 4 || ((uintptr_t)a.xcopy & 15))) return 1;
+    if (a.norm_w && ((uintptr_t)a.norm_w & 15)) return false;
+    if (a.xcopy && (a.ldxc % 4 || ((uintptr_t)a.xcopy & 15))) return false;
     const bool xadd = !tab && !tabf && a.xadd != nullptr;
     if (a.xadd && (tab || tabf || ((uintptr_t)a.xadd & 15) || a.ld_xadd % 4 || a.ldb_xadd % 4 || a.n_xadd < 1 ||
                    a.n_xadd > 4))
-        return 1;
+        return false;
     const int kz = a.ypart ? a.kz : 1;
     if (a.ypart && (kz < 2 || (a.tick && kz > 4) || a.norm_w || tab || tabf || a.xcopy || a.C % (32 * kz) ||
                     ((uintptr_t)a.ypart & 3)))
-        return 1;
-    if (a.tick && (!a.ypart || !a.y || a.epi != EPI_RESID)) return 1;
+        return false;
+    if (a.tick && (!a.ypart || !a.y || a.epi != EPI_RESID)) return false;
     // K slice per wave: the fewest steps that keep <= 16 waves
     const int S = a.C / kz / 32;
     int SPW = 1;
     while (SPW < 8 && (S / SPW > 16 || S % SPW)) SPW *= 2;
-    if (S % SPW || S / SPW > 16) return 1;
+    if (S % SPW || S / SPW > 16) return false;
     const int W = S / SPW;
     const int NBC = a.nb <= 8 ? 8 : 16;
     const int PM = xadd ? (a.n_xadd <= 2 ? 2 : 4) : 0;
@@ -344,13 +346,36 @@ int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
         return SPW == 4 && tpw == 3 && PM == 4;
     };
     while (TPW > 1 && (spills(TPW) || W < TPW)) --TPW;
-    if (spills(TPW) || W < TPW) return 1;
+    if (spills(TPW) || W < TPW) return false;
     const int wreg = std::max(a.nb * (32 * SPW + 4), TPW * 256);
     const size_t smem = ((size_t)W * wreg + (size_t)W * 16) * sizeof(float);
-    if (smem > 160 * 1024) return 1;
+    if (smem > 160 * 1024) return false;
     const dim3 grid((T + TPW - 1) / TPW, kz);
-    if (a.tick && (int)grid.x > QTTS_GM_TICKS) return 1;
+    if (a.tick && (int)grid.x > QTTS_GM_TICKS) return false;
     const int src = tab ? GB_SRC_TAB : tabf ? GB_SRC_TABF : xadd ? GB_SRC_XADD : GB_SRC_X;
+    g.SPW = SPW; g.TPW = TPW; g.W = W; g.NBC = NBC; g.PM = PM; g.src = src; g.smem = smem; g.grid = grid;
+    return true;
+}
+
+bool qtts_gemvb_geom(const GemvArgs &a, int &gx, int &gz, int &rows_wg, int &ck) {
+    GbGeom g;
+    if (!gemvb_geom(a, g)) return false;
+    gx = (int)g.grid.x; gz = (int)g.grid.y; rows_wg = 16 * g.TPW; ck = a.C / gz;
+    return true;
+}
+
+int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
+    // (read per call: launches happen at graph capture, and tests switch it
+    // per model instance)
+    const char *ge = getenv("QTTS_HIP_GEMVB");
+    if (ge && !atoi(ge)) return 1;
+    const GemvArgs &a = in;
+    GbGeom g;
+    if (!gemvb_geom(a, g)) return 1;
+    const int SPW = g.SPW, TPW = g.TPW, W = g.W, NBC = g.NBC, PM = g.PM, src = g.src;
+    const size_t smem = g.smem;
+    const dim3 grid = g.grid;
+    const bool tab = a.table != nullptr, tabf = !tab && a.table_f32 != nullptr;
     const void *srcp = tab ? (const void *)a.table : tabf ? (const void *)a.table_f32 : (const void *)a.x;
     const int *idsp = (tab || tabf) ? a.ids + a.ids_off : nullptr;
     const dim3 block(64 * W);

@@ -708,11 +708,24 @@ __device__ __forceinline__ int sample_dist_nt(FastSmemNT<NT> &fs, const float (&
     if (k == 0) return 0;                     // nothing eligible: the reference returns 0
     if constexpr (STOP == 1) return (int)M;
     const uint32_t Kmax = okey(M);
+    // keys 2^31 or more below the maximum in key order (most values of the
+    // other sign -- often half the row) all count in bin FARB, one LDS atomic per wave and
+    // slot instead of 64 colliding ones; should the k-th key lie there, the
+    // bins bound more than KC candidates and the radix select takes over
+    constexpr int FARB = 32 + 16 * (31 - 5);
     int bb[EM];
 #pragma unroll
     for (int j = 0; j < EM; ++j) {
         bb[j] = DBINS;
-        if (kk[j] != 0u) { bb[j] = dist_bin(Kmax - kk[j]); atomicAdd(&fs.dh[bb[j]], 1); }
+        bool far = false;
+        if (kk[j] != 0u) {
+            const int bn = dist_bin(Kmax - kk[j]);
+            far = bn >= FARB;
+            bb[j] = far ? FARB : bn;
+            if (!far) atomicAdd(&fs.dh[bn], 1);
+        }
+        const unsigned long long fm = __ballot(far);
+        if (lane == 0 && fm) atomicAdd(&fs.dh[FARB], (int)__popcll(fm));
     }
     __syncthreads();                                                   // 2
     constexpr int BL = DBINS / 64;

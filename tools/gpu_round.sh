@@ -26,6 +26,9 @@ if [ "$MODE" = dist ]; then
   echo done; exit 0
 fi
 if [ "$MODE" = extra ]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests_extra.log 2>&1 || { echo "tests failed"; exit 1; }
+  tail -1 $O/gpu_tests_extra.log
+  timeout -k 10 60 ./tools/mb_sample > $O/mb_sample.txt 2>&1 && tail -3 $O/mb_sample.txt
   for b in 8 16; do
     timeout -k 10 600 python bench.py --batch $b --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_b$b.json 2> $O/bench_b$b.err
   done
