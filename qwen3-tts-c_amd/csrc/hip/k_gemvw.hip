@@ -150,6 +150,9 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
 #pragma unroll
     for (int i = 0; i < RW; ++i) yres[i] = y[resid ? row0 + w + 4 * i : 0];
 
+#ifdef QTTS_STAMPS
+    if (a.dbg_xfirst) __builtin_amdgcn_s_waitcnt(0);   // (diagnostics: x alone, no weight traffic behind it)
+#endif
     // 2. the whole weight slice of this lane in flight
     v4u wv[RW][NV];
 #pragma unroll
@@ -283,7 +286,9 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
             }
         }
     }
+    gw_stamp(a, 3);
     qtts_l2pf_sink(a.pf, pfr);   // (after the stores: the prefetch is off this launch's own path)
+    gw_stamp(a, 4);
 }
 
 }  // namespace

@@ -83,6 +83,9 @@ struct GemvArgs {
     const float *bias = nullptr;
     int epi = EPI_STORE;
     unsigned long long *dbg = nullptr;   // diagnostics (k_gemvb): [workgroup][8] phase stamps, 100 MHz clock
+#ifdef QTTS_STAMPS
+    int dbg_xfirst = 0;                  // (stamp builds) k_gemvw waits for x before issuing its weights
+#endif
     L2Prefetch pf;                      // batch-1 lean kernel (k_gemvw): the next launch's weights
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {

@@ -78,6 +78,11 @@ struct qtts_dev {
     hipStream_t st = nullptr;
     size_t wbytes = 0, sbytes = 0;
     std::vector<void *> wallocs, sallocs;
+    // small buffers (<= QTTS_ARENA_SMALL) are carved from 32 MB blocks
+    // (dalloc): one 2 MB-fragment mapping for every activation vector, norm
+    // weight and bias instead of a 4 KB page each
+    unsigned char *war = nullptr, *sar = nullptr;
+    size_t war_off = 0, war_cap = 0, sar_off = 0, sar_cap = 0;
     // talker
     std::vector<Layer> tl, sl;
     bf16_t *codec_emb = nullptr, *text_emb = nullptr, *fc1w = nullptr, *fc2w = nullptr, *head = nullptr;
@@ -188,9 +193,24 @@ struct qtts_dev {
 };
 
 // ----------------------------------------------------------------- helpers
+static constexpr size_t QTTS_ARENA_SMALL = (size_t)1 << 20, QTTS_ARENA_BLOCK = (size_t)32 << 20;
 static void *dalloc(qtts_dev *dv, size_t n, bool weight) {
     void *p = nullptr;
     if (n == 0) n = 16;
+    static const int arena = [] { const char *e = getenv("QTTS_HIP_ARENA"); return e ? atoi(e) : 1; }();
+    if (arena && n <= QTTS_ARENA_SMALL) {
+        unsigned char *&base = weight ? dv->war : dv->sar;
+        size_t &off = weight ? dv->war_off : dv->sar_off, &cap = weight ? dv->war_cap : dv->sar_cap;
+        const size_t need = (n + 255) & ~(size_t)255;
+        if (!base || off + need > cap) {
+            void *blk = dalloc(dv, QTTS_ARENA_BLOCK, weight);   // (recorded in wallocs / sallocs)
+            if (!blk) return nullptr;
+            base = (unsigned char *)blk; off = 0; cap = QTTS_ARENA_BLOCK;
+        }
+        p = base + off;
+        off += need;
+        return p;
+    }
     const hipError_t prior = hipPeekAtLastError();
     const hipError_t e = hipMalloc(&p, n);
     if (e != hipSuccess) {
@@ -209,6 +229,7 @@ static void free_state(qtts_dev *dv) {
     for (void *p : dv->sallocs) hipFree(p);
     dv->sallocs.clear();
     dv->sbytes = 0;
+    dv->sar = nullptr; dv->sar_off = dv->sar_cap = 0;
     dv->nb = 0;
     dv->nrun = 0;
     dv->ids_cap = 0;  // prompt scratch lived in sallocs
@@ -886,6 +907,11 @@ static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C, in
 //   launch's cur_wgs workgroups each cover next workgroups b, b + cur_wgs, ..
 //   (cur_wgs a multiple of 8: the same XCD), each slice clipped to what
 //   cap_chunks allows per covering workgroup
+#ifdef QTTS_STAMPS
+#define DBG_XFIRST(a) do { const char *e_ = getenv("QTTS_HIP_DBG_XFIRST"); (a).dbg_xfirst = e_ ? atoi(e_) : 0; } while (0)
+#else
+#define DBG_XFIRST(a) do { } while (0)
+#endif
 static L2Prefetch pf_gemvb(const qtts_dev *dv, const bf16_t *W, int R, int C, int nb, int kz, int n_xadd,
                            int cur_wgs, int cap_chunks) {
     L2Prefetch p;
@@ -1087,7 +1113,7 @@ static int subtalker(qtts_dev *dv) {
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             // QTTS_HIP_GM_DBG at batch 1: stamps of pass 5, layer 2's q|k|v / gate|up / down
             const bool sdbg = dv->gm_dbg && nb == 1 && g == 5 && l == 2;
-            if (sdbg) a.dbg = dv->gm_dbg;
+            if (sdbg) { a.dbg = dv->gm_dbg; DBG_XFIRST(a); }
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
             AttnArgs t;
@@ -1148,7 +1174,7 @@ static int subtalker(qtts_dev *dv) {
             a = gv(ly.wgu, 2 * d.Is, d.Hs, xa, d.Hs, dv->h_s, d.Is, nb, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
             if (pfm & 4) a.pf = pf_gemvw(dv, ly.wdown, d.Hs, d.Is);
-            if (sdbg) a.dbg = dv->gm_dbg + 2 * 2048 * 8;
+            if (sdbg) { a.dbg = dv->gm_dbg + 2 * 2048 * 8; DBG_XFIRST(a); }
             if (tab0) set_src(a);   // the residual is the input table row (x_st was not written)
             if (fused_o) {
                 add_in(a, dv->opart, d.KVs, d.Hs, nb, xb);
@@ -1164,7 +1190,7 @@ static int subtalker(qtts_dev *dv) {
                 if (l + 1 < d.Ls) a.pf = pf_gemvw(dv, dv->sl[l + 1].wqkv, QKV, d.Hs);
                 else if (g >= 1) a.pf = pf_gemvw(dv, dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs);
             }
-            if (sdbg) a.dbg = dv->gm_dbg + 3 * 2048 * 8;
+            if (sdbg) { a.dbg = dv->gm_dbg + 3 * 2048 * 8; DBG_XFIRST(a); }
             if (kzd && split_out(dv, a, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
             if (pfb) {   // down -> the next layer's q|k|v, or the head
                 const int np2 = pend ? npend : 0, cw = gemvb_wgs(a);
@@ -1462,7 +1488,7 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
         std::vector<unsigned long long> h(4 * 2048 * 8);
         CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
         static const char *op[4] = {"q|k|v", "O / -", "gate|up", "down"};
-        static const char *ph[5] = {"start", "x staged", "dot done", "barrier", "end (wg 0)"};
+        static const char *ph[5] = {"start", "x staged", "dot done", "epilogue", "pf landed"};
         for (int g = 0; g < 4; ++g) {
             const unsigned long long *b = h.data() + (size_t)g * 2048 * 8;
             unsigned long long t0 = ~0ull;
