@@ -168,6 +168,7 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
     L2PfRegs pfr;
     qtts_l2pf_issue<256, NT>(a.pf, blockIdx.x + gridDim.x * blockIdx.y, pfr, W);
 
+    if constexpr (AM) gw_stamp(a, 5);
     if constexpr (AM) {   // 3a. the attention merge, split order (k_attn_dec's last-split merge)
         const int HDm = a.am_hd, GP = a.am_gph, NO = GP * HDm, stride = NO + 2 * GP;
         const int nact = (am_p + 1 + a.am_ch - 1) / a.am_ch;
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
             }
             xv[q] = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
         }
+        gw_stamp(a, 6);
     }
     // 3. residual + partials summed in partial order, RMS statistic
     if (trow) {

@@ -78,9 +78,9 @@ struct qtts_dev {
     hipStream_t st = nullptr;
     size_t wbytes = 0, sbytes = 0;
     std::vector<void *> wallocs, sallocs;
-    // small buffers (<= QTTS_ARENA_SMALL) are carved from 32 MB blocks
-    // (dalloc): one 2 MB-fragment mapping for every activation vector, norm
-    // weight and bias instead of a 4 KB page each
+    // QTTS_HIP_ARENA=1: small buffers (<= QTTS_ARENA_SMALL) carved from
+    // 32 MB blocks (dalloc): one 2 MB-fragment mapping for every activation
+    // vector, norm weight and bias instead of one allocation each
     unsigned char *war = nullptr, *sar = nullptr;
     size_t war_off = 0, war_cap = 0, sar_off = 0, sar_cap = 0;
     // talker
@@ -197,7 +197,10 @@ static constexpr size_t QTTS_ARENA_SMALL = (size_t)1 << 20, QTTS_ARENA_BLOCK = (
 static void *dalloc(qtts_dev *dv, size_t n, bool weight) {
     void *p = nullptr;
     if (n == 0) n = 16;
-    static const int arena = [] { const char *e = getenv("QTTS_HIP_ARENA"); return e ? atoi(e) : 1; }();
+    // (off by default: +1.2 % in one same-box A/B, -1.3 % in the next,
+    // profiles/r04g_ab_arena.txt; read per call: tests switch it per model)
+    const char *ae = getenv("QTTS_HIP_ARENA");
+    const int arena = ae ? atoi(ae) : 0;
     if (arena && n <= QTTS_ARENA_SMALL) {
         unsigned char *&base = weight ? dv->war : dv->sar;
         size_t &off = weight ? dv->war_off : dv->sar_off, &cap = weight ? dv->war_cap : dv->sar_cap;
@@ -1112,7 +1115,7 @@ static int subtalker(qtts_dev *dv) {
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
             // QTTS_HIP_GM_DBG at batch 1: stamps of pass 5, layer 2's q|k|v / gate|up / down
-            const bool sdbg = dv->gm_dbg && nb == 1 && g == 5 && l == 2;
+            const bool sdbg = dv->gm_dbg && dv->gm_dbg_layer == 99 && nb == 1 && g == 5 && l == 2;
             if (sdbg) { a.dbg = dv->gm_dbg; DBG_XFIRST(a); }
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
@@ -1488,12 +1491,12 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
         std::vector<unsigned long long> h(4 * 2048 * 8);
         CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
         static const char *op[4] = {"q|k|v", "O / -", "gate|up", "down"};
-        static const char *ph[5] = {"start", "x staged", "dot done", "epilogue", "pf landed"};
+        static const char *ph[7] = {"start", "x staged", "dot done", "epilogue", "pf landed", "w issued", "merged"};
         for (int g = 0; g < 4; ++g) {
             const unsigned long long *b = h.data() + (size_t)g * 2048 * 8;
             unsigned long long t0 = ~0ull;
             for (int i = 0; i < 2048; ++i) if (b[i * 8] && b[i * 8] < t0) t0 = b[i * 8];
-            for (int k = 0; k < 5; ++k) {
+            for (int k = 0; k < 7; ++k) {
                 std::vector<double> v;
                 for (int i = 0; i < 2048; ++i) if (b[i * 8 + k]) v.push_back((b[i * 8 + k] - t0) * 0.01);
                 if (v.empty()) continue;

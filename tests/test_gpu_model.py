@@ -119,14 +119,15 @@ def test_eos_stop_reported_like_reference(gpu):
 
 
 @pytest.mark.parametrize("env", [{}, {"QTTS_HIP_BSPLIT": "0"}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"},
-                                 {"QTTS_HIP_BKZ_MAX": "4"}])
+                                 {"QTTS_HIP_BKZ_MAX": "4"}, {"QTTS_HIP_L2PF": "63"}])
 def test_batch_slots_match_single_runs(tiny_dir, oracle, monkeypatch, env):
     """Lock-step batch (B GEMV columns, one weight read per frame): every
     slot's audio equals the oracle's for its own prompt / speaker -- with the
     O / down projections split over K (partials added by the next residual
     reader) and without, on the staged-plane batch GEMV (k_gemvm) instead of
     the per-wave-slice one (k_gemvb), with every split-K producer reducing its
-    own partials, and with up to 4 split-K columns."""
+    own partials, with up to 4 split-K columns, and with the batch chain's
+    next-launch L2 prefetch."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     m = qtts.QwenTTS(tiny_dir)
@@ -332,12 +333,13 @@ def test_cli_stream_flag(tiny_dir):
 
 
 @pytest.mark.parametrize("env", [{"QTTS_HIP_PTAB": "0"}, {"QTTS_HIP_ATTN_O": "0"}, {"QTTS_HIP_NO_GRAPH": "1"},
-                                 {"QTTS_HIP_L2PF": "0"}, {"QTTS_HIP_SAMPLE_W": "0"}])
+                                 {"QTTS_HIP_L2PF": "0"}, {"QTTS_HIP_SAMPLE_W": "0"}, {"QTTS_HIP_ARENA": "1"}])
 def test_e2e_debug_switch_paths(tiny_dir, monkeypatch, env):
     """The debug switches' paths stay bit-exact: the per-pass input projection
     instead of the projected tables, sub-talker attention and O projection as
     two kernels, eager launches instead of the frame graphs, no next-launch
-    L2 prefetch, the 256-thread sampler (the default path is covered by
+    L2 prefetch, the 256-thread sampler, small buffers carved from 32 MB blocks
+    (the default path is covered by
     test_e2e_codes_bit_exact_and_audio)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
