@@ -541,6 +541,24 @@ __global__ __launch_bounds__(256) void k_attn_short(AttnArgs a) {
     __shared__ float sc[2 * 16];
     attn_short_wg<HD, false>(a, blockIdx.x, blockIdx.y, lq, sc, nullptr, true, NoIssue(),
                              a.qkv_tab ? a.qkv_tab : a.qkv, a.qkv_tab ? a.tab_ids + a.tab_off : nullptr);
+    if (a.xc_dst && blockIdx.x == 0) {   // the input row as the residual (AttnArgs::xc_dst)
+        const int r = blockIdx.y;
+        const int *ip = a.tab_ids + a.tab_off + (size_t)r * a.tab_bstride;
+        if (a.tab_row_sel) ip += (size_t)a.tab_row_sel[r] * a.tab_rstride;
+        const size_t row = (size_t)(*ip) * a.xc_n;
+        float *dst = a.xc_dst + (size_t)r * a.xc_n;
+        for (int c = 4 * (int)threadIdx.x; c < a.xc_n; c += 4 * (int)blockDim.x) {
+            float4 v;
+            if (a.xc_tab) {
+                v = *reinterpret_cast<const float4 *>(a.xc_tab + row + c);
+            } else {
+                const uint2 u = *reinterpret_cast<const uint2 *>(a.xc_tab16 + row + c);
+                v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u),
+                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xFFFF0000u));
+            }
+            *reinterpret_cast<float4 *>(dst + c) = v;
+        }
+    }
 }
 
 // Short-context attention + the O projection split by kv head (the
@@ -649,6 +667,11 @@ int qtts_attention(const AttnArgs &a, hipStream_t st) {
     }
     const int gph = a.NH / a.KV;
     const bool hd_ok = a.HD == 128 || a.HD == 64 || a.HD == 32 || a.HD == 16;
+    if (a.xc_dst && (!(a.mode == 0 && a.win == 0 && gph == 2 && hd_ok && a.S <= 16) || !a.qkv_tab ||
+                     (!a.xc_tab && !a.xc_tab16) || a.xc_n % 4 || ((uintptr_t)a.xc_dst & 15))) {
+        fprintf(stderr, "qtts_attention: residual copy (xc_dst) only on the short table path\n");
+        return -1;
+    }
     if (a.mode == 0 && a.win == 0 && gph == 2 && hd_ok && a.S <= 16) {
         const dim3 grid(a.KV, a.nrows);
         switch (a.HD) {

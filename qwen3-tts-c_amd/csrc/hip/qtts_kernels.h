@@ -144,6 +144,14 @@ struct AttnArgs {
     // prologue) instead of the last split's
     int defer = 0;
     L2Prefetch pf;                 // k_attn_o: the next launch's weights
+    // k_attn_short with a q|k|v table (the batch sub-talker's layer 0): kv
+    // head 0's workgroup of row r also copies the input row of id(r) (the
+    // table ids above) from xc_tab (fp32) or xc_tab16 (bf16) to xc_dst + r
+    // xc_n -- the residual the skipped q|k|v GEMV would have copied
+    const float *xc_tab = nullptr;
+    const bf16_t *xc_tab16 = nullptr;
+    float *xc_dst = nullptr;
+    int xc_n = 0;
     // lanes per key of the split kernel at HD 128 (4 / 8 / 16), latched by the
     // model at creation (QTTS_HIP_ATTN_LPK); 0 = the default for HD / defer
     int lpk = 0;

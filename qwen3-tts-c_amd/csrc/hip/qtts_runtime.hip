@@ -169,6 +169,7 @@ struct qtts_dev {
     std::vector<Prof> prof;
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
+    bool tab0b = true;       // QTTS_HIP_TAB0B=0: batch layer-0 q|k|v by GEMV instead of the table
     // QTTS_HIP_L2PF=<mask>: which edges of the batch-1 sub-talker chain carry
     // the next-launch weight prefetch (0 none): 1 q|k|v -> attention + O,
     // 2 attention + O -> gate|up, 4 gate|up -> down, 8 down -> next q|k|v or
@@ -420,6 +421,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_lpk = lk ? atoi(lk) : 0;
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
+    const char *tb = getenv("QTTS_HIP_TAB0B");
+    dv->tab0b = !(tb && !atoi(tb));
     const char *pf = getenv("QTTS_HIP_L2PF");
     if (pf) dv->l2pf = atoi(pf);
     const char *pft = getenv("QTTS_HIP_L2PF_TK");
@@ -1140,11 +1143,18 @@ static int subtalker(qtts_dev *dv) {
             // (batch 1 only: at batch 8 / 16 the per-row recompute measured slower than
             // the separate attention + split-K O projection, 98 vs 107 / 132 vs 155
             // audio-s/s, profiles/r01av_bench_batch_attn_o.txt)
-            if (tab0) {
+            // batch, pass g >= 1, layer 0: the same table, read by the short
+            // attention kernel, which also copies the input row to the
+            // residual (AttnArgs::xc_dst; the skipped GEMV's xcopy)
+            const bool hd_ok = d.HDs == 128 || d.HDs == 64 || d.HDs == 32 || d.HDs == 16;
+            const bool tab0b = l == 0 && g >= 1 && nb >= 2 && dv->tab0b && dv->qkv0_tab && (!proj || ptab) &&
+                               d.NHs == 2 * d.KVs && d.G <= 16 && hd_ok;
+            if (tab0 || tab0b) {
                 t.qkv_tab = dv->qkv0_tab + (g == 1 ? 0 : (size_t)d.V + (size_t)(g - 2) * d.Vs) * QKV;
                 t.tab_ids = src.ids; t.tab_bstride = src.ids_bstride; t.tab_row_sel = src.row_sel;
                 t.tab_rstride = src.ids_rstride; t.tab_off = src.ids_off;
             }
+            if (tab0b) { t.xc_tab = src.table_f32; t.xc_tab16 = src.table; t.xc_dst = xa; t.xc_n = d.Hs; }
             if (pfm & 1) a.pf = pf_attn_o(dv, ly.wo, d.Hs, d.NHs, d.HDs);
             if (pfm & 2) t.pf = kv_only ? first_op_pf(g + 1) : pf_gemvw(dv, ly.wgu, 2 * d.Is, d.Hs);
             // batch: q|k|v -> O (two launches ahead, the attention in between)
@@ -1166,7 +1176,12 @@ static int subtalker(qtts_dev *dv) {
                     fused_o = true;
                 }
             } else {
-                CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
+                if (tab0b) {
+                    ProfScope pa(dv, PK_ATTN, 0);
+                    CKI(qtts_attention(t, st));
+                } else {
+                    CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
+                }
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 o.y = xa;
                 if (kzo) opend = split_out(dv, o, dv->bpo, kzo);
