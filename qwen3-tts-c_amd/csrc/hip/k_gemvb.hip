@@ -38,7 +38,6 @@
 #include <algorithm>
 
 #include "qtts_gemvm_dev.h"
-#include "qtts_l2pf.h"
 
 namespace {
 
@@ -197,9 +196,6 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
 #pragma unroll
         for (int t = 0; t < TPW; ++t)
             wv[t][j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rw, wo[t] + 64u * j, 0, 0));
-    // the next launch's weight slices into this XCD's L2 (GemvArgs::pf)
-    L2PfRegs pfr;
-    qtts_l2pf_issue<1024, false, 2>(a.pf, blockIdx.x + gridDim.x * blockIdx.y, pfr, Wt, (int)blockDim.x);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave writes and reads its rows: LDS is in order
     gb_stamp(a, 1);
 
@@ -273,10 +269,9 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
             }
         }
         reduce_last(a, 16 * TPW, reinterpret_cast<int *>(ssq));
-        qtts_l2pf_sink(a.pf, pfr);
         return;
     }
-    if (!tile_wave) { qtts_l2pf_sink(a.pf, pfr); return; }
+    if (!tile_wave) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int bb = 4 * (lane >> 4) + i;
@@ -291,7 +286,6 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
         epilogue(a, bb, r, val, up);
     }
     gb_stamp(a, 4);
-    qtts_l2pf_sink(a.pf, pfr);
 }
 
 }  // namespace
@@ -354,13 +348,6 @@ static bool gemvb_geom(const GemvArgs &a, GbGeom &g) {
     if (a.tick && (int)grid.x > QTTS_GM_TICKS) return false;
     const int src = tab ? GB_SRC_TAB : tabf ? GB_SRC_TABF : xadd ? GB_SRC_XADD : GB_SRC_X;
     g.SPW = SPW; g.TPW = TPW; g.W = W; g.NBC = NBC; g.PM = PM; g.src = src; g.smem = smem; g.grid = grid;
-    return true;
-}
-
-bool qtts_gemvb_geom(const GemvArgs &a, int &gx, int &gz, int &rows_wg, int &ck) {
-    GbGeom g;
-    if (!gemvb_geom(a, g)) return false;
-    gx = (int)g.grid.x; gz = (int)g.grid.y; rows_wg = 16 * g.TPW; ck = a.C / gz;
     return true;
 }
 

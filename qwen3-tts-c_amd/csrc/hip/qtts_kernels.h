@@ -18,15 +18,11 @@ enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SILU = 2, EPI_RESID = 3, EPI_SWIGLU
 // (rows of 2^lg chunks at stride ld; chunks <= threads x QTTS_PF_LOADS).  One
 // 4-B load per chunk brings its line in.
 constexpr int QTTS_PF_LOADS = 4;
-// A prefetching workgroup b covers the next launch's workgroups t = b + i *
-// tstride (i < ntgt, t < tmax): with tstride a multiple of 8 they share b's XCD.
 struct L2Prefetch {
     const unsigned char *base = nullptr;   // nullptr: none
     int pm = 1 << 30;
     long long pa = 0, pb = 0;
-    int chunks = 0, lg = 30, ld = 0;       // per target
-    int ntgt = 1, tstride = 0, tmax = 1 << 30;
-    unsigned cmax = 0xFFFFFFFFu;           // last chunk column of a row slice
+    int chunks = 0, lg = 30, ld = 0;
     unsigned *sink = nullptr;              // never written (the loads' values are folded into a test)
 };
 
@@ -95,9 +91,7 @@ struct GemvArgs {
         if (table_f32) return C % 4 == 0 && ((uintptr_t)table_f32 & 15) == 0 && nw_ok;
         return ((uintptr_t)x & 15) == 0 && nw_ok;
     }
-};// the batch GEMV's launch geometry for these arguments (k_gemvb.hip; false:
-// not covered): grid gx x gz workgroups, rows_wg weight rows and ck columns each
-bool qtts_gemvb_geom(const GemvArgs &a, int &gx, int &gz, int &rows_wg, int &ck);
+};
 
 int qtts_gemv(const GemvArgs &a, hipStream_t st);
 // batch-1 wave-per-row GEMV for Infinity-Cache-resident weights (k_gemvw.hip); 1 = not covered

@@ -174,9 +174,8 @@ struct qtts_dev {
     // the next-launch weight prefetch (0 none): 1 q|k|v -> attention + O,
     // 2 attention + O -> gate|up, 4 gate|up -> down, 8 down -> next q|k|v or
     // head, 16 head -> the next pass's first launch (two launches ahead);
-    // 32: the batch (2-16 rows) chain on k_gemvb (off by default: batch 8
-    // 138.7 / 138.8 vs 141.3 / 141.4, batch 16 221.8 / 221.4 vs 224.7 / 224.7
-    // audio-s/s with it, same box, profiles/r04g_ab_l2pf_batch.txt)
+    // (the same for the batch chain on k_gemvb measured 2 % slower at batch 8
+    // and 16, profiles/r04g_ab_l2pf_batch.txt, and was removed)
     int l2pf = 31;
     int l2pf_tk = 0;         // QTTS_HIP_L2PF_TK bits (batch-1 talker, non-temporal): 1 q|k|v -> O's W_o, 2 O -> gate|up
     unsigned *pf_sink = nullptr;
@@ -909,46 +908,11 @@ static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C, in
     p.sink = dv->pf_sink;
     return p;
 }
-//   k_gemvb (batch 2-16, grid gx x gz, rows_wg x ck slices at (x, z)): this
-//   launch's cur_wgs workgroups each cover next workgroups b, b + cur_wgs, ..
-//   (cur_wgs a multiple of 8: the same XCD), each slice clipped to what
-//   cap_chunks allows per covering workgroup
 #ifdef QTTS_STAMPS
 #define DBG_XFIRST(a) do { const char *e_ = getenv("QTTS_HIP_DBG_XFIRST"); (a).dbg_xfirst = e_ ? atoi(e_) : 0; } while (0)
 #else
 #define DBG_XFIRST(a) do { } while (0)
 #endif
-static L2Prefetch pf_gemvb(const qtts_dev *dv, const bf16_t *W, int R, int C, int nb, int kz, int n_xadd,
-                           int cur_wgs, int cap_chunks) {
-    L2Prefetch p;
-    if (!(dv->l2pf & 32) || cur_wgs < 8 || cur_wgs % 8) return p;
-    static float dummy[4] __attribute__((aligned(16)));
-    GemvArgs g;
-    g.W = W; g.R = R; g.C = C; g.nb = nb; g.x = dummy; g.ldx = C; g.y = dummy; g.ldy = R;
-    if (kz > 1) { g.ypart = dummy; g.kz = kz; g.y = nullptr; }
-    if (n_xadd > 0) { g.xadd = dummy; g.n_xadd = n_xadd; g.ld_xadd = nb * C; g.ldb_xadd = C; }
-    int gx, gz, rows, ck;
-    if (!qtts_gemvb_geom(g, gx, gz, rows, ck)) return p;
-    const int cpr = ck * 2 / 64;
-    if (cpr < 1 || ck * 2 % 64) return p;
-    int lg = 0;
-    while ((1 << lg) < cpr) ++lg;
-    const int T = gx * gz, ntgt = (T + cur_wgs - 1) / cur_wgs;
-    // (the last row slice may be short: every target prefetches at most its rows)
-    int rows_pf = std::min(rows, R - (gx - 1) * rows);
-    while (rows_pf > 1 && ntgt * (rows_pf << lg) > cap_chunks) rows_pf /= 2;
-    if (rows_pf < 1 || ntgt * (rows_pf << lg) > cap_chunks) return p;
-    p.base = reinterpret_cast<const unsigned char *>(W);
-    p.pm = gx; p.pa = (long long)rows * C * 2; p.pb = (long long)ck * 2;
-    p.chunks = rows_pf << lg; p.lg = lg; p.ld = C * 2;
-    p.ntgt = ntgt; p.tstride = cur_wgs; p.tmax = T; p.cmax = (unsigned)cpr - 1u; p.sink = dv->pf_sink;
-    return p;
-}
-// the current batch launch's workgroup count (0: not on k_gemvb)
-static int gemvb_wgs(const GemvArgs &a) {
-    int gx, gz, rows, ck;
-    return qtts_gemvb_geom(a, gx, gz, rows, ck) ? gx * gz : 0;
-}
 //   k_attn_o (grid (R / RPW, KV), linear b = rb + (R / RPW) kvh): rows
 //   [RPW rb, +RPW) x columns [2 HD kvh, +2 HD) of W_o [R][NH HD]
 static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH, int HD) {
@@ -1157,9 +1121,6 @@ static int subtalker(qtts_dev *dv) {
             if (tab0b) { t.xc_tab = src.table_f32; t.xc_tab16 = src.table; t.xc_dst = xa; t.xc_n = d.Hs; }
             if (pfm & 1) a.pf = pf_attn_o(dv, ly.wo, d.Hs, d.NHs, d.HDs);
             if (pfm & 2) t.pf = kv_only ? first_op_pf(g + 1) : pf_gemvw(dv, ly.wgu, 2 * d.Is, d.Hs);
-            // batch: q|k|v -> O (two launches ahead, the attention in between)
-            const bool pfb = nb >= 2 && (dv->l2pf & 32);
-            if (pfb && !kv_only) a.pf = pf_gemvb(dv, ly.wo, d.Hs, AD, nb, kzo, 0, gemvb_wgs(a), 1536);
             if (dv->attn_o && nb == 1) {
                 if (!tab0) CKI(pgemv(dv, a, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
@@ -1185,7 +1146,6 @@ static int subtalker(qtts_dev *dv) {
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 o.y = xa;
                 if (kzo) opend = split_out(dv, o, dv->bpo, kzo);
-                if (pfb) o.pf = pf_gemvb(dv, ly.wgu, 2 * d.Is, d.Hs, nb, 1, opend ? kzo : 0, gemvb_wgs(o), 1536);
                 if (!kv_only) CKI(pgemv(dv, o, PK_GEMV_SUB));
             }
             if (kv_only) break;
@@ -1199,7 +1159,6 @@ static int subtalker(qtts_dev *dv) {
             } else if (opend) {
                 add_in(a, dv->bpo, kzo, d.Hs, nb, xb);
             }
-            if (pfb) a.pf = pf_gemvb(dv, ly.wdown, d.Hs, d.Is, nb, kzd, 0, gemvb_wgs(a), 1536);
             CKI(pgemv(dv, a, PK_GEMV_SUB));
             if (fused_o || opend) std::swap(xa, xb);
             a = gv(ly.wdown, d.Hs, d.Is, dv->h_s, d.Is, xa, d.Hs, nb, EPI_RESID);
@@ -1210,12 +1169,6 @@ static int subtalker(qtts_dev *dv) {
             }
             if (sdbg) { a.dbg = dv->gm_dbg + 3 * 2048 * 8; DBG_XFIRST(a); }
             if (kzd && split_out(dv, a, dv->bpd, kzd)) { pend = dv->bpd; npend = kzd; }
-            if (pfb) {   // down -> the next layer's q|k|v, or the head
-                const int np2 = pend ? npend : 0, cw = gemvb_wgs(a);
-                if (l + 1 < d.Ls) a.pf = pf_gemvb(dv, dv->sl[l + 1].wqkv, QKV, d.Hs, nb, 1, np2, cw, 1536);
-                else if (g >= 1)
-                    a.pf = pf_gemvb(dv, dv->lm + (size_t)(g - 1) * d.Vs * d.Hs, d.Vs, d.Hs, nb, 1, np2, cw, 1536);
-            }
             CKI(pgemv(dv, a, PK_GEMV_SUB));
         }
         if (g == 0) continue;  // pass 0 produces no logits
@@ -1224,8 +1177,6 @@ static int subtalker(qtts_dev *dv) {
         a.norm_w = dv->st_norm; a.eps = d.eps; a.nt = 0;
         if (pend) add_in(a, pend, npend, d.Hs, nb, nullptr);
         if (pfm & 16) a.pf = first_op_pf(g + 1);   // (two launches ahead: the sampler runs in between)
-        if (nb >= 2 && (dv->l2pf & 32) && g + 1 < d.G)   // batch: the next pass's layer-0 q|k|v
-            a.pf = pf_gemvb(dv, dv->sl[0].wqkv, QKV, d.Hs, nb, 1, 0, gemvb_wgs(a), 1536);
         SampArgs s;
         s.logits = dv->logits_s; s.ld = d.Vs; s.n = d.Vs; s.nb = nb;
         s.top_k = dv->par.st_top_k; s.top_p = dv->par.st_top_p; s.temp = dv->par.st_temperature;

@@ -119,16 +119,15 @@ def test_eos_stop_reported_like_reference(gpu):
 
 
 @pytest.mark.parametrize("env", [{}, {"QTTS_HIP_BSPLIT": "0"}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"},
-                                 {"QTTS_HIP_BKZ_MAX": "4"}, {"QTTS_HIP_L2PF": "63"}, {"QTTS_HIP_TAB0B": "0"}])
+                                 {"QTTS_HIP_BKZ_MAX": "4"}, {"QTTS_HIP_TAB0B": "0"}])
 def test_batch_slots_match_single_runs(tiny_dir, oracle, monkeypatch, env):
     """Lock-step batch (B GEMV columns, one weight read per frame): every
     slot's audio equals the oracle's for its own prompt / speaker -- with the
     O / down projections split over K (partials added by the next residual
     reader) and without, on the staged-plane batch GEMV (k_gemvm) instead of
     the per-wave-slice one (k_gemvb), with every split-K producer reducing its
-    own partials, with up to 4 split-K columns, with the batch chain's
-    next-launch L2 prefetch, and with layer 0's q|k|v by GEMV instead of the
-    load-time table (passes >= 1)."""
+    own partials, with up to 4 split-K columns, and with layer 0's q|k|v by
+    GEMV instead of the load-time table (passes >= 1)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     m = qtts.QwenTTS(tiny_dir)
