@@ -14,7 +14,8 @@ struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
 // displace the sub-talker's weights from the Infinity Cache)
 // Single target (workgroup b's slice of the next launch; the batch-1
 // kernels): the slice base is uniform, one scalar division per launch.
-template <int NT, bool NTL = false>
+// CS: log2 of the bytes one load stands for (64; 128 = one load per L2 line)
+template <int NT, bool NTL = false, int CS = 6>
 __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
     const unsigned char *st = p.base ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
                                      : reinterpret_cast<const unsigned char *>(fallback);
@@ -26,7 +27,7 @@ __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2Pf
     for (int j = 0; j < QTTS_PF_LOADS; ++j) {
         const unsigned c0 = threadIdx.x + NT * j;
         const unsigned c = c0 < n ? c0 : 0u;
-        off[j] = (c >> p.lg) * (unsigned)p.ld + ((c & m) << 6);
+        off[j] = (c >> p.lg) * (unsigned)p.ld + ((c & m) << CS);
     }
 #pragma unroll
     for (int j = 0; j < QTTS_PF_LOADS; ++j) {

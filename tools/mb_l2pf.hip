@@ -13,6 +13,7 @@
 //   pf 3   the product's form (qtts_l2pf.h): one 4-B load per 64-B chunk,
 //          offsets computed by selects first (pf 1's per-lane conditions make
 //          the compiler reuse in-flight registers and wait for every load)
+//   pf 4   the same with one load per 128 B (one per L2 line)
 //   hot    every op reads the SAME weights (L2-resident upper bound)
 //
 //   hipcc -O3 --offload-arch=gfx950 -Iqwen3-tts-c_amd/csrc/hip tools/mb_l2pf.hip -o tools/mb_l2pf && tools/mb_l2pf
@@ -76,13 +77,14 @@ __global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out, u
         }
 #pragma unroll
         for (int j = 0; j < 12; ++j) acc ^= pv[j].x;
-    } else if constexpr (PF == 3) {
-        // (the next op's slice: contiguous nbytes)
+    } else if constexpr (PF == 3 || PF == 4) {
+        // (the next op's slice: contiguous nbytes; PF 4: one load per 128 B)
+        constexpr int CS = PF == 4 ? 7 : 6;
         L2Prefetch p;
         p.base = reinterpret_cast<const unsigned char *>(o.nW); p.pa = (long long)nbytes; p.pb = 0;
-        p.chunks = (int)(nbytes / 64); p.lg = 30; p.ld = 0; p.sink = sink;
+        p.chunks = (int)(nbytes >> CS); p.lg = 30; p.ld = 0; p.sink = sink;
         L2PfRegs r;
-        qtts_l2pf_issue<256>(p, blockIdx.x, r, o.W);
+        qtts_l2pf_issue<256, false, CS>(p, blockIdx.x, r, o.W);
 #pragma unroll
         for (int j = 0; j < QTTS_PF_LOADS; ++j) acc ^= r.v[j];
     } else if constexpr (PF == 2) {
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out, u
         s = wsum(s);
         if (lane == 0) out[blockIdx.x * 4 * RW + w + 4 * i] = s * 1e-3f;
     }
-    if constexpr (PF == 1 || PF == 3)
+    if constexpr (PF == 1 || PF == 3 || PF == 4)
         if (acc == 0x9E3779B9u && threadIdx.x == 0) sink[0] = acc;
 }
 
@@ -180,9 +182,10 @@ int main() {
         float t1 = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (auto &o : ops) { DISPATCH(o, 1, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
         float t2 = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (auto &o : ops) { DISPATCH(o, 2, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
         float t3 = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (auto &o : ops) { DISPATCH(o, 3, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
+        float t4 = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (auto &o : ops) { DISPATCH(o, 4, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
         // hot: every launch of a shape reads the first layer's matrix of that shape
         float th = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (size_t k = 0; k < ops.size(); ++k) { Op o = ops[k % 4]; DISPATCH(o, 0, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
-        printf("us per op: pf0 %.2f  pf1 %.2f  pf2 %.2f  pf3 %.2f  hot %.2f\n", t0, t1, t2, t3, th);
+        printf("us per op: pf0 %.2f  pf1 %.2f  pf2 %.2f  pf3 %.2f  pf4 %.2f  hot %.2f\n", t0, t1, t2, t3, t4, th);
     }
     return 0;
 }
