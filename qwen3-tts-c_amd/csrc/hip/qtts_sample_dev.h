@@ -1048,7 +1048,10 @@ __device__ __forceinline__ void sample_row(const SampArgs &a, int b, unsigned ch
                 a.n_gen[b] = ng + 1;
                 a.st_rng[b] = a.seed_bits;
             }
-            if (a.out_tok) a.out_tok[b] = tok;
+            // the sub-talker's table readers take this id (pass 1) and keep it
+            // for a stopped row (its samplers return early): EOS (>= Vs) would
+            // index past the last pass's table, so a stop leaves id 0
+            if (a.out_tok) a.out_tok[b] = (a.fixed == 0 && tok == a.eos) ? 0 : tok;
         } else {
             a.st_rng[b] = rng;
             if (a.codes) a.codes[(size_t)b * a.codes_bstride + (size_t)a.cur_row[b] * a.G + a.g] = tok;

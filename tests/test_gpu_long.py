@@ -202,3 +202,25 @@ def test_hd128_attention_switch_paths_vs_reference(gpu, monkeypatch, env, frames
         _codes_equal(m.last_codes(), g["decode_codes"][:frames], f"hd128 {frames} frames {env}")
     finally:
         m.close()
+
+
+def test_eos_stop_17b_batch_1_and_3(gpu):
+    """EOS mode (the reference's default: max_new_tokens 4096, stop at EOS,
+    Q.c:1282-1330) on the synthetic 1.7B whose codec-head EOS row is scaled
+    x1.4 (bench.py --eos): the utterance stops well inside the capacity, alone
+    and in a lock-step batch of 3 where the other rows keep decoding after
+    one stops.  Regression: a stopped row's table id (the talker's EOS id, >=
+    the sub-talker vocabulary) indexed past the last pass's q|k|v / input
+    table."""
+    from synth_model import prompt_ids
+    m = qtts.QwenTTS(model_dir("1.7b", eos_gain=1.4))
+    try:
+        m.set_params(max_tokens=4096, fixed=0, seed=42, **DEFAULT)
+        a = m.generate(prompt_ids("p128", seed=1234), "aiden", "english")
+        assert a is not None and len(a) > 0
+        assert m.c.last_stop_reason == 1 and 0 < m.c.last_stop_step < 4096
+        prompts = [prompt_ids("p128", seed=1234 + i) for i in range(3)]
+        rc, aud = m.generate_batch(prompts, ["aiden", "vivian", "serena"], ["english"] * 3)
+        assert rc == 0 and all(x is not None and len(x) > 0 for x in aud)
+    finally:
+        m.close()
