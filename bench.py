@@ -194,6 +194,21 @@ def profile_roofline(m, lib, variant=""):
                 gemv_ms_per_frame=float(t[(k == 0) | (k == 1)].sum()))
 
 
+def hbm_stream_bw(lib, gib=2, iters=10):
+    """This GPU's own HBM stream bandwidth (the roofline against
+    a stream figure measured on the box beside the 8 TB/s nominal):
+    qtts_hip_hbm_bw's non-temporal float4 read stream and float4 copy over
+    2 GiB buffers (>> the 256 MB Infinity Cache), HIP events on their stream."""
+    import ctypes as C
+    lib.qtts_hip_hbm_bw.restype = C.c_int
+    lib.qtts_hip_hbm_bw.argtypes = [C.c_size_t, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    rd, cp = C.c_double(0), C.c_double(0)
+    if lib.qtts_hip_hbm_bw(gib << 30, iters, C.byref(rd), C.byref(cp)) != 0:
+        return None
+    return {"read_GBs": round(rd.value, 1), "copy_GBs": round(cp.value, 1), "buffer_GiB": gib, "iters": iters,
+            "kernel": "qtts_hip_hbm_bw (k_membw.hip): nt float4 loads, 8 per lane in flight, 8 WG x 256 thr per CU"}
+
+
 def lscpu():
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -561,6 +576,7 @@ def main():
     # (the 0.6B line reads the 0.6B profile passes: <tag>_06b_kernel_stats.csv / _pmc.json)
     roof = None if args.no_profile or vc is not None else profile_roofline(
         m, qtts.lib(), "" if args.preset == "1.7b" else args.preset.replace(".", "") + "_")
+    hbm = None if args.no_profile else hbm_stream_bw(qtts.lib())
     m.close()
 
     cpu = None
@@ -632,6 +648,8 @@ def main():
                                      "bytes_per_frame": int(fw + KV_BYTES_PER_POS * pos * args.batch) // args.batch,
                                      "mean_kv_pos": pos,
                                      "achieved_fp32_kv": round(ach32, 1),
+                                     "measured_stream": hbm,
+                                     "frac_of_measured_read": round(ach / hbm["read_GBs"], 4) if hbm else None,
                                      "note": "SURVEY.md 8(d): frames/s x (W + 114688 B x pos) / 8 TB/s, KV at 2 B/elem; "
                                              "this build keeps the reference's fp32 KV (achieved_fp32_kv counts it); "
                                              "whole utterance wall (prefill + codec included)"}
@@ -648,6 +666,8 @@ def main():
                                else round(roof["rocprof_avg_us"], 2),
                                "avg_launch_bytes": int(roof["avg_bytes"]),
                                "launches_per_frame": roof["launches_per_frame"],
+                               "measured_stream": hbm,
+                               "frac_of_measured_read": round(roof["achieved_GBs"] / hbm["read_GBs"], 4) if hbm else None,
                                "profiles": roof["profile_src"]}
             out["frame_profile"] = {"kernel_ms_per_frame": round(roof["frame_kernel_ms"], 3),
                                     "share_ms": {k: round(v, 3) for k, v in roof["share_ms"].items()},

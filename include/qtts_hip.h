@@ -233,6 +233,12 @@ int qtts_hip_sync(void);
  * Returns the number of kernels (<0 on error).  Advances the state by one
  * frame, so call it after a generation, not in the middle of one. */
 int qtts_dev_profile_frame(qtts_dev_t *dev, int step, int max, int *kind, double *bytes, float *ms, char *names);
+/* Measurement: the current device's HBM stream bandwidth over two `bytes`-sized
+ * buffers (>> the 256 MB Infinity Cache): a non-temporal float4 read stream and
+ * a float4 copy (read + write bytes), `iters` timed launches each with HIP
+ * events on their own stream, GB/s (the roofline against a
+ * bandwidth measured on the box beside the 8 TB/s nominal). */
+int qtts_hip_hbm_bw(size_t bytes, int iters, double *read_gbs, double *copy_gbs);
 
 #ifdef __cplusplus
 }

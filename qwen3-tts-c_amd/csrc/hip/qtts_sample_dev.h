@@ -28,6 +28,7 @@
 // selected (value desc, index asc).  Full path: bitonic sort in LDS.
 #pragma once
 #include <float.h>
+#include <stddef.h>
 #include "qtts_common.h"
 #include "qtts_kernels.h"
 
@@ -598,15 +599,18 @@ struct FastSmemNT {
     float top_v[KFAST];
     int top_i[KFAST];
     int misc[4];
-    int dh[DBINS];                     // distance histogram (shared; 4 copies by wave measured slower, 5.21 vs 4.98 us)
+    alignas(16) int dh[DBINS];         // (read as int4) distance histogram (shared; 4 copies by wave measured slower, 5.21 vs 4.98 us)
     unsigned long long cand[KC];       // candidate keys (value key << 32 | ~index), slots by atomic
     int crank[KC];                     // candidate ranks, summed over the waves' slices
-    float pv[KC];
+    alignas(16) float pv[KC];          // (read as float4)
     int pi[KC];
     float red[NW];
     int redn[NW];
     int ncand;
 };
+// the int4 / float4 LDS reads of dh and pv (ds_read_b128) need 16-B offsets
+static_assert(offsetof(FastSmemNT<256>, dh) % 16 == 0 && offsetof(FastSmemNT<256>, pv) % 16 == 0, "FastSmemNT<256>");
+static_assert(offsetof(FastSmemNT<1024>, dh) % 16 == 0 && offsetof(FastSmemNT<1024>, pv) % 16 == 0, "FastSmemNT<1024>");
 
 // block-wide exclusive scans of two small per-thread counts (16 | 16 bits)
 template <int NT>

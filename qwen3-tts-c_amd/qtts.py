@@ -79,7 +79,7 @@ EXPORTS = [
     "qtts_dev_subtalker_host", "qtts_dev_codec_decode_host", "qtts_hip_matvec_bf16",
     "qtts_hip_rmsnorm_matvec_bf16", "qtts_hip_decode_matvec_bf16", "qtts_hip_resident_matvec_bf16", "qtts_hip_sample_top_k", "qtts_hip_causal_conv1d",
     "qtts_hip_transposed_conv1d", "qtts_hip_snake_beta", "qtts_hip_expf_glibc", "qtts_hip_sync",
-    "qtts_dev_profile_frame", "qtts_dev_codec_stream_begin", "qtts_dev_codec_stream_begin_ex",
+    "qtts_dev_profile_frame", "qtts_hip_hbm_bw", "qtts_dev_codec_stream_begin", "qtts_dev_codec_stream_begin_ex",
     "qtts_dev_codec_stream_prime", "qtts_dev_codec_stream_push_slot",
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
     "qtts_dev_codec_async_end", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",

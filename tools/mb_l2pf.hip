@@ -16,6 +16,12 @@
 //   pf 4   the same with one load per 128 B (one per L2 line)
 //   hot    every op reads the SAME weights (L2-resident upper bound)
 //
+// XCC check: a graph of k_op launches with a stamp kernel between them records
+// s_getreg(HW_REG_XCC_ID) per workgroup (the premise above: workgroup b on XCD
+// b % 8 in EVERY launch); printed as the share of (launch, workgroup) pairs
+// that match b % 8 and the number of workgroups whose XCD changed between
+// launches.
+//
 //   hipcc -O3 --offload-arch=gfx950 -Iqwen3-tts-c_amd/csrc/hip tools/mb_l2pf.hip -o tools/mb_l2pf && tools/mb_l2pf
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -111,6 +117,31 @@ __global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out, u
         if (acc == 0x9E3779B9u && threadIdx.x == 0) sink[0] = acc;
 }
 
+// XCD of every workgroup of this launch (a vector store from lane 0)
+__global__ __launch_bounds__(256) void k_xcc(unsigned *out) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    if (threadIdx.x == 0) out[blockIdx.x] = x;
+}
+// the same stamp taken inside a weight-streaming k_op-shaped launch
+template <int RW, int NV>
+__global__ __launch_bounds__(256) void k_op_xcc(Op o, const float *in, float *out, unsigned *xo) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int C = 512 * NV;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < RW; ++i)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            const v4u wv = reinterpret_cast<const v4u *>(o.W + (size_t)(blockIdx.x * 4 * RW + w + 4 * i) * C)[lane + 64 * k];
+            s += __uint_as_float(wv.x << 16) * in[lane];
+        }
+    if (threadIdx.x == 0) xo[blockIdx.x] = x;
+    if (s == 1.2345e-30f) out[threadIdx.x] = s;
+}
+
 #define DISPATCH(o, PF, ...)                                                                              \
     do {                                                                                                  \
         const int rw_ = (o).R / 256 / 4, nv_ = (o).C / 512;                                                \
@@ -177,6 +208,46 @@ int main() {
         CK(hipGraphDestroy(g));
         return ms * 1e3f / (reps * passes * ops.size());
     };
+    {   // XCC premise: 64 launches alternating the stamp kernel and a gate|up-shaped stamped k_op
+        const int NL = 64;
+        unsigned *xo;
+        CK(hipMalloc(&xo, (size_t)NL * 256 * 4));
+        CK(hipMemset(xo, 0xff, (size_t)NL * 256 * 4));
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        for (int l = 0; l < NL; ++l) {
+            if (l & 1) hipLaunchKernelGGL(k_xcc, dim3(256), dim3(256), 0, st, xo + (size_t)l * 256);
+            else hipLaunchKernelGGL((k_op_xcc<6, 2>), dim3(256), dim3(256), 0, st, ops[2 + 4 * ((l / 2) % L)], va, vb,
+                                    xo + (size_t)l * 256);
+        }
+        CK(hipStreamEndCapture(st, &g));
+        CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        CK(hipGraphLaunch(ge, st));
+        CK(hipStreamSynchronize(st));
+        std::vector<unsigned> h((size_t)NL * 256);
+        CK(hipMemcpy(h.data(), xo, h.size() * 4, hipMemcpyDeviceToHost));
+        int match = 0, changed = 0, bad = 0;
+        int hist[8][8] = {};
+        for (int l = 0; l < NL; ++l)
+            for (int b = 0; b < 256; ++b) {
+                const unsigned x = h[(size_t)l * 256 + b];
+                if (x > 7) { ++bad; continue; }
+                match += x == (unsigned)(b % 8);
+                if (l > 0 && h[(size_t)(l - 1) * 256 + b] != x) ++changed;
+                if (l == 0) hist[b % 8][x]++;
+            }
+        printf("xcc: %d launches x 256 workgroups: %d of %d (launch, workgroup) pairs on XCD b %% 8, "
+               "%d workgroup XCD changes between consecutive launches, %d unreadable\n",
+               NL, match, NL * 256 - bad, changed, bad);
+        printf("xcc: launch 0, workgroups b = 0..15 ->");
+        for (int b = 0; b < 16; ++b) printf(" %u", h[b]);
+        printf("\nxcc: launch 1, workgroups b = 0..15 ->");
+        for (int b = 0; b < 16; ++b) printf(" %u", h[256 + b]);
+        printf("\n");
+        CK(hipGraphExecDestroy(ge));
+        CK(hipGraphDestroy(g));
+    }
     for (int rep = 0; rep < 2; ++rep) {
         float t0 = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (auto &o : ops) { DISPATCH(o, 0, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
         float t1 = timed([&] { int i = 0; for (int p = 0; p < passes; ++p) for (auto &o : ops) { DISPATCH(o, 1, st, o, (i & 1) ? vb : va, (i & 1) ? va : vb, sink); ++i; } });
