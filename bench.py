@@ -262,7 +262,7 @@ def cpu_threads_default():
 
 
 def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128, speaker="aiden", timeout=900,
-                 greedy=False):
+                 greedy=False, wait_policy=None):
     """The reference c/ CLI (oracle/_ref/qwen-tts, built unmodified by
     oracle/Makefile) timed as BASELINE.md §2 plans: --benchmark-warmup /
     --benchmark-runs with the [persistent] lines parsed (c/main.c:262-271).
@@ -274,6 +274,8 @@ def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128
     if not os.path.exists(exe):
         return None
     env = dict(os.environ, OMP_NUM_THREADS=str(threads), **OMP_PLACEMENT)
+    if wait_policy:
+        env["OMP_WAIT_POLICY"] = wait_policy
     cmd = [exe, "-d", md, "-t", ",".join(map(str, ids)), "-s", speaker, "-l", "english", "-o", "/tmp/qtts_cpu.wav",
            "--fixed-codec-tokens", str(frames), "--benchmark-warmup", str(warmup), "--benchmark-runs", str(runs), "-v"]
     if greedy:
@@ -294,7 +296,7 @@ def cpu_baseline(md, ids, threads, frames=8, warmup=1, runs=2, target_frames=128
     ext_ms = fixed_ms + (med["talker_ms"] + med["codec_ms"]) / n * target_frames
     audio_s = target_frames * 0.08
     return dict(value=audio_s / (ext_ms / 1e3), unit="audio-s/s", cores=threads, kind="reference",
-                physical_cores=physical_cores(), placement=cpu_placement(),
+                physical_cores=physical_cores(), placement=dict(cpu_placement(), OMP_WAIT_POLICY=wait_policy),
                 runs=runs_,
                 sample=(f"reference c/ (oracle/_ref/qwen-tts: unmodified c/ sources, scalar GEMV + OpenMP, no BLAS in "
                         f"the image) on the same synthetic model and prompt{', greedy' if greedy else ''}, {threads} OpenMP "

@@ -170,6 +170,10 @@ struct qtts_dev {
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
     bool tab0b = true;       // QTTS_HIP_TAB0B=0: batch layer-0 q|k|v by GEMV instead of the table
+    // QTTS_HIP_ATTN_TAIL=0: batch sub-talker attention as its own launch
+    // (k_attn_short) instead of the q|k|v GEMV's tail (GemvArgs::tail)
+    bool attn_tail = true;
+    int *atick = nullptr;    // the tail's kv-head tickets [64] (zeroed)
     // QTTS_HIP_L2PF=<mask>: which edges of the batch-1 sub-talker chain carry
     // the next-launch weight prefetch (0 none): 1 q|k|v -> attention + O,
     // 2 attention + O -> gate|up, 4 gate|up -> down, 8 down -> next q|k|v or
@@ -422,6 +426,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_o = !(ao && !atoi(ao));
     const char *tb = getenv("QTTS_HIP_TAB0B");
     dv->tab0b = !(tb && !atoi(tb));
+    const char *atl = getenv("QTTS_HIP_ATTN_TAIL");
+    dv->attn_tail = !(atl && !atoi(atl));
     const char *pf = getenv("QTTS_HIP_L2PF");
     if (pf) dv->l2pf = atoi(pf);
     const char *pft = getenv("QTTS_HIP_L2PF_TK");
@@ -642,6 +648,8 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         A(pf_sink, unsigned, 1);
         A(btick, int, QTTS_GM_TICKS);
         CK(hipMemsetAsync(dv->btick, 0, QTTS_GM_TICKS * sizeof(int), dv->st));
+        A(atick, int, 64);
+        CK(hipMemsetAsync(dv->atick, 0, 64 * sizeof(int), dv->st));
         if (dv->gm_dbg_layer >= 0) {
             A(gm_dbg, unsigned long long, 4 * 2048 * 8);
             CK(hipMemsetAsync(dv->gm_dbg, 0, 4 * 2048 * 8 * 8, dv->st));
@@ -805,6 +813,21 @@ static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind
     CKI(pgemv(dv, a, kind));
     ProfScope ps(dv, PK_ATTN, 0);
     return qtts_attention(t, dv->st);
+}
+// batch (nb >= 2): the q|k|v GEMV with the short attention as its tail
+// (k_gemvb, GemvArgs::tail): one launch per layer fewer.  Falls back to the
+// two launches where the tail does not cover the shape (or QTTS_HIP_ATTN_TAIL=0).
+static int qkv_attn_tail(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
+    if (dv->attn_tail && a.nb >= 2 && t.KV <= 64) {
+        GemvArgs at = a;
+        at.tail = &t;
+        at.att_tick = dv->atick;
+        ProfScope ps(dv, kind, gemv_bytes(a));
+        const int rc = qtts_gemvb(at, dv->st);
+        if (rc != 1) return rc;
+        ps.cancel();
+    }
+    return qkv_attn(dv, a, t, kind);
 }
 static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float *y, int ldy, int nb, int epi) {
     GemvArgs a;
@@ -1081,8 +1104,8 @@ static int subtalker(qtts_dev *dv) {
             const bool kv_only = g == 0 && l == d.Ls - 1;
             GemvArgs a = gv(ly.wqkv, QKV, d.Hs, xa, d.Hs, dv->qkv_s, QKV, nb, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
-            // QTTS_HIP_GM_DBG at batch 1: stamps of pass 5, layer 2's q|k|v / gate|up / down
-            const bool sdbg = dv->gm_dbg && dv->gm_dbg_layer == 99 && nb == 1 && g == 5 && l == 2;
+            // QTTS_HIP_GM_DBG=99: stamps of pass 5, layer 2's q|k|v / (batch: O) / gate|up / down
+            const bool sdbg = dv->gm_dbg && dv->gm_dbg_layer == 99 && g == 5 && l == 2;
             if (sdbg) { a.dbg = dv->gm_dbg; DBG_XFIRST(a); }
             if (l == 0 && (!proj || ptab)) { set_src(a); a.xcopy = dv->x_st; a.ldxc = d.Hs; a.xcopy_normed = 0; }
             else if (pend) add_in(a, pend, npend, d.Hs, nb, xb);
@@ -1141,11 +1164,12 @@ static int subtalker(qtts_dev *dv) {
                     ProfScope pa(dv, PK_ATTN, 0);
                     CKI(qtts_attention(t, st));
                 } else {
-                    CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
+                    CKI(qkv_attn_tail(dv, a, t, PK_GEMV_SUB));
                 }
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 o.y = xa;
                 if (kzo) opend = split_out(dv, o, dv->bpo, kzo);
+                if (sdbg) o.dbg = dv->gm_dbg + 2048 * 8;
                 if (!kv_only) CKI(pgemv(dv, o, PK_GEMV_SUB));
             }
             if (kv_only) break;

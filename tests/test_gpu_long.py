@@ -19,6 +19,10 @@ Fixtures (tests/golden/make_golden_long.py, from the reference c/ build):
   sampling, 32 frames, each slot one reference run; decoded here as ONE
   lock-step batch on the batch GEMV (`k_gemvb`, RMS scale applied after the
   dot product, split-K O / down), codes compared slot by slot.
+* `long_17b_b8bench.npz` -- C4's bench workload itself: the 8 utterances of
+  `bench.py --batch 8` (p128 seeds 1234-1241, aiden), the whole 128 frames.
+* `long_eos17.npz` -- EOS mode on bench.py --eos's model: three utterances,
+  each one reference run to its EOS stop; the stop steps and codes.
 
 Bars: codes bit-exact (the first divergent frame / group is reported if not);
 waveform MSE < 1e-4 and max |d| < 1e-3 (north star); hidden / logits
@@ -155,15 +159,18 @@ def _b8_prompts(g):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"}, {"QTTS_HIP_TAB0B": "0"}])
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"}, {"QTTS_HIP_TAB0B": "0"},
+                                 {"QTTS_HIP_ATTN_TAIL": "0"}])
 def test_c4_batch8_lock_step_vs_reference(gpu, monkeypatch, env):
     """C4's per-GPU shape: the 8 reference utterances (32 frames, default
     sampling) decoded as ONE lock-step batch -- the batch GEMV with its RMS
     scale after the dot product, split-K O / down -- every slot's codes
     bit-exact against its own reference run, audio against the reference's
     samples.  Also on the staged-plane batch GEMV (GEMVB=0), with the
-    split-K producers reducing their own partials from 2 rows, and with layer
-    0's q|k|v by GEMV instead of the load-time table (TAB0B=0)."""
+    split-K producers reducing their own partials from 2 rows, with layer
+    0's q|k|v by GEMV instead of the load-time table (TAB0B=0), and with the
+    sub-talker attention as its own launch instead of the q|k|v GEMV's tail
+    (ATTN_TAIL=0)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = np.load(os.path.join(GOLDEN, "long_17b_b8.npz"))
@@ -204,23 +211,68 @@ def test_hd128_attention_switch_paths_vs_reference(gpu, monkeypatch, env, frames
         m.close()
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}])
+def test_c4_bench_workload_batch8_vs_reference(gpu, monkeypatch, env):
+    """C4's per-GPU bench workload itself (`bench.py --batch 8`, rank 0): p128
+    seeds 1234-1241, speaker aiden, seed 42, default sampling, the whole 128
+    frames -- decoded as ONE lock-step batch, every slot's 128 x 16 codes
+    bit-exact against its own reference run (long_17b_b8bench.npz), audio
+    against the reference's samples.  Also on the staged-plane batch GEMV."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = np.load(os.path.join(GOLDEN, "long_17b_b8bench.npz"))
+    man = _man()["b8bench"]
+    m = qtts.QwenTTS(model_dir("1.7b"))
+    try:
+        m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        rc, audio = m.generate_batch(_b8_prompts(g), man["speakers"], [man["language"]] * 8)
+        assert rc == 0
+        codes = m.last_codes_batch()
+        for b in range(8):
+            _codes_equal(codes[b], g["codes"][b], f"bench batch-8 slot {b} {env}")
+            _audio_close(audio[b][::man["audio_stride"]], g["audio_sub"][b], f"slot {b} every 16th sample")
+            _audio_close(audio[b][-1920:], g["audio_last"][b], f"slot {b} last frame")
+    finally:
+        m.close()
+
+
+def _eos_slot_check(codes, audio, g, man, b, what):
+    n = int(g["stop_step"][b])
+    _codes_equal(codes, g["codes"][b, :n], f"{what}: slot {b} codes up to the reference's stop")
+    assert audio is not None and len(audio) == n * 1920, (what, b, None if audio is None else len(audio), n)
+    _audio_close(audio[::man["audio_stride"]], g["audio_sub"][b, :len(audio[::man["audio_stride"]])],
+                 f"{what}: slot {b} every 16th sample")
+
+
 def test_eos_stop_17b_batch_1_and_3(gpu):
     """EOS mode (the reference's default: max_new_tokens 4096, stop at EOS,
     Q.c:1282-1330) on the synthetic 1.7B whose codec-head EOS row is scaled
-    x1.4 (bench.py --eos): the utterance stops well inside the capacity, alone
-    and in a lock-step batch of 3 where the other rows keep decoding after
-    one stops.  Regression: a stopped row's table id (the talker's EOS id, >=
-    the sub-talker vocabulary) indexed past the last pass's q|k|v / input
-    table."""
-    from synth_model import prompt_ids
-    m = qtts.QwenTTS(model_dir("1.7b", eos_gain=1.4))
+    x1.4 (bench.py --eos), against the reference's own EOS runs
+    (long_eos17.npz): each of the three utterances alone stops at the
+    reference's step with its codes bit-exact, and the same three as ONE
+    lock-step batch -- where the rows that stop first keep riding along while
+    the others decode -- give every slot the same stop step and codes.
+    Regression: a stopped row's table id (the talker's EOS id, >= the
+    sub-talker vocabulary) indexed past the last pass's q|k|v / input table."""
+    g = np.load(os.path.join(GOLDEN, "long_eos17.npz"))
+    man = _man()["eos17"]
+    m = qtts.QwenTTS(model_dir("1.7b", eos_gain=man["eos_gain"]))
     try:
-        m.set_params(max_tokens=4096, fixed=0, seed=42, **DEFAULT)
-        a = m.generate(prompt_ids("p128", seed=1234), "aiden", "english")
-        assert a is not None and len(a) > 0
-        assert m.c.last_stop_reason == 1 and 0 < m.c.last_stop_step < 4096
-        prompts = [prompt_ids("p128", seed=1234 + i) for i in range(3)]
-        rc, aud = m.generate_batch(prompts, ["aiden", "vivian", "serena"], ["english"] * 3)
-        assert rc == 0 and all(x is not None and len(x) > 0 for x in aud)
+        prompts = _b8_prompts(g)
+        stops = [int(x) for x in g["stop_step"]]
+        assert len(set(stops)) > 1, stops   # the batch run must have a row stopping before the others
+        for b, ids in enumerate(prompts):
+            m.set_params(max_tokens=4096, fixed=0, seed=man["seed"], **DEFAULT)
+            a = m.generate(ids, man["speakers"][b], man["language"])
+            assert m.c.last_stop_reason == 1, "no EOS stop"
+            assert m.c.last_stop_step == stops[b], (b, m.c.last_stop_step, stops[b])
+            _eos_slot_check(m.last_codes(), a, g, man, b, "batch 1")
+        m.set_params(max_tokens=4096, fixed=0, seed=man["seed"], **DEFAULT)
+        rc, aud = m.generate_batch(prompts, man["speakers"], [man["language"]] * len(prompts))
+        assert rc == 0
+        codes = m.last_codes_batch()
+        for b in range(len(prompts)):
+            _eos_slot_check(codes[b], aud[b], g, man, b, "lock-step batch of 3")
     finally:
         m.close()

@@ -21,4 +21,9 @@ for i in 1 2 3 4; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile --steps 10 --warmup 2 > $O/ab_on_$i.json 2> $O/ab_on_$i.err
   python -c "import json; f=lambda p: json.loads(open(p).read().strip().splitlines()[-1])['value']; print('pair $i off', f('$O/ab_off_$i.json'), 'on', f('$O/ab_on_$i.json'))"
 done
+# batch-8 sub-talker stamps (pass 5, layer 2) from the stamp build
+QTTS_LIB=$R/qwen3-tts-c_amd/lib_s/libqwen_tts_amd.so QTTS_HIP_GM_DBG=99 timeout -k 10 300 python bench.py --batch 8 --steps 1 --warmup 0 --no-profile --no-cpu-baseline > $O/st_b8.json 2> $O/st_b8.err
+grep gm_dbg $O/st_b8.err | tail -20
+QTTS_LIB=$R/qwen3-tts-c_amd/lib_s/libqwen_tts_amd.so QTTS_HIP_GM_DBG=99 timeout -k 10 300 python bench.py --batch 1 --steps 1 --warmup 0 --no-profile --no-cpu-baseline > $O/st_b1.json 2> $O/st_b1.err
+grep gm_dbg $O/st_b1.err | tail -20
 echo done

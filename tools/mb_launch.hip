@@ -39,7 +39,12 @@
 #include <algorithm>
 #include <vector>
 
-#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s failed: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+// every HIP call announces itself on stderr first (unbuffered): a fault inside
+// the runtime (the SIGSEGV under rocprofv3 --kernel-trace in round 4) then
+// names the call it happened in
+static int g_trace = 1;
+#define CK(x) do { if (g_trace) fprintf(stderr, "[mb_launch] %s:%d %s\n", __func__, __LINE__, #x); \
+                    hipError_t e = (x); if (e != hipSuccess) { printf("%s failed: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 constexpr int NL = 200, MAXG = 512;
@@ -163,6 +168,15 @@ __global__ __launch_bounds__(256) void k_gemv_gu(int i, const uint16_t *W, const
 }
 
 int main(int argc, char **argv) {
+    // --quiet: no per-call trace; --no-attr: no hipFuncSetAttribute (64 KB of
+    // dynamic LDS is within the default limit); --relaxed: capture in relaxed
+    // mode instead of global
+    bool no_attr = false, relaxed = false;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--quiet")) g_trace = 0;
+        if (!strcmp(argv[i], "--no-attr")) no_attr = true;
+        if (!strcmp(argv[i], "--relaxed")) relaxed = true;
+    }
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipEvent_t e0, e1;
@@ -177,13 +191,14 @@ int main(int argc, char **argv) {
     const size_t wn = (size_t)6144 * 1024;
     CK(hipMalloc(&W, wn * 2));
     CK(hipMemset(W, 0x3c, wn * 2));
-    CK(hipFuncSetAttribute((const void *)k_x4k_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+    if (!no_attr) CK(hipFuncSetAttribute((const void *)k_x4k_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     static unsigned long long hs[NL][MAXG][2];
 
     auto run = [&](const char *name, int grid, auto launch) {
         hipGraph_t g;
         hipGraphExec_t ge;
-        CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        if (g_trace) fprintf(stderr, "[mb_launch] variant %s grid %d\n", name, grid);
+        CK(hipStreamBeginCapture(st, relaxed ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal));
         for (int i = 0; i < NL; ++i) launch(i);
         CK(hipStreamEndCapture(st, &g));
         CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
