@@ -359,10 +359,13 @@ static bool gemvb_geom(const GemvArgs &a, GbGeom &g) {
                     ((uintptr_t)a.ypart & 3)))
         return false;
     if (a.tick && (!a.ypart || !a.y || a.epi != EPI_RESID)) return false;
-    // K slice per wave: the fewest steps that keep <= 16 waves
+    // K slice per wave: the fewest steps that keep <= wmax waves (16; the
+    // QTTS_HIP_GB_W=8 A/B switch: 512-thread workgroups, two per CU, one tile each)
+    const char *gbw = getenv("QTTS_HIP_GB_W");
+    const int wmax = gbw && atoi(gbw) == 8 ? 8 : 16;
     const int S = a.C / kz / 32;
     int SPW = 1;
-    while (SPW < 8 && (S / SPW > 16 || S % SPW)) SPW *= 2;
+    while (SPW < 8 && (S / SPW > wmax || S % SPW)) SPW *= 2;
     if (S % SPW || S / SPW > 16) return false;
     const int W = S / SPW;
     const int NBC = a.nb <= 8 ? 8 : 16;
@@ -370,7 +373,7 @@ static bool gemvb_geom(const GemvArgs &a, GbGeom &g) {
     // tiles per workgroup: about one round of workgroups over the 256 CUs,
     // within the register file (estimate below) and W >= TPW epilogue waves
     const int T = a.R / 16;
-    int TPW = (T * kz + 128) / 256;
+    int TPW = wmax == 8 && W <= 8 ? 1 : (T * kz + 128) / 256;
     TPW = std::max(1, std::min(TPW, 3));
     if (SPW == 8 && TPW > 2) TPW = 2;
     if (SPW <= 2 && TPW > 2) TPW = 2;
