@@ -436,10 +436,6 @@ static void wide_config(int R, int C, int epi, int &ks_out, int &nthr_out) {
 
 int qtts_gemv(const GemvArgs &in, hipStream_t st) {
     GemvArgs a = in;
-    if (a.tail) {   // only k_gemvb runs the attention tail (qtts_gemvb); never drop it silently
-        fprintf(stderr, "qtts_gemv: the attention tail (GemvArgs::tail) runs on qtts_gemvb only\n");
-        return -1;
-    }
     if (a.C % 64 || a.nb < 1 || a.nb > 16 || a.R < 1) {
         fprintf(stderr, "qtts_gemv: unsupported shape R=%d C=%d nb=%d\n", a.R, a.C, a.nb);
         return -1;

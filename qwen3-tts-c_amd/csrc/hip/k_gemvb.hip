@@ -37,7 +37,6 @@
 // exact (3 x bf16 planes, as k_gemvm / k_mgemm).
 #include <algorithm>
 
-#include "qtts_attn_dev.h"
 #include "qtts_gemvm_dev.h"
 
 namespace {
@@ -69,16 +68,9 @@ __device__ __forceinline__ void gb_stamp(const GemvArgs &a, int k) {
 
 // (src -- a.x, a.table or a.table_f32 by SRC --, ids, W and xadd lead the
 // arguments: preloaded into SGPRs, Makefile)
-// AHD > 0: the q|k|v GEMV with the sub-talker's short attention (head dim AHD,
-// <= 16 keys, GQA 2) as its tail (GemvArgs::tail): the rows are stored
-// write-through, each workgroup takes its kv head's ticket and the last of
-// that head's workgroups runs the attention of every batch row, one row per
-// 256-thread slice (attn_short_wg, the q|k|v read back with sc1 loads) -- the
-// separate attention launch of the batch path (k_attn_short) folded into the
-// end of the GEMV.
-template <int SPW, int TPW, int NBC, int PM, int SRC, int AHD = 0>
+template <int SPW, int TPW, int NBC, int PM, int SRC>
 __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids, const bf16_t *Wt, const float *xadd,
-                                                GemvArgs a, AttnArgs t) {
+                                                GemvArgs a) {
     gb_stamp(a, 0);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int SC = 32 * SPW;                 // columns of a wave's slice
@@ -243,8 +235,13 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
 #pragma unroll
         for (int q = 0; q < XQ; ++q) {
             if (!uok[q]) continue;
+            float sq[16];   // (all W slice sums in flight, then added in wave order)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) sq[k] = ssq[(k < W ? k : 0) * 16 + urow[q]];
             float s2 = 0.f;
-            for (int k = 0; k < W; ++k) s2 += ssq[k * 16 + urow[q]];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < W) s2 += sq[k];
             const float iv = rms_inv(s2, a.C, a.eps);
             float4 *xc = reinterpret_cast<float4 *>(a.xcopy + (size_t)urow[q] * a.ldxc + c0 + ucol);
             float4 v = *xc;
@@ -255,17 +252,39 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
     const bool tile_wave = w < TPW && r0 + 16 * w < a.R;
     floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
     if (tile_wave) {
-        v = reinterpret_cast<const floatx4 *>(smem)[w * 64 + lane];
-        for (int k = 1; k < W; ++k) v += reinterpret_cast<const floatx4 *>(smem + k * wreg)[w * 64 + lane];
-        if (norm) {   // batch rows 4 (lane >> 4) + i of the D fragment
+        // every wave's partial tile read at once (W <= 16; clamped, unconditional
+        // reads), then summed in wave order: the sums of a loop that waited for
+        // each read (that loop and the one below -- 16 and 64 dependent LDS
+        // round trips -- were 1.3-1.9 us of every normed batch launch's
+        // epilogue, profiles/r05a_b8_subtalker_stamps.txt)
+        floatx4 pt[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pt[k] = reinterpret_cast<const floatx4 *>(smem + (k < W ? k : 0) * wreg)[w * 64 + lane];
+        v = pt[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+            if (k < W) v += pt[k];
+        gb_stamp(a, 5);
+        if (norm) {
+            // lane l < 16 forms batch row l's statistic (the W slice sums in wave
+            // order) and its 1 / rms once; the D fragment's rows 4 (lane >> 4) + i
+            // fetch theirs by ds_bpermute
+            const int lb = lane & 15, lr = lb < nb ? lb : 0;
+            float sq[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) sq[k] = ssq[(k < W ? k : 0) * 16 + lr];
+            float s2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < W) s2 += sq[k];
+            const float iv = rms_inv(s2, a.C, a.eps);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int bb = 4 * (lane >> 4) + i;
-                float s2 = 0.f;
-                for (int k = 0; k < W; ++k) s2 += ssq[k * 16 + (bb < nb ? bb : 0)];
-                v[i] *= rms_inv(s2, a.C, a.eps);
+                v[i] *= __shfl(iv, bb < nb ? bb : 0, 64);
             }
         }
+        gb_stamp(a, 6);
     }
     const int r = r0 + 16 * w + (lane & 15);   // D: column = lane & 15 (weight row), row = 4 (lane >> 4) + i (batch row)
     if (a.tick) {      // self-reducing split-K producer (every thread reaches the ticket barrier)
@@ -277,43 +296,6 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
             }
         }
         reduce_last(a, 16 * TPW, reinterpret_cast<int *>(ssq));
-        return;
-    }
-    if constexpr (AHD > 0) {   // EPI_STORE (host): rows out write-through, then the kv head's ticket
-        if (tile_wave) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int bb = 4 * (lane >> 4) + i;
-                if (bb < nb && r < a.R) st_sc1(a.y + (size_t)bb * a.ldy + r, v[i]);
-            }
-        }
-        gb_stamp(a, 4);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int *flag = reinterpret_cast<int *>(ssq);   // (read above, before the barrier)
-        const int GPH = t.NH / t.KV, qrows = t.NH * AHD, krows = t.KV * AHD;
-        const int kvh = r0 < qrows ? (r0 / AHD) / GPH : r0 < qrows + krows ? (r0 - qrows) / AHD
-                                                                             : (r0 - qrows - krows) / AHD;
-        const int per = (GPH + 2) * AHD / (16 * TPW);   // workgroups per kv head (host: 16 TPW | AHD)
-        if (threadIdx.x == 0) {
-            const int old = __hip_atomic_fetch_add(a.att_tick + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag[0] = old == per - 1;
-        }
-        __syncthreads();
-        if (!flag[0]) return;
-        // the last of the head's workgroups: its attention for every batch row,
-        // one row per 256-thread slice (LDS reused: every partial tile was read
-        // before the barrier above)
-        const int slice = threadIdx.x >> 8, nsl = blockDim.x >> 8;
-        float *lq = smem + slice * (4 * AHD + 32), *sc = lq + 4 * AHD;
-        for (int rb = 0; rb < nb; rb += nsl) {
-            const int rr = rb + slice;
-            attn_short_wg<AHD, true>(t, kvh, rr < nb ? rr : nb - 1, lq, sc, nullptr, true, NoIssue(), t.qkv, nullptr,
-                                     (int)(threadIdx.x & 255), rr < nb);
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) __hip_atomic_store(a.att_tick + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gb_stamp(a, 5);
         return;
     }
     if (!tile_wave) return;
@@ -395,37 +377,18 @@ static bool gemvb_geom(const GemvArgs &a, GbGeom &g) {
     const dim3 grid((T + TPW - 1) / TPW, kz);
     if (a.tick && (int)grid.x > QTTS_GM_TICKS) return false;
     const int src = tab ? GB_SRC_TAB : tabf ? GB_SRC_TABF : xadd ? GB_SRC_XADD : GB_SRC_X;
-    if (a.tail) {   // the attention tail: q|k|v rows of whole heads per workgroup, 256-thread slices
-        const AttnArgs &t = *a.tail;
-        const size_t tsm = (size_t)(W / 4) * (4 * t.HD + 32) * sizeof(float);
-        if (t.HD != 128 || t.mode != 0 || t.win || t.KV < 1 || t.NH != 2 * t.KV || t.S > 16 || !a.att_tick ||
-            a.epi != EPI_STORE || a.ypart || a.tick || a.R != (t.NH + 2 * t.KV) * t.HD || t.HD % (16 * TPW) ||
-            W % 4 || t.qkv != a.y || t.ld_qkv != a.ldy || t.nrows != a.nb || tsm > smem || t.qkv_tab || TPW != 1 ||
-            tab || tabf)
-            return false;
-    }
     g.SPW = SPW; g.TPW = TPW; g.W = W; g.NBC = NBC; g.PM = PM; g.src = src; g.smem = smem; g.grid = grid;
     return true;
 }
 
-// (the attention tail is instantiated for the sub-talker's q|k|v shape only:
-// one 16-row tile per workgroup, x rows or x + split-K partials, HD 128)
 template <int SP, int TP, int NC, int PP, int SS>
 static void launch_gb(dim3 grid, dim3 block, size_t smem, hipStream_t st, const void *srcp, const int *idsp,
-                      const GemvArgs &a, const AttnArgs &tl) {
-    if constexpr (TP == 1 && (SS == GB_SRC_X || SS == GB_SRC_XADD)) {
-        if (a.tail) {
-            hipLaunchKernelGGL((k_gemvb<SP, TP, NC, PP, SS, 128>), grid, block, smem, st, srcp, idsp, a.W, a.xadd, a, tl);
-            static char nm[64];
-            snprintf(nm, sizeof nm, "k_gemvb<%d, %d, %d, %d, %d, 128>", SP, TP, NC, PP, SS);
-            qtts_last_kernel = nm;
-            return;
-        }
-    }
-    hipLaunchKernelGGL((k_gemvb<SP, TP, NC, PP, SS>), grid, block, smem, st, srcp, idsp, a.W, a.xadd, a, tl);
-    static char nm0[64];
-    snprintf(nm0, sizeof nm0, "k_gemvb<%d, %d, %d, %d, %d>", SP, TP, NC, PP, SS);
-    qtts_last_kernel = nm0;
+                      const GemvArgs &a) {
+    hipLaunchKernelGGL((k_gemvb<SP, TP, NC, PP, SS>), grid, block, smem, st, srcp, idsp, a.W, a.xadd, a);
+    // (rocprofv3's spelling of the instantiation: the bench looks its profile rows up by it)
+    static char nm[64];
+    snprintf(nm, sizeof nm, "k_gemvb<%d, %d, %d, %d, %d>", SP, TP, NC, PP, SS);
+    qtts_last_kernel = nm;
 }
 
 int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
@@ -443,8 +406,7 @@ int qtts_gemvb(const GemvArgs &in, hipStream_t st) {
     const void *srcp = tab ? (const void *)a.table : tabf ? (const void *)a.table_f32 : (const void *)a.x;
     const int *idsp = (tab || tabf) ? a.ids + a.ids_off : nullptr;
     const dim3 block(64 * W);
-    const AttnArgs tl = a.tail ? *a.tail : AttnArgs();
-#define QTTS_GB(SP, TP, NC, PP, SS) launch_gb<SP, TP, NC, PP, SS>(grid, block, smem, st, srcp, idsp, a, tl);
+#define QTTS_GB(SP, TP, NC, PP, SS) launch_gb<SP, TP, NC, PP, SS>(grid, block, smem, st, srcp, idsp, a);
 #define QTTS_GB_SRC(SP, TP, NC)                                                                        \
     if (src == GB_SRC_X) QTTS_GB(SP, TP, NC, 0, GB_SRC_X)                                              \
     else if (src == GB_SRC_TAB) QTTS_GB(SP, TP, NC, 0, GB_SRC_TAB)                                     \

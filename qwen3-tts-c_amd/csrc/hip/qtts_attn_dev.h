@@ -33,17 +33,13 @@ struct NoIssue { __device__ __forceinline__ void operator()() const {} };
 // rsrc: the q|k|v rows (a.qkv) or the table (a.qkv_tab); ids: a.tab_ids +
 // a.tab_off, or nullptr (no table) -- passed separately so a kernel can take
 // them as preloaded kernel arguments (k_attn_o)
-// tid_in >= 0: the thread's index within a 256-thread slice of a larger
-// workgroup (the batch q|k|v GEMV's attention tail runs one row per slice;
-// every slice calls this together, so the barriers inside stay uniform);
-// act = false: a slice past the last row (loads from a clamped row, no stores)
 template <int HD, bool SC1, class Issue = NoIssue>
 __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r, float *lq, float *scs,
                                               float *lout, bool wcache, Issue issue, const float *rsrc,
-                                              const int *ids, int tid_in = -1, bool act = true) {
+                                              const int *ids) {
     constexpr int D4 = HD / 4, LPK = HD / 16, NK = 16;
     float (*sc)[NK] = reinterpret_cast<float (*)[NK]>(scs);
-    const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x;
+    const int tid = threadIdx.x;
     const int KVD = a.KV * HD;
     const int p = a.pos ? a.pos[r] : a.pos_const, n = p + 1;
     const float *row = rsrc + (size_t)r * a.ld_qkv;
@@ -114,7 +110,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
             }
         }
         reinterpret_cast<float4 *>(lq)[tid] = y;
-        if (seg >= 2 && wcache && act && !(a.skip && a.skip[r])) {
+        if (seg >= 2 && wcache && !(a.skip && a.skip[r])) {
             float *dst = (seg == 2 ? a.kc : a.vc) + ((size_t)r * a.S + p) * KVD + kvh * HD;
             reinterpret_cast<float4 *>(dst)[l] = y;
         }
@@ -152,7 +148,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
     __syncthreads();
 
     // ---- P.V, keys in order (T.c:667-671)
-    if (go < 2 && act) {
+    if (go < 2) {
         float acc = 0.f;
 #pragma unroll
         for (int t = 0; t < NK; ++t)

@@ -23,10 +23,12 @@ struct L2Prefetch {
     int pm = 1 << 30;
     long long pa = 0, pb = 0;
     int chunks = 0, lg = 30, ld = 0;
+    // slices of the target: a workgroup b >= nwg of a launch wider than the
+    // next one's grid has no slice of its own and re-reads its fallback line
+    // (the start formula would otherwise run past the target's end)
+    int nwg = 0;
     unsigned *sink = nullptr;              // never written (the loads' values are folded into a test)
 };
-
-struct AttnArgs;
 
 struct GemvArgs {
     const bf16_t *W = nullptr;  // [R, C] bf16 row-major
@@ -85,14 +87,6 @@ struct GemvArgs {
     int dbg_xfirst = 0;                  // (stamp builds) k_gemvw waits for x before issuing its weights
 #endif
     L2Prefetch pf;                      // batch-1 lean kernel (k_gemvw): the next launch's weights
-    // batch q|k|v GEMV (k_gemvb, EPI_STORE) with the sub-talker's short
-    // attention as its tail: the q|k|v rows go out write-through, every
-    // workgroup takes a ticket of the kv head its rows belong to, and the last
-    // of a kv head's workgroups runs that head's attention for every batch row
-    // (host-side pointer: qtts_gemvb passes *tail by value; att_tick [KV]
-    // zeroed, reset by the last arriver).  nullptr: no tail.
-    const AttnArgs *tail = nullptr;
-    int *att_tick = nullptr;
     // the batch-1 fast path needs 16-B aligned fp32 rows (or a bf16 table)
     bool ldx_ok1() const {
         if (xadd && (((uintptr_t)xadd & 15) || ld_xadd % 4 || n_xadd < 1)) return false;

@@ -17,8 +17,9 @@ struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
 // CS: log2 of the bytes one load stands for (64; 128 = one load per L2 line)
 template <int NT, bool NTL = false, int CS = 6>
 __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
-    const unsigned char *st = p.base ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
-                                     : reinterpret_cast<const unsigned char *>(fallback);
+    // (b is uniform: a scalar select, no branch between loads)
+    const unsigned char *st = p.base && b < p.nwg ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
+                                                  : reinterpret_cast<const unsigned char *>(fallback);
     const unsigned m = (1u << p.lg) - 1u, n = (unsigned)p.chunks;
     // offsets first (selects, no exec-masked branches: those made the compiler
     // reuse an in-flight load's registers and wait for every load), then the loads

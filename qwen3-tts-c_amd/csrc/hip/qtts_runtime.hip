@@ -170,10 +170,6 @@ struct qtts_dev {
     bool profiling = false;
     bool attn_o = true;      // QTTS_HIP_ATTN_O=0: sub-talker attention and O projection as two kernels
     bool tab0b = true;       // QTTS_HIP_TAB0B=0: batch layer-0 q|k|v by GEMV instead of the table
-    // QTTS_HIP_ATTN_TAIL=0: batch sub-talker attention as its own launch
-    // (k_attn_short) instead of the q|k|v GEMV's tail (GemvArgs::tail)
-    bool attn_tail = true;
-    int *atick = nullptr;    // the tail's kv-head tickets [64] (zeroed)
     // QTTS_HIP_L2PF=<mask>: which edges of the batch-1 sub-talker chain carry
     // the next-launch weight prefetch (0 none): 1 q|k|v -> attention + O,
     // 2 attention + O -> gate|up, 4 gate|up -> down, 8 down -> next q|k|v or
@@ -426,8 +422,6 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_o = !(ao && !atoi(ao));
     const char *tb = getenv("QTTS_HIP_TAB0B");
     dv->tab0b = !(tb && !atoi(tb));
-    const char *atl = getenv("QTTS_HIP_ATTN_TAIL");
-    dv->attn_tail = !(atl && !atoi(atl));
     const char *pf = getenv("QTTS_HIP_L2PF");
     if (pf) dv->l2pf = atoi(pf);
     const char *pft = getenv("QTTS_HIP_L2PF_TK");
@@ -648,8 +642,6 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         A(pf_sink, unsigned, 1);
         A(btick, int, QTTS_GM_TICKS);
         CK(hipMemsetAsync(dv->btick, 0, QTTS_GM_TICKS * sizeof(int), dv->st));
-        A(atick, int, 64);
-        CK(hipMemsetAsync(dv->atick, 0, 64 * sizeof(int), dv->st));
         if (dv->gm_dbg_layer >= 0) {
             A(gm_dbg, unsigned long long, 4 * 2048 * 8);
             CK(hipMemsetAsync(dv->gm_dbg, 0, 4 * 2048 * 8 * 8, dv->st));
@@ -814,21 +806,6 @@ static int qkv_attn(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind
     ProfScope ps(dv, PK_ATTN, 0);
     return qtts_attention(t, dv->st);
 }
-// batch (nb >= 2): the q|k|v GEMV with the short attention as its tail
-// (k_gemvb, GemvArgs::tail): one launch per layer fewer.  Falls back to the
-// two launches where the tail does not cover the shape (or QTTS_HIP_ATTN_TAIL=0).
-static int qkv_attn_tail(qtts_dev *dv, const GemvArgs &a, const AttnArgs &t, int kind) {
-    if (dv->attn_tail && a.nb >= 2 && t.KV <= 64) {
-        GemvArgs at = a;
-        at.tail = &t;
-        at.att_tick = dv->atick;
-        ProfScope ps(dv, kind, gemv_bytes(a));
-        const int rc = qtts_gemvb(at, dv->st);
-        if (rc != 1) return rc;
-        ps.cancel();
-    }
-    return qkv_attn(dv, a, t, kind);
-}
 static GemvArgs gv(const bf16_t *W, int R, int C, const float *x, int ldx, float *y, int ldy, int nb, int epi) {
     GemvArgs a;
     a.W = W; a.R = R; a.C = C; a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy; a.nb = nb; a.epi = epi;
@@ -928,6 +905,7 @@ static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C, in
     if (bytes % 64) return p;
     p.base = reinterpret_cast<const unsigned char *>(W);
     p.pa = (long long)(R / grid) * C * 2; p.pb = 0; p.chunks = (int)(bytes / 64); p.lg = 30; p.ld = 0;
+    p.nwg = grid;
     p.sink = dv->pf_sink;
     return p;
 }
@@ -946,6 +924,7 @@ static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH,
     p.base = reinterpret_cast<const unsigned char *>(Wo);
     p.pm = R / RPW; p.pa = (long long)RPW * NH * HD * 2; p.pb = W2 * 2;
     p.chunks = RPW * cpr; p.lg = __builtin_ctz(cpr); p.ld = NH * HD * 2; p.sink = dv->pf_sink;
+    p.nwg = (R / RPW) * (NH / 2);   // (R / RPW) row blocks x the kv heads of a GQA-2 W_o
     return p;
 }
 
@@ -1164,7 +1143,7 @@ static int subtalker(qtts_dev *dv) {
                     ProfScope pa(dv, PK_ATTN, 0);
                     CKI(qtts_attention(t, st));
                 } else {
-                    CKI(qkv_attn_tail(dv, a, t, PK_GEMV_SUB));
+                    CKI(qkv_attn(dv, a, t, PK_GEMV_SUB));
                 }
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb
                 o.y = xa;
@@ -1481,6 +1460,9 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
         std::vector<unsigned long long> h(4 * 2048 * 8);
         CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
         static const char *op[4] = {"q|k|v", "O / -", "gate|up", "down"};
+        // (k_gemvw: 3 epilogue, 4 after the prefetch sink, 5 weights issued,
+        // 6 merged; k_gemvb: 2 = MFMAs done, 3 = after the final barrier,
+        // 4 = after the epilogue stores, 5 = tiles summed, 6 = normalised)
         static const char *ph[7] = {"start", "x staged", "dot done", "epilogue", "pf landed", "w issued", "merged"};
         for (int g = 0; g < 4; ++g) {
             const unsigned long long *b = h.data() + (size_t)g * 2048 * 8;

@@ -336,3 +336,16 @@ def test_expf_glibc_matches_libm(gpu):
     ref = np.array([libm.expf(float(v)) for v in x], np.float32)
     bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))[0]
     assert len(bad) == 0, (len(bad), x[bad[:5]], got[bad[:5]], ref[bad[:5]])
+
+
+def test_hbm_stream_bandwidth_entry(gpu):
+    """qtts_hip_hbm_bw (the bench line's measured stream bandwidth): both
+    figures positive and below the 8 TB/s nominal peak; sizes it refuses."""
+    lib = qtts.lib()
+    lib.qtts_hip_hbm_bw.restype = C.c_int
+    lib.qtts_hip_hbm_bw.argtypes = [C.c_size_t, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    rd, cp = C.c_double(0), C.c_double(0)
+    assert lib.qtts_hip_hbm_bw(1 << 30, 3, C.byref(rd), C.byref(cp)) == 0
+    assert 500.0 < rd.value < 8000.0 and 500.0 < cp.value < 8000.0, (rd.value, cp.value)
+    assert lib.qtts_hip_hbm_bw(1024, 3, C.byref(rd), C.byref(cp)) == -1
+    assert lib.qtts_hip_hbm_bw(512 << 20, 0, C.byref(rd), C.byref(cp)) == -1

@@ -159,18 +159,15 @@ def _b8_prompts(g):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"}, {"QTTS_HIP_TAB0B": "0"},
-                                 {"QTTS_HIP_ATTN_TAIL": "0"}])
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BSELF_MIN": "2"}, {"QTTS_HIP_TAB0B": "0"}])
 def test_c4_batch8_lock_step_vs_reference(gpu, monkeypatch, env):
     """C4's per-GPU shape: the 8 reference utterances (32 frames, default
     sampling) decoded as ONE lock-step batch -- the batch GEMV with its RMS
     scale after the dot product, split-K O / down -- every slot's codes
     bit-exact against its own reference run, audio against the reference's
     samples.  Also on the staged-plane batch GEMV (GEMVB=0), with the
-    split-K producers reducing their own partials from 2 rows, with layer
-    0's q|k|v by GEMV instead of the load-time table (TAB0B=0), and with the
-    sub-talker attention as its own launch instead of the q|k|v GEMV's tail
-    (ATTN_TAIL=0)."""
+    split-K producers reducing their own partials from 2 rows, and with layer
+    0's q|k|v by GEMV instead of the load-time table (TAB0B=0)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = np.load(os.path.join(GOLDEN, "long_17b_b8.npz"))

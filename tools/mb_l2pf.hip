@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out, u
         constexpr int CS = PF == 4 ? 7 : 6;
         L2Prefetch p;
         p.base = reinterpret_cast<const unsigned char *>(o.nW); p.pa = (long long)nbytes; p.pb = 0;
-        p.chunks = (int)(nbytes >> CS); p.lg = 30; p.ld = 0; p.sink = sink;
+        p.chunks = (int)(nbytes >> CS); p.lg = 30; p.ld = 0; p.sink = sink; p.nwg = gridDim.x;
         L2PfRegs r;
         qtts_l2pf_issue<256, false, CS>(p, blockIdx.x, r, o.W);
 #pragma unroll
