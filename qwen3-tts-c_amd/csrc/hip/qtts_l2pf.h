@@ -14,8 +14,11 @@ struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
 // displace the sub-talker's weights from the Infinity Cache)
 // Single target (workgroup b's slice of the next launch; the batch-1
 // kernels): the slice base is uniform, one scalar division per launch.
-// CS: log2 of the bytes one load stands for (64; 128 = one load per L2 line)
-template <int NT, bool NTL = false, int CS = 6>
+// (L2Prefetch::cs: log2 of the bytes one load stands for -- 6: every 64-B
+// chunk of the slice; 12: one load per 4 KB page, which is what the gain
+// comes from: round-5 counters show the consumer's L2 hits unchanged and its
+// UTCL1 translation misses cut 6-160x, profiles/r05c_l2pf_counters.txt)
+template <int NT, bool NTL = false>
 __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
     // (b is uniform: a scalar select, no branch between loads)
     const unsigned char *st = p.base && b < p.nwg ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
@@ -28,7 +31,7 @@ __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2Pf
     for (int j = 0; j < QTTS_PF_LOADS; ++j) {
         const unsigned c0 = threadIdx.x + NT * j;
         const unsigned c = c0 < n ? c0 : 0u;
-        off[j] = (c >> p.lg) * (unsigned)p.ld + ((c & m) << CS);
+        off[j] = (c >> p.lg) * (unsigned)p.ld + ((c & m) << p.cs);
     }
 #pragma unroll
     for (int j = 0; j < QTTS_PF_LOADS; ++j) {

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256) void k_op(Op o, const float *in, float *out, u
         p.base = reinterpret_cast<const unsigned char *>(o.nW); p.pa = (long long)nbytes; p.pb = 0;
         p.chunks = (int)(nbytes >> CS); p.lg = 30; p.ld = 0; p.sink = sink; p.nwg = gridDim.x;
         L2PfRegs r;
-        qtts_l2pf_issue<256, false, CS>(p, blockIdx.x, r, o.W);
+        p.cs = CS;
+        qtts_l2pf_issue<256, false>(p, blockIdx.x, r, o.W);
 #pragma unroll
         for (int j = 0; j < QTTS_PF_LOADS; ++j) acc ^= r.v[j];
     } else if constexpr (PF == 2) {
