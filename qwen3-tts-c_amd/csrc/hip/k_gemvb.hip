@@ -83,11 +83,10 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
     // allow measured slower at batch 8 (139.8 / 140.2 vs 142.3 / 142.0
     // audio-s/s, same box) although the stamps show q|k|v's last wave
     // finishing 3.5 us after its first (profiles/r03i_batch8_gemvb_stamps.txt)
-#ifdef QTTS_GB_ALLW
-    constexpr int SA = SPW <= 2 ? SPW : (SPW + 1) / 2;   // (A/B build: every step of SPW <= 2 before the staging)
-#else
-    constexpr int SA = (SPW + 1) / 2;
-#endif
+    // (SPW <= 2, the sub-talker's shapes: every step before the staging --
+    // batch 8 152.5 / 153.2 / 152.6 vs 151.1 / 151.0 / 150.8 audio-s/s with
+    // only the first, alternating processes, profiles/r05e_ab_prefetch_modes.txt)
+    constexpr int SA = SPW <= 2 ? SPW : (SPW + 1) / 2;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
     const int nb = a.nb;
     const int kz = gridDim.y, Ck = a.C / kz, woff = blockIdx.y * Ck;

@@ -23,7 +23,7 @@ struct L2Prefetch {
     int pm = 1 << 30;
     long long pa = 0, pb = 0;
     int chunks = 0, lg = 30, ld = 0;
-    int cs = 6;                            // log2 bytes per chunk (6: 64-B chunks; 12: one load per 4 KB page)
+    int cs = 6;                            // log2 bytes per chunk (64 B; the micro-benchmark also runs 128)
     // slices of the target: a workgroup b >= nwg of a launch wider than the
     // next one's grid has no slice of its own and re-reads its fallback line
     // (the start formula would otherwise run past the target's end)

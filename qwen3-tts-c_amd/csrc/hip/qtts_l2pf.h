@@ -14,10 +14,12 @@ struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
 // displace the sub-talker's weights from the Infinity Cache)
 // Single target (workgroup b's slice of the next launch; the batch-1
 // kernels): the slice base is uniform, one scalar division per launch.
-// (L2Prefetch::cs: log2 of the bytes one load stands for -- 6: every 64-B
-// chunk of the slice; 12: one load per 4 KB page, which is what the gain
-// comes from: round-5 counters show the consumer's L2 hits unchanged and its
-// UTCL1 translation misses cut 6-160x, profiles/r05c_l2pf_counters.txt)
+// (L2Prefetch::cs: log2 of the bytes one load stands for.  What the next
+// launch gains is NOT L2 hits -- round-5 counters show its TCC_HIT unchanged
+// and its UTCL1 translation misses cut 6-160x -- but touching only one line
+// per page (or per 2 MB of the whole next matrix) measured slower than this
+// full 64-B touch, profiles/r05e_ab_prefetch_modes.txt: the data movement
+// itself is part of the gain)
 template <int NT, bool NTL = false>
 __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
     // (b is uniform: a scalar select, no branch between loads)

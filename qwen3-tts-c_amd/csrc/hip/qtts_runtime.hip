@@ -177,9 +177,7 @@ struct qtts_dev {
     // (the same for the batch chain on k_gemvb measured 2 % slower at batch 8
     // and 16, profiles/r04g_ab_l2pf_batch.txt, and was removed)
     int l2pf = 31;
-    bool pf_page = false;    // QTTS_HIP_PF_PAGE=1: the prefetch touches one line per 4 KB page (pf_gemvw)
-    int l2pf_tk = 0;         // QTTS_HIP_L2PF_TK bits (batch-1 talker, non-temporal): 1 q|k|v -> O's W_o, 2 O -> gate|up,
-                             // 4 gate|up -> down, 8 down -> next q|k|v / codec head
+    int l2pf_tk = 0;         // QTTS_HIP_L2PF_TK bits (batch-1 talker, non-temporal): 1 q|k|v -> O's W_o, 2 O -> gate|up
     unsigned *pf_sink = nullptr;
     bool attn_defer = true;  // QTTS_HIP_ATTN_DEFER=0: batch-1 talker attention merges its own splits
     int attn_lpk = 0;        // QTTS_HIP_ATTN_LPK=4|8|16 (HD 128 split size), latched here: sizes att_part
@@ -426,8 +424,6 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->tab0b = !(tb && !atoi(tb));
     const char *pf = getenv("QTTS_HIP_L2PF");
     if (pf) dv->l2pf = atoi(pf);
-    const char *pp = getenv("QTTS_HIP_PF_PAGE");
-    if (pp) dv->pf_page = atoi(pp) != 0;
     const char *pft = getenv("QTTS_HIP_L2PF_TK");
     if (pft) dv->l2pf_tk = atoi(pft);
     const char *gd = getenv("QTTS_HIP_GM_DBG");
@@ -901,22 +897,9 @@ static void add_in(GemvArgs &g, const float *part, int n, int R, int nrun, float
 //   (a next launch of `grid` workgroups, 256 or 512: this launch's workgroup b
 //   < 256 takes the first cap bytes of the next one's workgroup b -- b and
 //   b + 256 share an XCD, so a 512 grid is half covered)
-// Page mode (qtts_dev::pf_page, QTTS_HIP_PF_PAGE): one load per 4 KB page of
-// the slice instead of one per 64-B chunk -- the translations are what the
-// next launch gains (UTCL1 misses), at 1/64 of the prefetch's fabric traffic.
 static L2Prefetch pf_gemvw(const qtts_dev *dv, const bf16_t *W, int R, int C, int grid = 256, bool on = true) {
     L2Prefetch p;
     if (!on || R % grid) return p;
-    if (dv->pf_page) {
-        const long long sb = (long long)(R / grid) * C * 2;
-        const long long pages = sb >> 12;
-        if (pages < 1 || pages > 256LL * QTTS_PF_LOADS) return p;
-        p.base = reinterpret_cast<const unsigned char *>(W);
-        p.pa = sb; p.pb = 0; p.chunks = (int)pages; p.lg = 30; p.ld = 0; p.cs = 12;
-        p.nwg = grid;
-        p.sink = dv->pf_sink;
-        return p;
-    }
     long long bytes = (long long)(R / grid) * C * 2;
     if (bytes > 64LL * 256 * QTTS_PF_LOADS) bytes = 64LL * 256 * QTTS_PF_LOADS;
     if (bytes % 64) return p;
@@ -941,7 +924,6 @@ static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH,
     p.base = reinterpret_cast<const unsigned char *>(Wo);
     p.pm = R / RPW; p.pa = (long long)RPW * NH * HD * 2; p.pb = W2 * 2;
     p.chunks = RPW * cpr; p.lg = __builtin_ctz(cpr); p.ld = NH * HD * 2; p.sink = dv->pf_sink;
-    if (dv->pf_page && NH * HD * 2 >= 4096) { p.chunks = RPW; p.lg = 0; }   // one load per row (a row is >= one page)
     p.nwg = (R / RPW) * (NH / 2);   // (R / RPW) row blocks x the kv heads of a GQA-2 W_o
     return p;
 }
@@ -997,14 +979,10 @@ static int talker_layers(qtts_dev *dv) {
         a.norm_w = ly.post; a.eps = d.eps;
         if (dbg) a.dbg = dv->gm_dbg + 2 * 2048 * 8;
         if (opend) add_in(a, dv->bpo, kzo, d.H, nb, xb);
-        if (nb == 1 && (dv->l2pf_tk & 4)) a.pf = pf_gemvw(dv, ly.wdown, d.H, d.I);
         CKI(pgemv(dv, a, PK_GEMV_TALKER));
         if (opend) std::swap(xa, xb);
         GemvArgs dn = gv(ly.wdown, d.H, d.I, dv->hbuf, d.I, xa, d.H, nb, EPI_RESID);
         if (dbg) dn.dbg = dv->gm_dbg + 3 * 2048 * 8;
-        // (down -> the next layer's q|k|v, or the codec head after the last layer)
-        if (nb == 1 && (dv->l2pf_tk & 8))
-            dn.pf = l + 1 < d.L ? pf_gemvw(dv, dv->tl[l + 1].wqkv, QKV, d.H) : pf_gemvw(dv, dv->head, d.V, d.H);
         if (kzd && split_out(dv, dn, dv->bpd, kzd, tk_self)) { pend = dv->bpd; npend = kzd; }
         CKI(pgemv(dv, dn, PK_GEMV_TALKER));
     }
