@@ -575,9 +575,11 @@ def main():
             for _ in range(2):
                 m.generate_voice_clone_audio_stream(prompts[0], wavs[0], vc[0][0], "english", chunk_frames=8)
             fp["first_packet_from_audio_ms"] = m.c.perf_first_packet_ms
-    # (the 0.6B line reads the 0.6B profile passes: <tag>_06b_kernel_stats.csv / _pmc.json)
-    roof = None if args.no_profile or vc is not None else profile_roofline(
-        m, qtts.lib(), "" if args.preset == "1.7b" else args.preset.replace(".", "") + "_")
+    # (the 0.6B line reads the 0.6B profile passes: <tag>_06b_kernel_stats.csv / _pmc.json;
+    # a batch-B line its own: <tag>_b8_kernel_stats.csv / _b8_pmc.json)
+    pvar = ("" if args.preset == "1.7b" else args.preset.replace(".", "") + "_") + \
+        (f"b{args.batch}_" if args.batch > 1 else "")
+    roof = None if args.no_profile or vc is not None else profile_roofline(m, qtts.lib(), pvar)
     hbm = None if args.no_profile else hbm_stream_bw(qtts.lib())
     m.close()
 

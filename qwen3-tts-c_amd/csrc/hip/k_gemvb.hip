@@ -86,7 +86,11 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
     // (SPW <= 2, the sub-talker's shapes: every step before the staging --
     // batch 8 152.5 / 153.2 / 152.6 vs 151.1 / 151.0 / 150.8 audio-s/s with
     // only the first, alternating processes, profiles/r05e_ab_prefetch_modes.txt)
+#ifdef QTTS_GB_ALLW4
+    constexpr int SA = SPW <= 2 || PM == 0 ? SPW : (SPW + 1) / 2;   // (A/B build: also every step of the partial-free shapes)
+#else
     constexpr int SA = SPW <= 2 ? SPW : (SPW + 1) / 2;
+#endif
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
     const int nb = a.nb;
     const int kz = gridDim.y, Ck = a.C / kz, woff = blockIdx.y * Ck;

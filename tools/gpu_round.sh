@@ -9,7 +9,7 @@
 #   extra = C5 voice clone batch 8, batch 8 / 16 lines, encoders, MFMA pass
 set -eo pipefail
 TAG=${1:-r02}
-MODE=${2:-all}   # all | core | prof (no tests) | extra | dist (2-rank gloo rehearsal)
+MODE=${2:-all}   # all | core | prof (no tests) | extra | batch | dist (2-rank gloo rehearsal)
 R=$GRAFT_REPO_ROOT
 [ -z "$R" ] && R=$(pwd)
 O=$R/gpurun_out/$TAG
@@ -23,6 +23,27 @@ trap trim EXIT
 if [ "$MODE" = dist ]; then
   QTTS_BENCH_BACKEND=gloo timeout -k 10 900 python bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline \
     --no-profile > $O/dist2.json 2> $O/dist2.err
+  echo done; exit 0
+fi
+if [ "$MODE" = batch ]; then
+  # the batch-8 line of record (C4's per-GPU shape) with its own rocprof stats
+  # and FETCH / WRITE passes (<tag>_b8_kernel_stats.csv / _b8_pmc.json, read
+  # by bench.py --batch 8), then the batch-16 line
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/b8/prof -o run -- python3 $R/bench.py --batch 8 --steps 2 --warmup 1 --no-cpu-baseline --no-profile > $O/prof_b8.json 2> $O/prof_b8.err
+  f=$(find $O/b8/prof -name "*kernel_trace.csv"); python3 $R/tools/trace_by_grid.py $f > $O/b8_by_grid.txt 2>&1 || true
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/b8/pmc_fetch -o run -- python3 $R/bench.py --batch 8 --no-cpu-baseline --no-profile --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch_b8.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $O/b8/pmc_write -o run -- python3 $R/bench.py --batch 8 --no-cpu-baseline --no-profile --steps 1 --warmup 0 --frames 8 > $O/pmc_write_b8.log 2>&1
+  python3 $R/tools/prof_summary.py $O/b8
+  cp $O/b8/kernel_stats.csv $R/profiles/${TAG}_b8_kernel_stats.csv
+  cp $O/b8/pmc.json $R/profiles/${TAG}_b8_pmc.json
+  cp $O/b8_by_grid.txt $R/profiles/${TAG}_b8_by_grid.txt
+  echo $TAG > $R/profiles/LATEST
+  cd $R
+  timeout -k 10 600 python bench.py --batch 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_b8.json 2> $O/bench_b8.err
+  cp $O/bench_b8.json $R/profiles/${TAG}_bench_batch8.json
+  timeout -k 10 600 python bench.py --batch 16 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_b16.json 2> $O/bench_b16.err
+  cp $O/bench_b16.json $R/profiles/${TAG}_bench_batch16.json
   echo done; exit 0
 fi
 if [ "$MODE" = extra ]; then

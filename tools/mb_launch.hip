@@ -171,11 +171,21 @@ int main(int argc, char **argv) {
     // --quiet: no per-call trace; --no-attr: no hipFuncSetAttribute (64 KB of
     // dynamic LDS is within the default limit); --relaxed: capture in relaxed
     // mode instead of global
-    bool no_attr = false, relaxed = false;
+    // --skip-big: leave out x4k_big (a 256-B by-value kernel argument): under
+    // rocprofv3 --kernel-trace the 8th hipGraphLaunch of that variant's graph
+    // faults inside the runtime (host SIGSEGV, round 5: profiles/r05d_mb_launch_fault.txt)
+    // --reps N: timed replays per variant (default 20); --only a,b: just these
+    // variants (fewer dispatch records under the profiler)
+    bool no_attr = false, relaxed = false, skip_big = false;
+    int reps_arg = 20;
+    const char *only = nullptr;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--quiet")) g_trace = 0;
         if (!strcmp(argv[i], "--no-attr")) no_attr = true;
         if (!strcmp(argv[i], "--relaxed")) relaxed = true;
+        if (!strcmp(argv[i], "--skip-big")) skip_big = true;
+        if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps_arg = atoi(argv[++i]);
+        if (!strcmp(argv[i], "--only") && i + 1 < argc) only = argv[++i];
     }
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -195,6 +205,18 @@ int main(int argc, char **argv) {
     static unsigned long long hs[NL][MAXG][2];
 
     auto run = [&](const char *name, int grid, auto launch) {
+        if (only) {   // comma-separated exact names
+            bool hit = false;
+            const size_t n = strlen(name);
+            for (const char *p = only; *p;) {
+                const char *q = strchr(p, ',');
+                const size_t m = q ? (size_t)(q - p) : strlen(p);
+                if (m == n && !strncmp(p, name, n)) hit = true;
+                if (!q) break;
+                p = q + 1;
+            }
+            if (!hit) return;
+        }
         hipGraph_t g;
         hipGraphExec_t ge;
         if (g_trace) fprintf(stderr, "[mb_launch] variant %s grid %d\n", name, grid);
@@ -204,7 +226,7 @@ int main(int argc, char **argv) {
         CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
         for (int r = 0; r < 3; ++r) CK(hipGraphLaunch(ge, st));
         CK(hipStreamSynchronize(st));
-        const int reps = 20;
+        const int reps = reps_arg;
         CK(hipEventRecord(e0, st));
         for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, st));
         CK(hipEventRecord(e1, st));
@@ -248,8 +270,9 @@ int main(int argc, char **argv) {
         run("stamp", grid, [&](int i) { hipLaunchKernelGGL(k_stamp, dim3(grid), dim3(256), 0, st, i); });
         run("x4k", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
             hipLaunchKernelGGL(k_x4k, dim3(grid), dim3(256), 0, st, i, in, out); });
-        run("x4k_big", grid, [&](int i) { Big b{}; b.i = i; pp(i, b.in, b.out);
-            hipLaunchKernelGGL(k_x4k_big, dim3(grid), dim3(256), 0, st, b); });
+        if (!skip_big)
+            run("x4k_big", grid, [&](int i) { Big b{}; b.i = i; pp(i, b.in, b.out);
+                hipLaunchKernelGGL(k_x4k_big, dim3(grid), dim3(256), 0, st, b); });
         run("x4k_vgpr", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
             hipLaunchKernelGGL(k_x4k_vgpr, dim3(grid), dim3(256), 0, st, i, in, out); });
         run("x4k_lds", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
