@@ -86,11 +86,10 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
     // (SPW <= 2, the sub-talker's shapes: every step before the staging --
     // batch 8 152.5 / 153.2 / 152.6 vs 151.1 / 151.0 / 150.8 audio-s/s with
     // only the first, alternating processes, profiles/r05e_ab_prefetch_modes.txt)
-#ifdef QTTS_GB_ALLW4
-    constexpr int SA = SPW <= 2 || PM == 0 ? SPW : (SPW + 1) / 2;   // (A/B build: also every step of the partial-free shapes)
-#else
+    // (also every step of the partial-free SPW 4 / 8 shapes -- the talker's --
+    // measured slower: batch 8 150.4-150.7 vs 152.0-152.6, batch 16 237.2 vs
+    // 238.5, profiles/r05f_ab_batch_allw.txt)
     constexpr int SA = SPW <= 2 ? SPW : (SPW + 1) / 2;
-#endif
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
     const int nb = a.nb;
     const int kz = gridDim.y, Ck = a.C / kz, woff = blockIdx.y * Ck;
