@@ -49,3 +49,28 @@ def test_oracle_long_prefill_and_steps_bit_exact(hd128):
         lg, hid = o.step(steps[i])
         np.testing.assert_array_equal(lg, g["step_logits"][i])
         np.testing.assert_array_equal(hid, g["step_hidden"][i])
+
+
+def test_long_fixtures_describe_the_bench_workloads():
+    """The round-5 reference fixtures hold what bench.py runs (no compute):
+    long_17b_b8bench = rank 0's 8 utterances of `bench.py --batch 8`
+    (rank_prompt_seeds), long_eos17 = the P128 prompts of bench.py --eos's
+    model with each slot's codes up to the reference's EOS stop."""
+    import bench
+    from synth_model import prompt_ids
+    man = json.load(open(os.path.join(GOLDEN, "long_manifest.json")))
+    g = np.load(os.path.join(GOLDEN, "long_17b_b8bench.npz"))
+    m = man["b8bench"]
+    assert m["prompt_seeds"] == bench.rank_prompt_seeds(0, 8) and m["frames"] == 128 and m["speakers"] == ["aiden"] * 8
+    for b, sd in enumerate(m["prompt_seeds"]):
+        n = int(g["prompt_len"][b])
+        np.testing.assert_array_equal(g["prompt_ids"][b, :n], prompt_ids("p128", sd))
+    assert g["codes"].shape == (8, 128, 16) and g["codes"].min() >= 0 and g["codes"].max() < 3072
+    e = np.load(os.path.join(GOLDEN, "long_eos17.npz"))
+    m = man["eos17"]
+    assert m["eos_gain"] == bench.EOS_GAIN and m["max_tokens"] > max(int(x) for x in e["stop_step"])
+    for b, sd in enumerate(m["prompt_seeds"]):
+        n, T = int(e["prompt_len"][b]), int(e["stop_step"][b])
+        np.testing.assert_array_equal(e["prompt_ids"][b, :n], prompt_ids("p128", sd))
+        assert (e["codes"][b, :T] >= 0).all() and (e["codes"][b, T:] == -1).all()
+    assert len(set(int(x) for x in e["stop_step"])) == len(m["prompt_seeds"])   # the batch test needs rows stopping apart
