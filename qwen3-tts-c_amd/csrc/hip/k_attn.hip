@@ -648,9 +648,12 @@ int qtts_attn_o(const AttnArgs &a, const bf16_t *Wo, int R, float *part, hipStre
 // splits) overrides both for split-size A/B runs.  The model latches it ONCE
 // at creation (qtts_dev::attn_lpk) and passes it in AttnArgs::lpk, so the
 // split scratch it sizes at allocation always covers the launch.
+// Round 5: 32-key splits at HD 128 also where the last split merges (the
+// lock-step batch): batch 8 153.5 / 153.3 vs 153.2 / 152.4 audio-s/s with
+// 64-key splits (profiles/r05h_batch_switch_sweep.txt).
 static int attn_lpk(int HD, bool defer, int env) {
     if (HD == 128 && (env == 4 || env == 8 || env == 16)) return env;
-    if (HD == 128 && defer) return 8;
+    if (HD == 128) return 8;
     return HD >= 32 ? HD / 32 : 1;
 }
 int qtts_attn_keys_per_split(int HD, bool defer, int lpk) { return 256 / attn_lpk(HD, defer, lpk); }

@@ -24,6 +24,9 @@
 //   x4k_code4    four such kernels in rotation (96 KB of code between reuses)
 //   x4k_loop     the same instruction count as a loop over a 96-B body
 //   x4k_resid    + y[r] += v epilogue (a dependent read-modify-write of the output)
+//   x32k / x64k  every workgroup reads the previous launch's whole 32 / 64 KB
+//                output (the batch GEMVs' x of 8 rows); _rep8: the output in 8
+//                copies, each XCD's workgroups reading their own
 //   gemv_gu      the sub-talker gate|up shape (6144 x 1024 bf16, Infinity-Cache
 //                resident), whole weight slice in flight before x (k_gemvw-like)
 //
@@ -133,6 +136,36 @@ __global__ __launch_bounds__(256) void k_x4k_resid(int i, const float *in, float
     if (threadIdx.x < 4) out[blockIdx.x * 4 + threadIdx.x] += s * 0.25f;
     stamp_end(i, t0);
 }
+// The batch GEMVs' x fetch: every workgroup reads the previous launch's
+// whole KB-KB output (KB = 32 / 64: the sub-talker / talker x of 8 batch
+// rows) and writes its KB floats of the next; REP = 1: the output is stored
+// in 8 copies and workgroup b reads the copy of its XCD, (b + 7) % 8
+// (profiles/r05a_mb_l2pf_xcc.txt), so the 8 XCDs' misses go to 8 different
+// sets of lines instead of all to one
+template <int KB, int REP>
+__global__ __launch_bounds__(256) void k_xbig(int i, const float *in, float *out) {
+    const auto t0 = now();
+    __shared__ float red[4];
+    constexpr int N = KB * 256, J = N / 1024;
+    const int c = REP ? (blockIdx.x + 7) % 8 : 0;
+    const float *src = in + (size_t)c * N;
+    float4 v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = reinterpret_cast<const float4 *>(src)[threadIdx.x + 256 * j];
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) a += v[j].x + v[j].y + v[j].z + v[j].w;
+    const float sw = wsum(a);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
+    __syncthreads();
+    const float s = (red[0] + red[1] + red[2] + red[3]) * 1e-3f;
+    if (threadIdx.x < KB) {
+#pragma unroll
+        for (int cc = 0; cc < (REP ? 8 : 1); ++cc) out[(size_t)cc * N + blockIdx.x * KB + threadIdx.x] = s;
+    }
+    stamp_end(i, t0);
+}
+
 // gate|up-like: grid 256, 24 rows per workgroup (RW 6), C = 1024 (NV 2)
 __global__ __launch_bounds__(256) void k_gemv_gu(int i, const uint16_t *W, const float *in, float *out) {
     const auto t0 = now();
@@ -193,10 +226,10 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     float *va, *vb;
-    CK(hipMalloc(&va, 8192 * 4));
-    CK(hipMalloc(&vb, 8192 * 4));
-    CK(hipMemset(va, 0, 8192 * 4));
-    CK(hipMemset(vb, 0, 8192 * 4));
+    CK(hipMalloc(&va, 8 * 16384 * 4));
+    CK(hipMalloc(&vb, 8 * 16384 * 4));
+    CK(hipMemset(va, 0, 8 * 16384 * 4));
+    CK(hipMemset(vb, 0, 8 * 16384 * 4));
     uint16_t *W;
     const size_t wn = (size_t)6144 * 1024;
     CK(hipMalloc(&W, wn * 2));
@@ -290,6 +323,16 @@ int main(int argc, char **argv) {
             hipLaunchKernelGGL(k_x4k_loop, dim3(grid), dim3(256), 0, st, i, in, out); });
         run("x4k_resid", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
             hipLaunchKernelGGL(k_x4k_resid, dim3(grid), dim3(256), 0, st, i, in, out); });
+        if (grid == 256) {
+            run("x32k", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
+                hipLaunchKernelGGL((k_xbig<32, 0>), dim3(grid), dim3(256), 0, st, i, in, out); });
+            run("x32k_rep8", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
+                hipLaunchKernelGGL((k_xbig<32, 1>), dim3(grid), dim3(256), 0, st, i, in, out); });
+            run("x64k", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
+                hipLaunchKernelGGL((k_xbig<64, 0>), dim3(grid), dim3(256), 0, st, i, in, out); });
+            run("x64k_rep8", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
+                hipLaunchKernelGGL((k_xbig<64, 1>), dim3(grid), dim3(256), 0, st, i, in, out); });
+        }
         if (grid == 256)
             run("gemv_gu", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
                 hipLaunchKernelGGL(k_gemv_gu, dim3(grid), dim3(256), 0, st, i, W, in, out); });
