@@ -1522,7 +1522,6 @@ int add_slot(CodecStream &S, int c, int h) {
 
 void codec_stream_free(CodecModel *m) {
     CodecStream &S = m->cs;
-    if (S.g1) hipGraphExecDestroy(S.g1);
     for (void *p : S.allocs) hipFree(p);
     S = CodecStream();
 }
@@ -1602,7 +1601,6 @@ int codec_stream_begin(CodecModel *m, int max_frames, int chunk) {
     for (size_t i = 0; i < io.size(); ++i) io[i] = (int)i;
     S.iota = (int *)salloc(S, io.size() * 4);
     S.zeros = (int *)salloc(S, (size_t)tc * 4);
-    S.g1_wav = (float *)salloc(S, 1920 * 4);
     for (void *p : S.allocs)
         if (!p) return -1;
     if (!S.bufA || !S.bufB || !S.bufC || !S.bufD || !S.rope_cos || !S.rope_sin || !S.iota || !S.zeros) return -1;
@@ -1633,53 +1631,6 @@ int codec_stream_push(CodecModel *m, const int *codes, int ldc_codes, int Ttot, 
     return codec_stream_push_to(m, codes, ldc_codes, Ttot, host_out, true);
 }
 
-static int stream_push_body(CodecModel *m, const int *codes, int Ttot, float *out, bool host);
-
-// The first packet's push (1 frame, position 0, no K/V history) replays a
-// graph of its ~220 launches instead of launching them one by one (host-bound
-// at that size).  The graph is captured right after the first eager push of a
-// stream -- the host-side state it reads (pos0 = 0, hl = 0) is reset for the
-// capture and restored after -- so the first request pays the capture and
-// every later first packet replays it.  QTTS_HIP_CODEC_G1=0: always eager.
-static int first_push(CodecModel *m, const int *codes, float *out, bool host) {
-    CodecStream &S = m->cs;
-    const char *e = getenv("QTTS_HIP_CODEC_G1");
-    if ((e && !atoi(e)) || !S.g1_wav) return 1;
-    if (S.g1 && S.g1_codes == codes && S.g1_part == m->xg_part) {
-        if (hipGraphLaunch(S.g1, m->st) != hipSuccess) return -1;
-        S.pos0 = 1;
-        S.hl = 1 < m->d.cwin - 1 ? 1 : m->d.cwin - 1;
-        if (hipMemcpyAsync(out, S.g1_wav, 1920 * 4, host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, m->st) !=
-            hipSuccess)
-            return -1;
-        if (host && hipStreamSynchronize(m->st) != hipSuccess) return -1;
-        return 1920;
-    }
-    // eager, then capture the same work for the next first packet
-    const int n = stream_push_body(m, codes, 1, out, host);
-    if (n != 1920) return n;
-    const int pos0 = S.pos0, hl = S.hl;
-    if (S.g1) { hipGraphExecDestroy(S.g1); S.g1 = nullptr; }
-    S.pos0 = 0;
-    S.hl = 0;
-    hipGraph_t g = nullptr;
-    bool ok = hipStreamBeginCapture(m->st, hipStreamCaptureModeThreadLocal) == hipSuccess;
-    const int r = ok ? stream_push_body(m, codes, 1, S.g1_wav, false) : -1;
-    ok = hipStreamEndCapture(m->st, &g) == hipSuccess && ok && r == 1920;
-    if (ok) ok = hipGraphInstantiate(&S.g1, g, nullptr, nullptr, 0) == hipSuccess;
-    if (g) hipGraphDestroy(g);
-    if (!ok) {
-        S.g1 = nullptr;
-        hipGetLastError();   // (an unsupported capture only disables the cache)
-    } else {
-        S.g1_codes = codes;
-        S.g1_part = m->xg_part;
-    }
-    S.pos0 = pos0;
-    S.hl = hl;
-    return n;
-}
-
 int codec_stream_push_to(CodecModel *m, const int *codes, int ldc_codes, int Ttot, float *out, bool host) {
     CodecStream &S = m->cs;
     const qtts_dims_t &d = m->d;
@@ -1692,16 +1643,6 @@ int codec_stream_push_to(CodecModel *m, const int *codes, int ldc_codes, int Tto
         fprintf(stderr, "qtts codec stream: %d frames exceed the stream capacity\n", S.pos0 + Ttot);
         return -1;
     }
-    if (Ttot == 1 && S.pos0 == 0 && S.hl == 0) {
-        const int n = first_push(m, codes, out, host);
-        if (n != 1) return n;
-    }
-    return stream_push_body(m, codes, Ttot, out, host);
-}
-
-static int stream_push_body(CodecModel *m, const int *codes, int Ttot, float *out, bool host) {
-    CodecStream &S = m->cs;
-    const qtts_dims_t &d = m->d;
     hipStream_t st = m->st;
     const int lat = d.clat, vq = d.ccbdim / 2, half = lat / 2, hm = S.hm;
     int written = 0;

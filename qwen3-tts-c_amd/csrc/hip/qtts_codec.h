@@ -33,13 +33,6 @@ struct CodecStream {
     int *iota = nullptr;       // [0 .. win + tc)
     int *zeros = nullptr;
     std::vector<void *> allocs;
-    // the first packet's push (1 frame from a fresh stream: position 0, no
-    // K/V history) as a HIP graph, captured after the first such push and
-    // replayed by later ones with the same inputs (first_push below)
-    hipGraphExec_t g1 = nullptr;
-    const int *g1_codes = nullptr;   // the codes pointer and workspace it was captured with
-    const float *g1_part = nullptr;
-    float *g1_wav = nullptr;         // its 1920-sample device output
 };
 
 struct CodecModel {
