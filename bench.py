@@ -492,6 +492,9 @@ def main():
     torch.cuda.synchronize()
     barrier(ws)
     el = time.perf_counter() - t0
+    # the last timed step's phases (run_batch's perf_* fields: prefill, decode
+    # loop, codec -- for a batch, every slot's codec pass)
+    phases = dict(prefill_ms=m.c.perf_prefill_ms, talker_ms=m.c.perf_talker_ms, codec_ms=m.c.perf_codec_ms)
     eos = None
     if args.eos:
         # the same utterances at the same length in fixed-length mode: what the
@@ -630,7 +633,7 @@ def main():
         }
         if fp:
             out["first_packet_ms"] = round(fp["first_packet_ms"], 2)
-            out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in fp.items()}
+        out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in (fp or phases).items()}
         out["ranks"] = ranks
         if enc:
             out["ref_audio_encode"] = enc

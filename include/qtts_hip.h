@@ -135,6 +135,17 @@ float *qtts_dev_codec_slot(qtts_dev_t *dev, int b, int T, int *out_samples);
 int qtts_dev_codec_timing(qtts_dev_t *dev, int on);
 int qtts_dev_codec_stage_ms(const qtts_dev_t *dev, float *ms);
 
+/* Several utterances' full codec decodes (a batch's slots; the reference
+ * decodes its one utterance after the loop, Q.c:1376-1383, Cd.c:581-749):
+ * job i decodes host_codes[i] ([T[i]][16] host ints) when host_codes and
+ * host_codes[i] are non-NULL, else slot slot[i]'s first T[i] generated frames.
+ * Up to QTTS_HIP_CODEC_LANES (default 4) decodes run side by side on their own
+ * streams and scratch, each the same kernels as a lone decode (bit-identical
+ * audio).  audio[i] (malloc'd host floats, T[i] * 1920 samples) and samples[i]
+ * are filled; returns 0, or -1 with every audio[i] NULL. */
+int qtts_dev_codec_multi(qtts_dev_t *dev, int n, const int *const *host_codes, const int *slot, const int *T,
+                         float **audio, int *samples);
+
 /* Streaming codec decode, exact and incremental (every codec op is causal:
  * conv histories, transposed-conv tails and the window-72 transformer K/V are
  * carried between pushes).  begin resets the stream (max_frames bounds the

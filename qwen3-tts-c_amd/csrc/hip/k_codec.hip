@@ -1210,14 +1210,15 @@ static int codec_transformer(CodecModel *m, const float *pc /*[lat][T]*/, int T,
     return xgm(m, og, st);
 }
 
-float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
+// the whole decode enqueued on m->st; the clamped waveform stays in m's
+// scratch (*wav, *L samples) until the next use of m
+static int codec_decode_enqueue(CodecModel *m, const int *codes, int T, float **wav_out, int *L_out) {
     const qtts_dims_t &d = m->d;
-    if (out_samples) *out_samples = 0;
-    if (ensure_codec_state(m, T)) return nullptr;
+    if (ensure_codec_state(m, T)) return -1;
     hipStream_t st = m->st;
     const int lat = d.clat, vq = d.ccbdim / 2, half = lat / 2;
     float *A = m->bufA, *B = m->bufB, *Cb = m->bufC, *D = m->bufD;
-#define DCK(x) do { if ((x) != 0) { fprintf(stderr, "qtts codec: stage failed at %s:%d\n", __FILE__, __LINE__); return nullptr; } } while (0)
+#define DCK(x) do { if ((x) != 0) { fprintf(stderr, "qtts codec: stage failed at %s:%d\n", __FILE__, __LINE__); return -1; } } while (0)
     m->timed = false;
     if (m->timing && !m->tev[0])
         for (hipEvent_t &e : m->tev)
@@ -1296,10 +1297,21 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
              cw(m, "decoder.decoder.5.alpha"), cw(m, "decoder.decoder.5.beta"), nullptr));
     hipLaunchKernelGGL(k_clamp, dim3((L + 255) / 256), dim3(256), 0, st, wav, L);
     mark(5);
+    *wav_out = wav;
+    *L_out = L;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+#undef DCK
+}
+
+float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
+    if (out_samples) *out_samples = 0;
+    float *wav = nullptr;
+    int L = 0;
+    if (codec_decode_enqueue(m, codes, T, &wav, &L)) return nullptr;
     float *host = (float *)malloc((size_t)L * sizeof(float));
     if (!host) return nullptr;
-    if (hipMemcpyAsync(host, wav, (size_t)L * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
+    if (hipMemcpyAsync(host, wav, (size_t)L * 4, hipMemcpyDeviceToHost, m->st) != hipSuccess ||
+        hipStreamSynchronize(m->st) != hipSuccess) {
         free(host);
         return nullptr;
     }
@@ -1309,7 +1321,83 @@ float *codec_decode(CodecModel *m, const int *codes, int T, int *out_samples) {
     }
     if (out_samples) *out_samples = L;
     return host;
-#undef DCK
+}
+
+// ---------------------------------------------------------------- independent decodes side by side
+// A batch's utterances are decoded by independent codec passes (one per slot,
+// as qwen_tts_generate decodes its one utterance, Cd.c:581-749).  One pass is
+// a chain of ~200 launches, most of them latency-bound (the transformer's
+// 128-row GEMMs, the small-channel early convs), so several passes run side by
+// side: lane k (m itself for k = 0, else a CodecModel that shares m's weights
+// and re-laid weights and owns its scratch, split-K workspace and stream)
+// decodes jobs k, k + nl, ...; each job's waveform goes device-to-device into
+// `dwav` behind its last kernel (the lane's scratch is reused by its next job
+// in stream order), and the host waits once for every lane.  The kernels,
+// shapes and split decisions are a lone decode's, so the audio is
+// bit-identical to codec_decode's.
+static void lane_sync_weights(CodecModel *m, CodecModel *ln) {
+    ln->d = m->d;
+    ln->cb = m->cb;
+    ln->w = m->w;
+    ln->wt = m->wt;
+    ln->timing = false;
+}
+
+CodecModel *codec_lane_new(CodecModel *m, hipStream_t st) {
+    CodecModel *ln = new CodecModel;
+    lane_sync_weights(m, ln);
+    ln->st = st;
+    return ln;
+}
+
+// (every re-laid weight a lane made was adopted by m or freed by
+// codec_decode_many, so the lane owns only its scratch)
+void codec_lane_delete(CodecModel *ln) {
+    if (!ln) return;
+    ln->wt.clear();
+    ln->w.clear();
+    codec_free_state(ln);
+    delete ln;
+}
+
+int codec_decode_many(CodecModel *m, CodecModel *const *lanes, int nl, int n, const int *const *codes,
+                      const int *T, float *dwav, const size_t *dwav_off, int *out_samples) {
+    if (nl < 1 || n < 0) return -1;
+    if (nl > n) nl = n;
+    for (int k = 1; k < nl; ++k) lane_sync_weights(m, lanes[k]);
+    hipEvent_t ready = nullptr;
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess) return -1;
+    int rc = hipEventRecord(ready, m->st) == hipSuccess ? 0 : -1;   // the codes were written on m->st
+    for (int k = 1; k < nl && !rc; ++k)
+        if (hipStreamWaitEvent(lanes[k]->st, ready, 0) != hipSuccess) rc = -1;
+    for (int i = 0; i < n && !rc; ++i) {
+        CodecModel *ln = i % nl == 0 ? m : lanes[i % nl];
+        float *wav = nullptr;
+        int L = 0;
+        if (codec_decode_enqueue(ln, codes[i], T[i], &wav, &L) ||
+            hipMemcpyAsync(dwav + dwav_off[i], wav, (size_t)L * 4, hipMemcpyDeviceToDevice, ln->st) != hipSuccess) {
+            rc = -1;
+            break;
+        }
+        out_samples[i] = L;
+    }
+    for (int k = 0; k < nl; ++k) {
+        CodecModel *ln = k == 0 ? m : lanes[k];
+        if (hipStreamSynchronize(ln->st) != hipSuccess) rc = -1;
+    }
+    hipEventDestroy(ready);
+    // adopt the re-laid weights a lane made (the first decode of a shape on
+    // it); a key made by two lanes keeps the first copy, the other is freed
+    // (every stream has drained)
+    for (int k = 1; k < nl; ++k) {
+        for (auto &kv : lanes[k]->wt) {
+            auto it = m->wt.find(kv.first);
+            if (it == m->wt.end()) m->wt[kv.first] = kv.second;
+            else if (it->second != kv.second) hipFree(kv.second);
+        }
+        lanes[k]->wt = m->wt;
+    }
+    return rc;
 }
 
 // ===================================================================== kernel-level C-ABI

@@ -74,6 +74,14 @@ int codec_put_tensor(CodecModel *m, const std::string &name, const void *host, i
 int codec_finalize(CodecModel *m);
 // codes: device int32 [T][cq] (time-major).  Returns malloc'd host audio.
 float *codec_decode(CodecModel *m, const int *codes_dev, int T, int *out_samples);
+// independent decodes side by side: job i (device codes[i], T[i] frames) on
+// lane i % nl (lane 0 = m, lanes[k] from codec_lane_new for k >= 1), its
+// waveform copied to dwav + dwav_off[i] (device), out_samples[i] samples;
+// returns after every lane's stream has drained
+CodecModel *codec_lane_new(CodecModel *m, hipStream_t st);
+void codec_lane_delete(CodecModel *lane);
+int codec_decode_many(CodecModel *m, CodecModel *const *lanes, int nl, int n, const int *const *codes, const int *T,
+                      float *dwav, const size_t *dwav_off, int *out_samples);
 // streaming decode: begin resets the state (max_frames bounds the absolute
 // position; chunk > 16 sizes the internal chunk for long pushes); push decodes T more frames (device codes, rows of stride ldc
 // ints) and writes T * 1920 samples to host_out.  Returns samples or -1.

@@ -164,6 +164,15 @@ struct qtts_dev {
     bool prime_pending = false;   // a qtts_dev_codec_stream_prime push runs on cst (cev marks its end)
     float *pwav = nullptr;        // the prime's discarded audio (never the codec_async output cwav)
     size_t pwav_cap = 0;
+    // a batch's codec passes side by side (qtts_dev_codec_multi): lanes 1.. with
+    // their own scratch and stream (lane 0 is `codec`), the waveforms and the
+    // host-given codes staged on the device
+    std::vector<CodecModel *> clanes;
+    std::vector<hipStream_t> clane_st;
+    float *mwav = nullptr;
+    size_t mwav_cap = 0;
+    int *mcodes = nullptr;
+    size_t mcodes_cap = 0;
     // per-kernel profiling of one eager frame (qtts_dev_profile_frame)
     struct Prof { int kind; double bytes; hipEvent_t a, b; const char *name; };
     std::vector<Prof> prof;
@@ -445,6 +454,10 @@ extern "C" void qtts_dev_destroy(qtts_dev_t *dv) {
     if (dv->hstop) hipHostFree(dv->hstop);
     for (hipEvent_t e : dv->fev)
         if (e) hipEventDestroy(e);
+    for (CodecModel *ln : dv->clanes) codec_lane_delete(ln);
+    for (hipStream_t st : dv->clane_st) hipStreamDestroy(st);
+    if (dv->mwav) hipFree(dv->mwav);
+    if (dv->mcodes) hipFree(dv->mcodes);
     if (dv->cwav) hipFree(dv->cwav);
     if (dv->pwav) hipFree(dv->pwav);
     if (dv->push_codes) hipFree(dv->push_codes);
@@ -1733,6 +1746,107 @@ extern "C" float *qtts_dev_codec_decode_host(qtts_dev_t *dv, const int *codes, i
         r = codec_decode(&dv->codec, dc, T, out_samples);
     hipFree(dc);
     return r;
+}
+
+// Several utterances' codec passes at once (a batch's slots, run_batch): job
+// i decodes host_codes[i] (T[i] frames, [T][cq] time-major) when given, else
+// slot slot[i]'s first T[i] generated frames.  QTTS_HIP_CODEC_LANES (default
+// 4) passes run side by side (codec_decode_many); 1 decodes them one after
+// another with codec_decode.  audio[i] is malloc'd host memory.
+extern "C" int qtts_dev_codec_multi(qtts_dev_t *dv, int n, const int *const *host_codes, const int *slot, const int *T,
+                                    float **audio, int *samples) {
+    if (!dv || n < 1 || !T || !audio || !samples) return -1;
+    for (int i = 0; i < n; ++i) {
+        audio[i] = nullptr;
+        samples[i] = 0;
+        const bool host = host_codes && host_codes[i];
+        if (T[i] < 1 || (!host && (!slot || slot[i] < 0 || slot[i] >= dv->nb || T[i] > dv->max_frames + 1)))
+            return -1;
+    }
+    hipSetDevice(dv->device);
+    CKI(join_prime(dv));
+    const int cq = dv->d.cq;
+    // host codes staged once for every job
+    size_t nh = 0;
+    for (int i = 0; i < n; ++i)
+        if (host_codes && host_codes[i]) nh += (size_t)T[i] * cq;
+    if (nh > dv->mcodes_cap) {
+        CK(hipDeviceSynchronize());
+        if (dv->mcodes) CK(hipFree(dv->mcodes));
+        dv->mcodes = nullptr;
+        dv->mcodes_cap = 0;
+        CK(hipMalloc(&dv->mcodes, nh * 4));
+        dv->mcodes_cap = nh;
+    }
+    std::vector<const int *> dcodes(n);
+    size_t ho = 0;
+    for (int i = 0; i < n; ++i) {
+        if (host_codes && host_codes[i]) {
+            CK(hipMemcpyAsync(dv->mcodes + ho, host_codes[i], (size_t)T[i] * cq * 4, hipMemcpyHostToDevice, dv->st));
+            dcodes[i] = dv->mcodes + ho;
+            ho += (size_t)T[i] * cq;
+        } else {
+            dcodes[i] = dv->codes + (size_t)slot[i] * (dv->max_frames + 1) * dv->d.G;
+        }
+    }
+    const char *e = getenv("QTTS_HIP_CODEC_LANES");
+    int nl = e ? atoi(e) : 4;
+    if (nl < 1) nl = 1;
+    if (nl > 16) nl = 16;
+    if (nl > n) nl = n;
+    auto fail = [&]() {
+        for (int i = 0; i < n; ++i) {
+            free(audio[i]);
+            audio[i] = nullptr;
+            samples[i] = 0;
+        }
+        return -1;
+    };
+    if (nl == 1) {
+        for (int i = 0; i < n; ++i) {
+            audio[i] = codec_decode(&dv->codec, dcodes[i], T[i], &samples[i]);
+            if (!audio[i]) return fail();
+        }
+        return 0;
+    }
+    while ((int)dv->clanes.size() < nl - 1) {
+        hipStream_t st = nullptr;
+        CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        dv->clane_st.push_back(st);
+        dv->clanes.push_back(codec_lane_new(&dv->codec, st));
+    }
+    std::vector<CodecModel *> lanes(nl, nullptr);
+    for (int k = 1; k < nl; ++k) lanes[k] = dv->clanes[k - 1];
+    // one hop of samples per frame: the decoder's total upsampling (2 x 2 x 8 x
+    // 5 x 4 x 3 = 1920 for the released codec), exactly codec_decode's L / T
+    const size_t hop = (size_t)dv->d.ratios[0] * dv->d.ratios[1] * dv->d.rates[0] * dv->d.rates[1] *
+                       dv->d.rates[2] * dv->d.rates[3];
+    std::vector<size_t> off(n);
+    size_t tot = 0;
+    for (int i = 0; i < n; ++i) {
+        off[i] = tot;
+        tot += (size_t)T[i] * hop;
+    }
+    if (tot > dv->mwav_cap) {
+        CK(hipDeviceSynchronize());
+        if (dv->mwav) CK(hipFree(dv->mwav));
+        dv->mwav = nullptr;
+        dv->mwav_cap = 0;
+        CK(hipMalloc(&dv->mwav, tot * 4));
+        dv->mwav_cap = tot;
+    }
+    std::vector<int> ns(n, 0);
+    if (codec_decode_many(&dv->codec, lanes.data(), nl, n, dcodes.data(), T, dv->mwav, off.data(), ns.data()))
+        return fail();
+    for (int i = 0; i < n; ++i) {
+        if ((size_t)ns[i] != (size_t)T[i] * hop) return fail();
+        audio[i] = (float *)malloc((size_t)ns[i] * sizeof(float));
+        if (!audio[i] ||
+            hipMemcpy(audio[i], dv->mwav + off[i], (size_t)ns[i] * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail();
+        samples[i] = ns[i];
+    }
+    return 0;
 }
 
 // ----------------------------------------------------------------- kernel-level C-ABI

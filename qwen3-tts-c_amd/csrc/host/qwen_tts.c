@@ -625,6 +625,22 @@ static void codec_log_end(qwen_tts_ctx_t *ctx, int samples) {
                 ms[0], ms[1], ms[2], ms[3], ms[4]);
 }
 
+/* voice clone: keep the audio after the reference frames of a decode of
+ * reference ++ generated codes (qwen3_tts_model.py:612-630, the same float
+ * cut); takes ownership of w */
+static void cut_reference(float *w, int nw, int n_ref, int tot, float **audio, int *samples) {
+    const int cut = (int)((double)n_ref / (double)tot * (double)nw);
+    *audio = NULL;
+    *samples = 0;
+    if (w && nw > cut) {
+        memmove(w, w + cut, (size_t)(nw - cut) * sizeof(float));
+        *audio = w;
+        *samples = nw - cut;
+    } else {
+        free(w);
+    }
+}
+
 static void params_of(const qwen_tts_ctx_t *ctx, qtts_gen_params_t *p) {
     p->temperature = ctx->temperature; p->top_p = ctx->top_p; p->repetition_penalty = ctx->repetition_penalty;
     p->top_k = ctx->top_k; p->st_temperature = ctx->subtalker_temperature; p->st_top_p = ctx->subtalker_top_p;
@@ -690,6 +706,18 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     if (stream && (qtts_dev_codec_stream_begin_ex(dev, max_tokens + sref, sref) != 0 ||
                    (sref && qtts_dev_codec_stream_prime(dev, vcs[0].ref_codes, sref) != 0)))
         goto out;
+    /* one utterance, fixed length, not streamed: the codec's exact streaming
+     * decode runs chunk by chunk on a second HIP stream behind the frames it
+     * reads (qtts_dev_codec_async_*), instead of one pass after the loop
+     * (Q.c:1376-1383); QTTS_HIP_CODEC_OVERLAP=<frames per push> (0: after the loop) */
+    int overlap = 0;
+    if (!stream && nb == 1 && fixed > 0 && !(vcs && vcs[0].ref_codes && vcs[0].n_ref > 0)) {
+        const char *e = getenv("QTTS_HIP_CODEC_OVERLAP");
+        overlap = e ? atoi(e) : 0;
+        if (overlap < 0) overlap = 0;
+        if (overlap && qtts_dev_codec_async_begin(dev, max_tokens) != 0) goto out;
+    }
+    int pushed = 0;
     double t_prefill = now_ms();
     if (qtts_dev_prefill(dev) != 0) goto out;
     double t_prefill_done = now_ms();
@@ -721,6 +749,12 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             ctx->perf_first_frame_ms = now_ms() - t_start;
         }
         if (ctx->progress_cb) ctx->progress_cb(step + 1, max_tokens, ctx->progress_cb_userdata);
+        if (overlap && (step + 1) % overlap == 0) {
+            if (qtts_dev_codec_async_push(dev, 0, pushed, step + 1 - pushed) < 0) {
+                free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
+            }
+            pushed = step + 1;
+        }
         if (lagged) {   /* EOS mode: frame step is queued; stop once every slot had stopped by frame step - 1 */
             int done = 0;
             if (step >= 1 && qtts_dev_frame_done(dev, step - 1, &done) != 0) {
@@ -790,40 +824,98 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
         samples[0] = streamed * 1920;
         if (streamed <= 0) { free(sbuf); audio[0] = NULL; rc = -1; }
         ctx->perf_codec_ms = t_stream;
+    } else if (nb == 1) {
+        audio[0] = NULL;
+        samples[0] = 0;
+        if (ngen[0] <= 0) {
+            rc = -1;
+        } else if (overlap) {
+            /* the frames after the last push, then the waveform the pushes wrote */
+            codec_log_begin(ctx, ngen[0]);
+            float *w = (float *)malloc((size_t)ngen[0] * 1920 * sizeof(float));
+            if (w && (pushed == ngen[0] || qtts_dev_codec_async_push(dev, 0, pushed, ngen[0] - pushed) >= 0) &&
+                qtts_dev_codec_async_end(dev, w, ngen[0]) == ngen[0] * 1920) {
+                audio[0] = w;
+                samples[0] = ngen[0] * 1920;
+            } else {
+                free(w);
+                rc = -1;
+            }
+            codec_log_end(ctx, samples[0]);
+        } else if (vcs && vcs[0].ref_codes && vcs[0].n_ref > 0) {
+            /* voice clone: decode reference ++ generated codes, keep the part
+             * after the reference (qwen3_tts_model.py:612-630, same float cut) */
+            const vclone_t *vc = &vcs[0];
+            const int tot = vc->n_ref + ngen[0];
+            int *all = (int *)malloc((size_t)tot * G * sizeof(int)), nw = 0;
+            if (all && qtts_dev_get_codes(dev, 0, all + (size_t)vc->n_ref * G, ngen[0]) == ngen[0]) {
+                memcpy(all, vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
+                codec_log_begin(ctx, tot);
+                float *w = qtts_dev_codec_decode_host(dev, all, tot, &nw);
+                codec_log_end(ctx, w ? nw : 0);
+                cut_reference(w, nw, vc->n_ref, tot, &audio[0], &samples[0]);
+            }
+            free(all);
+            if (!audio[0]) rc = -1;
+        } else {
+            codec_log_begin(ctx, ngen[0]);
+            audio[0] = qtts_dev_codec_slot(dev, 0, ngen[0], &samples[0]);
+            codec_log_end(ctx, audio[0] ? samples[0] : 0);
+            if (!audio[0] || samples[0] <= 0) rc = -1;
+        }
     } else {
+        /* a batch: every slot's codec pass in one call, several side by side
+         * (qtts_dev_codec_multi); a voice-clone slot decodes its reference ++
+         * generated codes and keeps the part after the reference */
+        int **hc = (int **)calloc(nb, sizeof(int *));
+        int *slot = (int *)calloc(nb, sizeof(int)), *tj = (int *)calloc(nb, sizeof(int));
+        int *bj = (int *)calloc(nb, sizeof(int));
+        float **aj = (float **)calloc(nb, sizeof(float *));
+        int *sj = (int *)calloc(nb, sizeof(int));
+        int nj = 0;
         for (int b = 0; b < nb; b++) {
             audio[b] = NULL;
             samples[b] = 0;
-            if (ngen[b] <= 0) { rc = -1; continue; }
-            if (vcs && vcs[b].ref_codes && vcs[b].n_ref > 0) {
-                /* voice clone: decode reference ++ generated codes, keep the part
-                 * after the reference (qwen3_tts_model.py:612-630, same float cut) */
-                const vclone_t *vc = &vcs[b];
-                const int tot = vc->n_ref + ngen[b];
-                int *all = (int *)malloc((size_t)tot * G * sizeof(int)), nw = 0;
-                if (all && qtts_dev_get_codes(dev, b, all + (size_t)vc->n_ref * G, ngen[b]) == ngen[b]) {
-                    memcpy(all, vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
-                    codec_log_begin(ctx, tot);
-                    float *w = qtts_dev_codec_decode_host(dev, all, tot, &nw);
-                    codec_log_end(ctx, w ? nw : 0);
-                    const int cut = (int)((double)vc->n_ref / (double)tot * (double)nw);
-                    if (w && nw > cut) {
-                        memmove(w, w + cut, (size_t)(nw - cut) * sizeof(float));
-                        audio[b] = w;
-                        samples[b] = nw - cut;
-                    } else {
-                        free(w);
-                    }
+        }
+        if (!hc || !slot || !tj || !bj || !aj || !sj) rc = -1;
+        for (int b = 0; b < nb && rc == 0; b++) {
+            if (ngen[b] <= 0) { rc = -1; break; }
+            const vclone_t *vc = vcs && vcs[b].ref_codes && vcs[b].n_ref > 0 ? &vcs[b] : NULL;
+            slot[nj] = b;
+            bj[nj] = b;
+            tj[nj] = (vc ? vc->n_ref : 0) + ngen[b];
+            if (vc) {
+                hc[nj] = (int *)malloc((size_t)tj[nj] * G * sizeof(int));
+                if (!hc[nj] || qtts_dev_get_codes(dev, b, hc[nj] + (size_t)vc->n_ref * G, ngen[b]) != ngen[b]) {
+                    rc = -1;
+                    break;
                 }
-                free(all);
-                if (!audio[b]) rc = -1;
-                continue;
+                memcpy(hc[nj], vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
             }
-            codec_log_begin(ctx, ngen[b]);
-            audio[b] = qtts_dev_codec_slot(dev, b, ngen[b], &samples[b]);
-            codec_log_end(ctx, audio[b] ? samples[b] : 0);
+            codec_log_begin(ctx, tj[nj]);
+            nj++;
+        }
+        if (rc == 0 && qtts_dev_codec_multi(dev, nj, (const int *const *)hc, slot, tj, aj, sj) != 0) rc = -1;
+        for (int j = 0; j < nj && rc == 0; j++) {
+            const int b = bj[j];
+            codec_log_end(ctx, sj[j]);
+            if (hc[j]) {
+                cut_reference(aj[j], sj[j], vcs[b].n_ref, tj[j], &audio[b], &samples[b]);
+                aj[j] = NULL;
+            } else {
+                audio[b] = aj[j];
+                samples[b] = sj[j];
+                aj[j] = NULL;
+            }
             if (!audio[b] || samples[b] <= 0) rc = -1;
         }
+        for (int j = 0; j < nb; j++) {
+            if (hc) free(hc[j]);
+            if (aj) free(aj[j]);
+        }
+        free(hc); free(slot); free(tj); free(bj); free(aj); free(sj);
+    }
+    if (!stream) {
         ctx->perf_codec_ms = now_ms() - t_codec;
     }
     ctx->perf_total_ms = now_ms() - t_start;

@@ -82,7 +82,7 @@ EXPORTS = [
     "qtts_dev_profile_frame", "qtts_hip_hbm_bw", "qtts_dev_codec_stream_begin", "qtts_dev_codec_stream_begin_ex",
     "qtts_dev_codec_stream_prime", "qtts_dev_codec_stream_push_slot",
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
-    "qtts_dev_codec_async_end", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",
+    "qtts_dev_codec_async_end", "qtts_dev_codec_multi", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",
     "qtts_dev_encode_audio",
 ]
 

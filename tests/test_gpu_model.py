@@ -173,7 +173,8 @@ def test_batch12_self_reducing_split_k(tiny_dir, oracle):
 
 
 def test_batch_eos_slots_stop_independently(tiny_eos_dir):
-    """Slots stop at their own EOS; finished slots keep their frame count."""
+    """Slots stop at their own EOS; finished slots keep their frame count (and
+    their codec passes, of different lengths, run side by side)."""
     o = Oracle(tiny_eos_dir)
     m = qtts.QwenTTS(tiny_eos_dir)
     try:
