@@ -139,7 +139,8 @@ int qtts_dev_codec_stage_ms(const qtts_dev_t *dev, float *ms);
  * decodes its one utterance after the loop, Q.c:1376-1383, Cd.c:581-749):
  * job i decodes host_codes[i] ([T[i]][16] host ints) when host_codes and
  * host_codes[i] are non-NULL, else slot slot[i]'s first T[i] generated frames.
- * Up to QTTS_HIP_CODEC_LANES (default 4) decodes run side by side on their own
+ * Up to QTTS_HIP_CODEC_LANES (default 8; fewer when their scratch would pass
+ * 16 GB) decodes run side by side on their own
  * streams and scratch, each the same kernels as a lone decode (bit-identical
  * audio).  audio[i] (malloc'd host floats, T[i] * 1920 samples) and samples[i]
  * are filled; returns 0, or -1 with every audio[i] NULL. */

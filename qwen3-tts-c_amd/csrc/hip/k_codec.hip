@@ -1018,12 +1018,8 @@ static void *scratch_alloc(CodecModel *m, size_t bytes) {
     return p;
 }
 
-static int ensure_codec_state(CodecModel *m, int T) {
-    const qtts_dims_t &d = m->d;
-    if (T <= m->t_cap) return 0;
-    codec_free_state(m);
-    const int cap = T < 64 ? 64 : T;
-    // largest channel-major intermediate over the decoder
+// largest channel-major intermediate over the decoder at `cap` frames (elements)
+static size_t codec_buf_elems(const qtts_dims_t &d, int cap) {
     size_t L = (size_t)cap * d.ratios[0] * d.ratios[1];
     size_t mx = (size_t)d.clat * L * 4;  // ConvNeXt pw1 [L][4C]
     if ((size_t)d.cdec * L > mx) mx = (size_t)d.cdec * L;
@@ -1034,7 +1030,24 @@ static int ensure_codec_state(CodecModel *m, int T) {
         if ((size_t)C * L > mx) mx = (size_t)C * L;
     }
     const size_t lat_t = (size_t)d.clat * cap;
-    if (lat_t > mx) mx = lat_t;
+    return lat_t > mx ? lat_t : mx;
+}
+
+// device bytes of one decode state for T frames (ensure_codec_state's allocations)
+size_t codec_state_bytes(const CodecModel *m, int T) {
+    const qtts_dims_t &d = m->d;
+    const size_t cap = T < 64 ? 64 : T;
+    const size_t hid = d.chid, kvd = (size_t)d.ckv * (d.chid / d.cheads);
+    return 4 * codec_buf_elems(d, (int)cap) * 4 + cap * (4 * hid + 2 * kvd + 2 * (size_t)d.cinter + 2) * 4 +
+           ((size_t)8 << 20) * 4 + 2 * cap * (hid / d.cheads) * 4;
+}
+
+static int ensure_codec_state(CodecModel *m, int T) {
+    const qtts_dims_t &d = m->d;
+    if (T <= m->t_cap) return 0;
+    codec_free_state(m);
+    const int cap = T < 64 ? 64 : T;
+    const size_t mx = codec_buf_elems(d, cap);
     m->buf_elems = mx;
     m->bufA = (float *)scratch_alloc(m, mx * 4);
     m->bufB = (float *)scratch_alloc(m, mx * 4);

@@ -78,6 +78,7 @@ float *codec_decode(CodecModel *m, const int *codes_dev, int T, int *out_samples
 // lane i % nl (lane 0 = m, lanes[k] from codec_lane_new for k >= 1), its
 // waveform copied to dwav + dwav_off[i] (device), out_samples[i] samples;
 // returns after every lane's stream has drained
+size_t codec_state_bytes(const CodecModel *m, int T);   // one lane's scratch for T frames
 CodecModel *codec_lane_new(CodecModel *m, hipStream_t st);
 void codec_lane_delete(CodecModel *lane);
 int codec_decode_many(CodecModel *m, CodecModel *const *lanes, int nl, int n, const int *const *codes, const int *T,

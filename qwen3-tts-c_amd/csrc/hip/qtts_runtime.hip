@@ -1751,8 +1751,11 @@ extern "C" float *qtts_dev_codec_decode_host(qtts_dev_t *dv, const int *codes, i
 // Several utterances' codec passes at once (a batch's slots, run_batch): job
 // i decodes host_codes[i] (T[i] frames, [T][cq] time-major) when given, else
 // slot slot[i]'s first T[i] generated frames.  QTTS_HIP_CODEC_LANES (default
-// 4) passes run side by side (codec_decode_many); 1 decodes them one after
-// another with codec_decode.  audio[i] is malloc'd host memory.
+// 8, fewer when the extra lanes' scratch would pass 16 GB) passes run side by
+// side (codec_decode_many); 1 decodes them one after another with
+// codec_decode.  audio[i] is malloc'd host memory.  Measured (1.7B, 128
+// frames, profiles/r05lm_ab_codec_lanes.txt): a batch of 8's codec 73.4 ->
+// 60.7 ms, of 16 146.8 -> 120.0 ms (the passes are mostly conv throughput).
 extern "C" int qtts_dev_codec_multi(qtts_dev_t *dv, int n, const int *const *host_codes, const int *slot, const int *T,
                                     float **audio, int *samples) {
     if (!dv || n < 1 || !T || !audio || !samples) return -1;
@@ -1790,10 +1793,16 @@ extern "C" int qtts_dev_codec_multi(qtts_dev_t *dv, int n, const int *const *hos
         }
     }
     const char *e = getenv("QTTS_HIP_CODEC_LANES");
-    int nl = e ? atoi(e) : 4;
+    int nl = e ? atoi(e) : 8;
     if (nl < 1) nl = 1;
     if (nl > 16) nl = 16;
     if (nl > n) nl = n;
+    // the extra lanes' scratch within 16 GB (a 128-frame decode state is ~0.4 GB,
+    // a 4096-frame one ~12 GB: long EOS utterances decode on fewer lanes)
+    int tmax = 1;
+    for (int i = 0; i < n; ++i) tmax = T[i] > tmax ? T[i] : tmax;
+    const size_t per_lane = codec_state_bytes(&dv->codec, tmax);
+    while (nl > 1 && (size_t)(nl - 1) * per_lane > ((size_t)16 << 30)) --nl;
     auto fail = [&]() {
         for (int i = 0; i < n; ++i) {
             free(audio[i]);

@@ -706,18 +706,6 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
     if (stream && (qtts_dev_codec_stream_begin_ex(dev, max_tokens + sref, sref) != 0 ||
                    (sref && qtts_dev_codec_stream_prime(dev, vcs[0].ref_codes, sref) != 0)))
         goto out;
-    /* one utterance, fixed length, not streamed: the codec's exact streaming
-     * decode runs chunk by chunk on a second HIP stream behind the frames it
-     * reads (qtts_dev_codec_async_*), instead of one pass after the loop
-     * (Q.c:1376-1383); QTTS_HIP_CODEC_OVERLAP=<frames per push> (0: after the loop) */
-    int overlap = 0;
-    if (!stream && nb == 1 && fixed > 0 && !(vcs && vcs[0].ref_codes && vcs[0].n_ref > 0)) {
-        const char *e = getenv("QTTS_HIP_CODEC_OVERLAP");
-        overlap = e ? atoi(e) : 0;
-        if (overlap < 0) overlap = 0;
-        if (overlap && qtts_dev_codec_async_begin(dev, max_tokens) != 0) goto out;
-    }
-    int pushed = 0;
     double t_prefill = now_ms();
     if (qtts_dev_prefill(dev) != 0) goto out;
     double t_prefill_done = now_ms();
@@ -749,12 +737,6 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             ctx->perf_first_frame_ms = now_ms() - t_start;
         }
         if (ctx->progress_cb) ctx->progress_cb(step + 1, max_tokens, ctx->progress_cb_userdata);
-        if (overlap && (step + 1) % overlap == 0) {
-            if (qtts_dev_codec_async_push(dev, 0, pushed, step + 1 - pushed) < 0) {
-                free(sbuf); free(stopped); free(ngen); free(sstep); goto out;
-            }
-            pushed = step + 1;
-        }
         if (lagged) {   /* EOS mode: frame step is queued; stop once every slot had stopped by frame step - 1 */
             int done = 0;
             if (step >= 1 && qtts_dev_frame_done(dev, step - 1, &done) != 0) {
@@ -829,19 +811,6 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
         samples[0] = 0;
         if (ngen[0] <= 0) {
             rc = -1;
-        } else if (overlap) {
-            /* the frames after the last push, then the waveform the pushes wrote */
-            codec_log_begin(ctx, ngen[0]);
-            float *w = (float *)malloc((size_t)ngen[0] * 1920 * sizeof(float));
-            if (w && (pushed == ngen[0] || qtts_dev_codec_async_push(dev, 0, pushed, ngen[0] - pushed) >= 0) &&
-                qtts_dev_codec_async_end(dev, w, ngen[0]) == ngen[0] * 1920) {
-                audio[0] = w;
-                samples[0] = ngen[0] * 1920;
-            } else {
-                free(w);
-                rc = -1;
-            }
-            codec_log_end(ctx, samples[0]);
         } else if (vcs && vcs[0].ref_codes && vcs[0].n_ref > 0) {
             /* voice clone: decode reference ++ generated codes, keep the part
              * after the reference (qwen3_tts_model.py:612-630, same float cut) */

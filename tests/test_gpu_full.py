@@ -219,27 +219,6 @@ def test_full_batch_codec_lanes_bit_identical(full_tts, full_oracle, monkeypatch
     _audio_close(runs["8"][7], full_oracle.codec_decode(codes[7]))
 
 
-@pytest.mark.parametrize("overlap", ["16", "7"])
-def test_full_codec_overlapped_with_decode(full_tts, full_oracle, monkeypatch, overlap):
-    """QTTS_HIP_CODEC_OVERLAP: one fixed-length utterance's codec decode runs
-    as the exact streaming decode on a second stream, a push every `overlap`
-    frames behind the frames it reads (7: a remainder push after the loop).
-    Same codes; audio = the after-the-loop decode within the streaming
-    codec's fp-order bound (1e-5) and the oracle's decode within the parity
-    bar."""
-    ids = prompt_ids("p128", 1279)
-    full_tts.set_params(max_tokens=4096, fixed=40, seed=42, **DEFAULT)
-    monkeypatch.setenv("QTTS_HIP_CODEC_OVERLAP", "0")
-    base = full_tts.generate(ids, "aiden", "english")
-    codes = full_tts.last_codes()
-    monkeypatch.setenv("QTTS_HIP_CODEC_OVERLAP", overlap)
-    for _ in range(2):   # the second call reuses the stream state
-        a = full_tts.generate(ids, "aiden", "english")
-        np.testing.assert_array_equal(full_tts.last_codes(), codes)
-        assert a.shape == base.shape and np.abs(a - base).max() < 1e-5, np.abs(a - base).max()
-    _audio_close(a, full_oracle.codec_decode(codes))
-
-
 def test_full_voice_clone_b8_vs_oracle_c5(full_tts, full_oracle):
     """BASELINE C5 (1.7B voice clone, batch 8): ICL prompts of 20-34
     reference frames + x-vectors (> 64 prefill rows: the matrix-core
