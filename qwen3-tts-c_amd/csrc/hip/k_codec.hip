@@ -456,6 +456,114 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
     }
 }
 
+// The codec's plain linears (XA_ROWS x XB_WT: the transformer's projections,
+// Cd.c:267-461, and the ConvNeXt pointwise convs, Cd.c:493-507, at T / 2T / 4T
+// rows): C = A W^T, fp32 A [M][K] and W [N][K], on the bf16 matrix cores with
+// k_convb's exact split (both operands as three bf16 planes, the six products
+// with i + j <= 4; fp32-equivalent).  k_xgemm ran them at 21-34 us per
+// 128-row projection (profiles/r05o_codec_kernels.txt): one float per thread
+// per load, 32-wide K steps, each step's loads one stage ahead.  Here a
+// workgroup (4 waves of 32 x 32 on a 64 x 64 tile) takes XL_KS = 128 columns
+// of K per stage as 16 float4 loads per thread (the next stage's issued before
+// this one's MFMAs), both tiles fp32 in LDS, and each wave splits its
+// fragments in registers: 8 blocks of 16 K x 6 v_mfma_f32_32x32x16_bf16 per
+// stage, alternate blocks on two accumulators.  Split-K over blockIdx.z (K / XL_KS stages dealt evenly) with the
+// raw partials in g.part for k_xg_reduce, as k_xgemm.
+constexpr int XL_KS = 128, XL_LD = XL_KS + 4;
+
+__device__ __forceinline__ void xl_split2(float x0, float x1, uint32_t &a, uint32_t &b, uint32_t &c) {
+    a = cb_pk(x0, x1);
+    const float e0 = x0 - cb_lo(a), e1 = x1 - cb_hi(a);
+    b = cb_pk(e0, e1);
+    c = cb_pk(e0 - cb_lo(b), e1 - cb_hi(b));
+}
+__device__ __forceinline__ void xl_split8(const float4 &u, const float4 &v, bf16x8 &h1, bf16x8 &h2, bf16x8 &h3) {
+    uint4 p1, p2, p3;
+    xl_split2(u.x, u.y, p1.x, p2.x, p3.x);
+    xl_split2(u.z, u.w, p1.y, p2.y, p3.y);
+    xl_split2(v.x, v.y, p1.z, p2.z, p3.z);
+    xl_split2(v.z, v.w, p1.w, p2.w, p3.w);
+    h1 = __builtin_bit_cast(bf16x8, p1);
+    h2 = __builtin_bit_cast(bf16x8, p2);
+    h3 = __builtin_bit_cast(bf16x8, p3);
+}
+
+__global__ __launch_bounds__(256, 1) void k_xlin(XGemm g) {
+    __shared__ __attribute__((aligned(16))) float As[64 * XL_LD];
+    __shared__ __attribute__((aligned(16))) float Bs[64 * XL_LD];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    const int nz = gridDim.z, z = blockIdx.z;
+    const int nst = g.K / XL_KS;
+    const int s0 = (int)((long)nst * z / nz), s1 = (int)((long)nst * (z + 1) / nz);
+    // stage loads: element e = tid + 256 j of the 64 x 32 float4 tile: row e / 32, float4 column e % 32
+    // the stage's 16 float4 per thread as named registers (an indexed array
+    // here stayed in scratch: the compiler kept it addressable across the
+    // stage loop)
+    float4 ra0, ra1, ra2, ra3, ra4, ra5, ra6, ra7, rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7;
+    // (rows past M read row M - 1 and are zeroed when staged)
+    const int lr = tid >> 5, lc = 4 * (tid & 31);
+    auto arow = [&](int j) { const int m = m0 + lr + 8 * j; return g.A + (size_t)(m < g.M ? m : g.M - 1) * g.lda + lc; };
+    const float *pa0 = arow(0), *pa1 = arow(1), *pa2 = arow(2), *pa3 = arow(3), *pa4 = arow(4), *pa5 = arow(5),
+                *pa6 = arow(6), *pa7 = arow(7);
+    const float *pb0 = g.B + (size_t)(n0 + lr) * g.ldb + lc;
+    const size_t sb = (size_t)8 * g.ldb;
+#define XL_L1(j, k0)                                                                                       \
+    ra##j = *reinterpret_cast<const float4 *>(pa##j + (k0));                                               \
+    rb##j = *reinterpret_cast<const float4 *>(pb0 + j * sb + (k0));
+#define XL_LOAD(k0) XL_L1(0, k0) XL_L1(1, k0) XL_L1(2, k0) XL_L1(3, k0) XL_L1(4, k0) XL_L1(5, k0) XL_L1(6, k0) XL_L1(7, k0)
+#define XL_S1(j)                                                                                           \
+    *reinterpret_cast<float4 *>(As + (lr + 8 * j) * XL_LD + lc) = m0 + lr + 8 * j < g.M ? ra##j : make_float4(0.f, 0.f, 0.f, 0.f); \
+    *reinterpret_cast<float4 *>(Bs + (lr + 8 * j) * XL_LD + lc) = rb##j;
+    floatx16 acc, acc2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { acc[i] = 0.f; acc2[i] = 0.f; }
+    if (s0 < s1) { XL_LOAD(s0 * XL_KS) }
+    const int ra_row = wm + (lane & 31), rb_row = wn + (lane & 31), kh = 8 * (lane >> 5);
+    for (int s = s0; s < s1; ++s) {
+        XL_S1(0) XL_S1(1) XL_S1(2) XL_S1(3) XL_S1(4) XL_S1(5) XL_S1(6) XL_S1(7)
+        __syncthreads();
+        if (s + 1 < s1) { XL_LOAD((s + 1) * XL_KS) }
+        // two 16-K blocks per step on two accumulators, their chains
+        // interleaved (no MFMA waits on the one just issued)
+#pragma unroll
+        for (int kb = 0; kb < XL_KS; kb += 32) {
+            const float *pa = As + ra_row * XL_LD + kb + kh, *pb = Bs + rb_row * XL_LD + kb + kh;
+            bf16x8 a1, a2, a3, b1, b2, b3, c1, c2, c3, d1, d2, d3;
+            xl_split8(*reinterpret_cast<const float4 *>(pa), *reinterpret_cast<const float4 *>(pa + 4), a1, a2, a3);
+            xl_split8(*reinterpret_cast<const float4 *>(pb), *reinterpret_cast<const float4 *>(pb + 4), b1, b2, b3);
+            xl_split8(*reinterpret_cast<const float4 *>(pa + 16), *reinterpret_cast<const float4 *>(pa + 20), c1, c2, c3);
+            xl_split8(*reinterpret_cast<const float4 *>(pb + 16), *reinterpret_cast<const float4 *>(pb + 20), d1, d2, d3);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d3, acc2, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c2, d2, acc2, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c3, d1, acc2, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d2, acc2, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c2, d1, acc2, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, d1, acc2, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    acc += acc2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m = m0 + wm + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn + (lane & 31);
+        if (m >= g.M) continue;
+        if (nz > 1) g.part[((size_t)z * g.M + m) * g.N + n] = acc[i];
+        else xg_epi(g, m, n, acc[i]);
+    }
+#undef XL_LOAD
+#undef XL_L1
+#undef XL_S1
+}
+
 // w (fp32, n elements) -> three exact bf16 planes at planes[p * n + i]
 __global__ void k_wt_split(const float *w, size_t n, unsigned short *planes) {
     const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 2;
@@ -750,6 +858,8 @@ static int conv_launch(const XGemm &gin, int nph, hipStream_t st) {
     const bool bf = !g.sa || g.K / g.Kw / (g.kz > 1 ? g.kz : 1) <= CB_SNAKE_MAX;
     if (bf) {
         // 256-column tiles where the grid still holds >= 2 workgroups per CU
+        // (the two column blocks' MFMA chains interleaved measured the same:
+        // codec 7.9 ms per 128 frames either way, profiles/r05st_ab_codec.txt)
         const int tiles4 = ((g.N + 255) / 256) * cg.y * cg.z;
         if (tiles4 >= 512) {
             const dim3 c4((g.N + 255) / 256, cg.y, cg.z);
@@ -788,8 +898,34 @@ static bool xgemv_ok(const XGemm &g) {
            g.ldb % 4 == 0 && ((uintptr_t)g.B & 15) == 0 && (size_t)4 * g.K * 4 + 512 <= 64 * 1024;
 }
 
+// k_xlin covers plain fp32 linears above k_xgemv's 4 rows with 16-B rows
+static bool xlin_ok(const XGemm &g) {
+    return g.amode == XA_ROWS && g.bmode == XB_WT && g.M > 4 && g.N % 64 == 0 && g.K % XL_KS == 0 &&
+           g.lda % 4 == 0 && g.ldb % 4 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.B & 15) == 0;
+}
+
 int qtts_xgemm(const XGemm &g, hipStream_t st) {
     if (g.M <= 0 || g.N <= 0 || g.K <= 0) return 0;
+    static const bool xl_on = [] { const char *e = getenv("QTTS_HIP_XLIN"); return !(e && !atoi(e)); }();
+    if (xl_on && xlin_ok(g)) {
+        dim3 grid(g.N / 64, (g.M + 63) / 64, 1);
+        // split-K where the tiles would not fill the chip: >= 1 stage each,
+        // partials within the workspace
+        const int tiles = grid.x * grid.y, nst = g.K / XL_KS;
+        int nz = 1;
+        if (g.part && tiles < 256) {
+            nz = (256 + tiles - 1) / tiles;
+            if (nz > nst) nz = nst;
+            while (nz > 1 && (size_t)nz * g.M * g.N > g.part_elems) --nz;
+        }
+        grid.z = nz;
+        hipLaunchKernelGGL(k_xlin, grid, dim3(256), 0, st, g);
+        if (nz > 1) {
+            const size_t n = (size_t)g.M * g.N;
+            hipLaunchKernelGGL(k_xg_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, nz);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (xgemv_ok(g)) {
         int ks = 1;   // KSPLIT: grid >= 512 workgroups, >= 1 block per lane
         while (ks < 32 && (g.N + 32 / ks - 1) / (32 / ks) < 512 && g.K / 32 / (2 * ks) >= 1) ks *= 2;
