@@ -1477,10 +1477,17 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
         // 6 merged; k_gemvb: 2 = MFMAs done, 3 = after the final barrier,
         // 4 = after the epilogue stores, 5 = tiles summed, 6 = normalised)
         static const char *ph[7] = {"start", "x staged", "dot done", "epilogue", "pf landed", "w issued", "merged"};
+        unsigned long long tq = 0;   // the first launch's first start: the launch offsets below
         for (int g = 0; g < 4; ++g) {
             const unsigned long long *b = h.data() + (size_t)g * 2048 * 8;
-            unsigned long long t0 = ~0ull;
+            unsigned long long t0 = ~0ull, tend = 0;
             for (int i = 0; i < 2048; ++i) if (b[i * 8] && b[i * 8] < t0) t0 = b[i * 8];
+            for (int i = 0; i < 2048 * 8; ++i) if (b[i] > tend) tend = b[i];
+            if (t0 != ~0ull) {
+                if (!tq) tq = t0;
+                fprintf(stderr, "[gm_dbg] %-8s launch at %7.2f us after the first, last stamp %6.2f us into it\n", op[g],
+                        (t0 - tq) * 0.01, (tend - t0) * 0.01);
+            }
             for (int k = 0; k < 7; ++k) {
                 std::vector<double> v;
                 for (int i = 0; i < 2048; ++i) if (b[i * 8 + k]) v.push_back((b[i * 8 + k] - t0) * 0.01);
