@@ -4,7 +4,9 @@
 # voice-clone batch bench (prefill GEMM, batch decode GEMV, codec convs), then
 # the bench line itself -- after the summaries are in the box's profiles/ so
 # the line's roofline.rocprof_avg_us / traffic come from the same code.
-# Usage (via gpurun): bash tools/gpu_round.sh <tag> [all|core|prof|extra|dist]
+# Usage (via gpurun): bash tools/gpu_round.sh <tag> [all|core|prof|prof1|vc|extra|batch|dist]
+#   prof1 = the profiles and the 1.7B / 0.6B bench lines only (no tests)
+#   vc    = the C5 line, the encoders and the MFMA pass only
 #   core  = tests + profiles + the 1.7B and 0.6B (C2) bench lines (fits one call)
 #   extra = C5 voice clone batch 8, batch 8 / 16 lines, encoders, MFMA pass
 set -eo pipefail
@@ -60,7 +62,7 @@ if [ "$MODE" = all ] || [ "$MODE" = core ]; then
   # 1 = some test failed (keep measuring); anything else (timeout, abort, crash) ends the call
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests rc=$rc"; exit $rc; fi
 fi
-if [ "$MODE" != extra ]; then
+if [ "$MODE" != extra ] && [ "$MODE" != vc ]; then
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch.log 2>&1
@@ -82,7 +84,7 @@ timeout -k 10 900 python bench.py --preset 0.6b --greedy --no-cpu-1thread > $O/b
 cp $O/bench_06b.json $R/profiles/${TAG}_bench_06b.json
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
 fi
-[ "$MODE" = core ] && { echo done; exit 0; }
+{ [ "$MODE" = core ] || [ "$MODE" = prof1 ]; } && { echo done; exit 0; }
 # BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8
 timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 > $O/bench_vc8.json 2> $O/bench_vc8.err
 cp $O/bench_vc8.json $R/profiles/${TAG}_bench_vc8.json
