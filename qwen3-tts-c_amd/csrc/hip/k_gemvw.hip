@@ -69,6 +69,9 @@ __device__ __forceinline__ void gw_stamp(const GemvArgs &a, int k) {
 // s_load meanwhile).
 enum { GW_SRC_X = 0, GW_SRC_TAB = 1, GW_SRC_TABF = 2, GW_SRC_ROWSEL = 4 };
 
+#ifndef QTTS_GW_WSD
+#define QTTS_GW_WSD 2   // the talker shapes issue RW / QTTS_GW_WSD weight rows before x is staged (2. below)
+#endif
 template <int RW, int NV, bool NT, int AM_MS = 0>
 __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W, const int *ids, int src_kind,
                                                GemvArgs a) {
@@ -153,10 +156,25 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
 #ifdef QTTS_STAMPS
     if (a.dbg_xfirst) __builtin_amdgcn_s_waitcnt(0);   // (diagnostics: x alone, no weight traffic behind it)
 #endif
-    // 2. the whole weight slice of this lane in flight
+    // 2. the weight slice of this lane in flight -- for the talker's HBM
+    //    shapes only its first RW1 rows here, the rest once x is staged: x is
+    //    an L2 / Infinity-Cache read, but it queues behind every weight request
+    //    the chip's workgroups issued before it (in-graph stamps, the 1.7B
+    //    gate|up: x lands 3.1-8.1 us into the launch behind the 50 MB stream,
+    //    profiles/r05v_talker_layer_stamps.txt).  Half the rows first: x
+    //    staged 2.5 -> 1.1 us (q|k|v), 3.7 -> 1.8 (down), 5.8 -> 4.4 (gate|up),
+    //    +1.7 % audio-s/s in 4 alternating rounds; a third first, or the split
+    //    for the sub-talker's Infinity-Cache shapes too, gave it back
+    //    (profiles/r05wx_ab_split_issue.txt)
+#if defined(QTTS_GW_WS_AM)
+    constexpr bool WS = NT && RW >= 2;   // (A/B build: the O projection with the attention merge too)
+#else
+    constexpr bool WS = NT && !AM && RW >= 2;
+#endif
+    constexpr int RW1 = WS ? (RW / QTTS_GW_WSD > 0 ? RW / QTTS_GW_WSD : 1) : RW;
     v4u wv[RW][NV];
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
+    for (int i = 0; i < RW1; ++i) {
         const v4u *p = reinterpret_cast<const v4u *>(W + (size_t)(row0 + w + 4 * i) * C) + lane;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
@@ -257,6 +275,17 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
         }
     }
     __syncthreads();
+    if constexpr (WS) {   // the rest of the slice (2. above)
+#pragma unroll
+        for (int i = RW1; i < RW; ++i) {
+            const v4u *p = reinterpret_cast<const v4u *>(W + (size_t)(row0 + w + 4 * i) * C) + lane;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                if constexpr (NT) wv[i][k] = __builtin_nontemporal_load(p + 64 * k);
+                else wv[i][k] = p[64 * k];
+            }
+        }
+    }
 
     // 4. one wave per row: the lane's chunks in order, then the wave sum
     float acc[RW];
