@@ -166,11 +166,9 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
     //    +1.7 % audio-s/s in 4 alternating rounds; a third first, or the split
     //    for the sub-talker's Infinity-Cache shapes too, gave it back
     //    (profiles/r05wx_ab_split_issue.txt)
-#if defined(QTTS_GW_WS_AM)
-    constexpr bool WS = NT && RW >= 2;   // (A/B build: the O projection with the attention merge too)
-#else
+    // (the O projection with the attention merge in its prologue keeps every
+    // row first: split, 33.25-33.46 vs 33.76-33.94 audio-s/s)
     constexpr bool WS = NT && !AM && RW >= 2;
-#endif
     constexpr int RW1 = WS ? (RW / QTTS_GW_WSD > 0 ? RW / QTTS_GW_WSD : 1) : RW;
     v4u wv[RW][NV];
 #pragma unroll
