@@ -89,6 +89,8 @@ __global__ __launch_bounds__(1024) void k_gemvb(const void *src, const int *ids,
     // (also every step of the partial-free SPW 4 / 8 shapes -- the talker's --
     // measured slower: batch 8 150.4-150.7 vs 152.0-152.6, batch 16 237.2 vs
     // 238.5, profiles/r05f_ab_batch_allw.txt)
+    // (a quarter of the talker shapes' steps first measured slower too: batch 8
+    // 155.6-155.7 vs 157.2-157.8, profiles/r05aa_ab_batch_steps_first.txt)
     constexpr int SA = SPW <= 2 ? SPW : (SPW + 1) / 2;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
     const int nb = a.nb;
