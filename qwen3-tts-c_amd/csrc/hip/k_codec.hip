@@ -335,7 +335,7 @@ __device__ __forceinline__ void cb_split8(const float (&v)[8], uint4 &p1, uint4 
 
 // WN waves along t (2 or 4): a 64 x 64*WN tile per workgroup of 128*WN
 // threads; the staged weights serve WN waves per 32-row half.
-template <int KW, int WN, bool DB>
+template <int KW, int WN>
 __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
     constexpr int NT = 128 * WN, BNT = 64 * WN;
     const int nzk = g.kz > 1 ? g.kz : 1, ph = blockIdx.z / nzk, kzi = blockIdx.z - ph * nzk;
@@ -347,11 +347,8 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
     constexpr int NA = 3 * KW * CV_BM * 2;                   // 16-B weight items per stage
     constexpr int NAT = (NA + NT - 1) / NT;
     constexpr int NBT = (2 * NBW + NT - 1) / NT;             // (half, column) input items per thread
-    // DB: two stage buffers -- stage s + 1 is split and written while stage
-    // s's MFMAs run (one barrier per stage instead of two)
-    constexpr int NBUF = DB ? 2 : 1, ASZ = 3 * KW * CV_BM * 16, BSZ = 3 * NBW * 16;
-    __shared__ __attribute__((aligned(16))) unsigned short As[NBUF * ASZ];
-    __shared__ __attribute__((aligned(16))) unsigned short Bs[NBUF * BSZ];
+    __shared__ __attribute__((aligned(16))) unsigned short As[3 * KW * CV_BM * 16];
+    __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * NBW * 16];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int m0 = blockIdx.y * CV_BM, n0 = blockIdx.x * BNT;
     const int wm = (wave / WN) * 32, wn = (wave % WN) * 64;
@@ -392,16 +389,13 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
         __syncthreads();
     }
     const int r = lane & 31, hh = lane >> 5;
-    // stage c0s (its loads in ra / rb) -> LDS buffer buf: the weight planes as
-    // they are, the input window SnakeBeta'd and split into three planes
-    auto stage = [&](int c0s, int buf) {
-        unsigned short *as = As + buf * ASZ, *bs = Bs + buf * BSZ;
+    for (int c0 = cbeg; c0 < cend; c0 += CV_BC) {
 #pragma unroll
         for (int j = 0; j < NAT; ++j) {
             const int e = tid + NT * j;
             if (e < NA) {
                 const int pt = e / (CV_BM * 2), m = (e >> 1) % CV_BM, h = e & 1;   // pt = plane * KW + tap
-                *reinterpret_cast<uint4 *>(&as[pt * CV_BM * 16 + cb_swz(m, h)]) = ra[j];
+                *reinterpret_cast<uint4 *>(&As[pt * CV_BM * 16 + cb_swz(m, h)]) = ra[j];
             }
         }
 #pragma unroll
@@ -409,33 +403,32 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
             const int e = tid + NT * j, h = e / NBW, x = e - h * NBW;
             if (h < 2) {
                 if (snake) {
-                    const int cl = c0s - cbeg + 8 * h;
+                    const int cl = c0 - cbeg + 8 * h;
 #pragma unroll
                     for (int q = 0; q < 8; ++q) rb[j][q] = snake1(rb[j][q], Ssa[cl + q], Ssb[cl + q]);
                 }
                 uint4 p1, p2, p3;
                 cb_split8(rb[j], p1, p2, p3);
                 const int o = cb_swz(x, h);
-                *reinterpret_cast<uint4 *>(&bs[o]) = p1;
-                *reinterpret_cast<uint4 *>(&bs[NBW * 16 + o]) = p2;
-                *reinterpret_cast<uint4 *>(&bs[2 * NBW * 16 + o]) = p3;
+                *reinterpret_cast<uint4 *>(&Bs[o]) = p1;
+                *reinterpret_cast<uint4 *>(&Bs[NBW * 16 + o]) = p2;
+                *reinterpret_cast<uint4 *>(&Bs[2 * NBW * 16 + o]) = p3;
             }
         }
-    };
-    auto compute = [&](int buf) {
-        const unsigned short *as = As + buf * ASZ, *bs = Bs + buf * BSZ;
+        __syncthreads();
+        if (c0 + CV_BC < cend) load(c0 + CV_BC);
 #pragma unroll
         for (int tap = 0; tap < KW; ++tap) {
             const int sh = tap * dil, oa = cb_swz(wm + r, hh);
-            const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(&as[(0 * KW + tap) * CV_BM * 16 + oa]);
-            const bf16x8 a2 = *reinterpret_cast<const bf16x8 *>(&as[(1 * KW + tap) * CV_BM * 16 + oa]);
-            const bf16x8 a3 = *reinterpret_cast<const bf16x8 *>(&as[(2 * KW + tap) * CV_BM * 16 + oa]);
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(&As[(0 * KW + tap) * CV_BM * 16 + oa]);
+            const bf16x8 a2 = *reinterpret_cast<const bf16x8 *>(&As[(1 * KW + tap) * CV_BM * 16 + oa]);
+            const bf16x8 a3 = *reinterpret_cast<const bf16x8 *>(&As[(2 * KW + tap) * CV_BM * 16 + oa]);
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
                 const int ob = cb_swz(wn + 32 * nb + r + sh, hh);
-                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(&bs[ob]);
-                const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(&bs[NBW * 16 + ob]);
-                const bf16x8 b3 = *reinterpret_cast<const bf16x8 *>(&bs[2 * NBW * 16 + ob]);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(&Bs[ob]);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(&Bs[NBW * 16 + ob]);
+                const bf16x8 b3 = *reinterpret_cast<const bf16x8 *>(&Bs[2 * NBW * 16 + ob]);
                 floatx16 &acc = nb ? acc1 : acc0;
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc, 0, 0, 0);
@@ -445,27 +438,7 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
             }
         }
-    };
-    if constexpr (DB) {
-        stage(cbeg, 0);
         __syncthreads();
-        int buf = 0;
-        for (int c0 = cbeg; c0 < cend; c0 += CV_BC) {
-            const bool more = c0 + CV_BC < cend;
-            if (more) load(c0 + CV_BC);
-            compute(buf);
-            if (more) stage(c0 + CV_BC, buf ^ 1);
-            __syncthreads();
-            buf ^= 1;
-        }
-    } else {
-        for (int c0 = cbeg; c0 < cend; c0 += CV_BC) {
-            stage(c0, 0);
-            __syncthreads();
-            if (c0 + CV_BC < cend) load(c0 + CV_BC);
-            compute(0);
-            __syncthreads();
-        }
     }
     float *pz = nzk > 1 ? g.part + (size_t)blockIdx.z * g.M * g.N : nullptr;
 #pragma unroll
@@ -887,32 +860,23 @@ static int conv_launch(const XGemm &gin, int nph, hipStream_t st) {
         // 256-column tiles where the grid still holds >= 2 workgroups per CU
         // (the two column blocks' MFMA chains interleaved measured the same:
         // codec 7.9 ms per 128 frames either way, profiles/r05st_ab_codec.txt)
-        // QTTS_HIP_CONV_DB: 0 one stage buffer, two barriers per stage; 1 two
-        // buffers everywhere; 2 two buffers where they keep the occupancy
-        // (k_convb<7, 4>: LDS 86 -> 160 KB, one workgroup per CU either way)
-        static const int dbm = [] { const char *e = getenv("QTTS_HIP_CONV_DB"); return e ? atoi(e) : 0; }();
         const int tiles4 = ((g.N + 255) / 256) * cg.y * cg.z;
-#define QTTS_CB(KW_, WN_, G_, T_)                                                                      \
-        if (dbm == 1 || (dbm == 2 && KW_ == 7 && WN_ == 4))                                          \
-            hipLaunchKernelGGL((k_convb<KW_, WN_, true>), G_, dim3(T_), 0, st, g);                   \
-        else hipLaunchKernelGGL((k_convb<KW_, WN_, false>), G_, dim3(T_), 0, st, g);
         if (tiles4 >= 512) {
             const dim3 c4((g.N + 255) / 256, cg.y, cg.z);
             switch (g.Kw) {
-                case 7: QTTS_CB(7, 4, c4, 512) break;
-                case 3: QTTS_CB(3, 4, c4, 512) break;
-                case 2: QTTS_CB(2, 4, c4, 512) break;
-                default: QTTS_CB(1, 4, c4, 512) break;
+                case 7: hipLaunchKernelGGL((k_convb<7, 4>), c4, dim3(512), 0, st, g); break;
+                case 3: hipLaunchKernelGGL((k_convb<3, 4>), c4, dim3(512), 0, st, g); break;
+                case 2: hipLaunchKernelGGL((k_convb<2, 4>), c4, dim3(512), 0, st, g); break;
+                default: hipLaunchKernelGGL((k_convb<1, 4>), c4, dim3(512), 0, st, g); break;
             }
         } else {
             switch (g.Kw) {
-                case 7: QTTS_CB(7, 2, cg, 256) break;
-                case 3: QTTS_CB(3, 2, cg, 256) break;
-                case 2: QTTS_CB(2, 2, cg, 256) break;
-                default: QTTS_CB(1, 2, cg, 256) break;
+                case 7: hipLaunchKernelGGL((k_convb<7, 2>), cg, dim3(256), 0, st, g); break;
+                case 3: hipLaunchKernelGGL((k_convb<3, 2>), cg, dim3(256), 0, st, g); break;
+                case 2: hipLaunchKernelGGL((k_convb<2, 2>), cg, dim3(256), 0, st, g); break;
+                default: hipLaunchKernelGGL((k_convb<1, 2>), cg, dim3(256), 0, st, g); break;
             }
         }
-#undef QTTS_CB
     } else {
         switch (g.Kw) {
             case 7: hipLaunchKernelGGL(k_conv<7>, cg, dim3(256), 0, st, g); break;
