@@ -768,10 +768,15 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
         c.y = a.y + (size_t)r0 * ys;
         c.nb = nr;
         int rc = 1;
-        // <= 16 rows (a custom-voice prompt): the batch decode kernel (k_gemvm,
-        // x split once per workgroup, ~1 round over the CUs) streams the
-        // weights faster than the 64-row prefill GEMM
-        if (nr >= 2 && nr <= 16) rc = qtts_gemvm(c, dv->st);
+        // <= 16 rows (a custom-voice prompt): the batch decode kernels (k_gemvb,
+        // x sliced per wave, else k_gemvm, x split once per workgroup; ~1
+        // round over the CUs) stream the weights faster than the 64-row
+        // prefill GEMM.  (QTTS_HIP_PREFILL_GEMVB=0: k_gemvm only, the round-4
+        // path: 72 us of prefill per talker layer at the P128 prompt's rows,
+        // profiles/r05af_first_packet.txt)
+        static const bool pgb = [] { const char *e = getenv("QTTS_HIP_PREFILL_GEMVB"); return !(e && !atoi(e)); }();
+        if (nr >= 2 && nr <= 16 && pgb) rc = qtts_gemvb(c, dv->st);
+        if (rc == 1 && nr >= 2 && nr <= 16) rc = qtts_gemvm(c, dv->st);
         if (rc == 1 && nr >= 2) rc = qtts_mgemm(c, dv->pinv, dv->st);
         if (rc < 0) return -1;
         if (rc == 1) {
