@@ -168,7 +168,9 @@ __global__ __launch_bounds__(256) void k_gemvw(const void *src, const bf16_t *W,
     //    (profiles/r05wx_ab_split_issue.txt)
     // (the O projection with the attention merge in its prologue keeps every
     // row first: split, 33.25-33.46 vs 33.76-33.94 audio-s/s)
-    constexpr bool WS = NT && !AM && RW >= 2;
+    // (and the 0.6B talker's 1024-wide rows keep every row first: split,
+    // C2 38.33-38.52 vs 38.45-38.54 audio-s/s, profiles/r05wx_ab_split_issue.txt)
+    constexpr bool WS = NT && !AM && RW >= 2 && NV >= 4;
     constexpr int RW1 = WS ? (RW / QTTS_GW_WSD > 0 ? RW / QTTS_GW_WSD : 1) : RW;
     v4u wv[RW][NV];
 #pragma unroll
