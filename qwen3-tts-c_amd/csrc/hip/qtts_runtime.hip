@@ -114,6 +114,7 @@ struct qtts_dev {
     // batch split-K (nb >= 2): second talker residual, O / down partials; the
     // talker's final residual = tk_xfin + sum of tk_npend partials at tk_pend
     float *x_tk2 = nullptr, *bpo = nullptr, *bpd = nullptr;
+    float *ppart = nullptr;      // prefill split-K partials (<= 16 rows, kz <= 4)
     float *tk_xfin = nullptr;
     const float *tk_pend = nullptr;
     int tk_npend = 0;
@@ -606,6 +607,7 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     A(x_tk2, float, B * d.H);
     A(bpo, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
     A(bpd, float, (size_t)4 * B * (d.H > d.Hs ? d.H : d.Hs));
+    A(ppart, float, (size_t)4 * 16 * (d.H > d.Hs ? d.H : d.Hs));
     A(opart, float, (size_t)B * ((size_t)d.KVs * d.Hs > (size_t)d.KV * d.H ? (size_t)d.KVs * d.Hs : (size_t)d.KV * d.H));
     A(qkv_s, float, B * dv->QKVs());
     A(att_s, float, B * d.NHs * d.HDs);
@@ -775,7 +777,17 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
         // path: 72 us of prefill per talker layer at the P128 prompt's rows,
         // profiles/r05af_first_packet.txt)
         static const bool pgb = [] { const char *e = getenv("QTTS_HIP_PREFILL_GEMVB"); return !(e && !atoi(e)); }();
-        if (nr >= 2 && nr <= 16 && pgb) rc = qtts_gemvb(c, dv->st);
+        // the residual projections (O, down: R / 16 row tiles, too few for
+        // the chip) split over K in two columns that reduce their own
+        // partials, as the talker's decode does (QTTS_HIP_PREFILL_SPLIT=0: none)
+        static const bool psk = [] { const char *e = getenv("QTTS_HIP_PREFILL_SPLIT"); return !(e && !atoi(e)); }();
+        if (nr >= 2 && nr <= 16 && pgb && psk && c.epi == EPI_RESID && !c.norm_w && c.R / 16 < 256 &&
+            c.C % 64 == 0 && c.R <= (dv->d.H > dv->d.Hs ? dv->d.H : dv->d.Hs)) {
+            GemvArgs k = c;
+            k.ypart = dv->ppart; k.kz = 2; k.ld_ypart = (size_t)nr * k.R; k.tick = dv->btick;
+            rc = qtts_gemvb(k, dv->st);
+        }
+        if (rc == 1 && nr >= 2 && nr <= 16 && pgb) rc = qtts_gemvb(c, dv->st);
         if (rc == 1 && nr >= 2 && nr <= 16) rc = qtts_gemvm(c, dv->st);
         if (rc == 1 && nr >= 2) rc = qtts_mgemm(c, dv->pinv, dv->st);
         if (rc < 0) return -1;
