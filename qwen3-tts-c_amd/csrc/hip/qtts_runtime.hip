@@ -779,12 +779,14 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
         static const bool pgb = [] { const char *e = getenv("QTTS_HIP_PREFILL_GEMVB"); return !(e && !atoi(e)); }();
         // the residual projections (O, down: R / 16 row tiles, too few for
         // the chip) split over K in two columns that reduce their own
-        // partials, as the talker's decode does (QTTS_HIP_PREFILL_SPLIT=0: none)
-        static const bool psk = [] { const char *e = getenv("QTTS_HIP_PREFILL_SPLIT"); return !(e && !atoi(e)); }();
+        // partials, as the talker's decode does (QTTS_HIP_PREFILL_SPLIT=kz,
+        // 2 or 4; 0: none)
+        static const int psk = [] { const char *e = getenv("QTTS_HIP_PREFILL_SPLIT");
+                                    int v = e ? atoi(e) : 2; return v == 4 ? 4 : v ? 2 : 0; }();
         if (nr >= 2 && nr <= 16 && pgb && psk && c.epi == EPI_RESID && !c.norm_w && c.R / 16 < 256 &&
-            c.C % 64 == 0 && c.R <= (dv->d.H > dv->d.Hs ? dv->d.H : dv->d.Hs)) {
+            c.C % (32 * psk) == 0 && c.R <= (dv->d.H > dv->d.Hs ? dv->d.H : dv->d.Hs)) {
             GemvArgs k = c;
-            k.ypart = dv->ppart; k.kz = 2; k.ld_ypart = (size_t)nr * k.R; k.tick = dv->btick;
+            k.ypart = dv->ppart; k.kz = psk; k.ld_ypart = (size_t)nr * k.R; k.tick = dv->btick;
             rc = qtts_gemvb(k, dv->st);
         }
         if (rc == 1 && nr >= 2 && nr <= 16 && pgb) rc = qtts_gemvb(c, dv->st);
