@@ -633,7 +633,10 @@ def main():
         }
         if fp:
             out["first_packet_ms"] = round(fp["first_packet_ms"], 2)
-        out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in (fp or phases).items()}
+        # batch 1: the first-packet request's fields, then the last timed step's
+        # phases as step_*; a batch: the phases
+        det = dict(fp, **{"step_" + k: v for k, v in phases.items()}) if fp else phases
+        out["detail"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in det.items()}
         out["ranks"] = ranks
         if enc:
             out["ref_audio_encode"] = enc

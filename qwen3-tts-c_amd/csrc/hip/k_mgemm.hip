@@ -14,6 +14,10 @@
 // Mapping: one workgroup = 16 weight rows (the MFMA N side) x all M rows
 // (up to 4 tiles of 16 on the MFMA M side); the four waves take K steps of 32
 // round-robin, then reduce their partial tiles through LDS in wave order.
+// Grids under 1024 workgroups split K over grid.z (partials to scratch,
+// summed in column order with the epilogue by k_mgemm_reduce): at one
+// workgroup per CU each SIMD holds one wave, which waits out every K step's
+// loads alone.
 // Lane l of a wave loads W[row l&15][k0 + 8(l>>4) .. +7] (one 16 B load) and
 // x[t = l&15][same k] (two float4), which are exactly the B and A operand
 // fragments of mfma_f32_16x16x32_bf16 (cdna_hip_programming.md section 3).
@@ -51,8 +55,11 @@ __global__ __launch_bounds__(256) void k_row_rms(const float *x, int ldx, int C,
 // activation re-reads from L2, R/16 per chunk at NW = 1, bound the > 64-row
 // case.  Per-wave K partition and the in-order wave reduction are those of
 // NW = 1, so the results are bit-identical.
+// part != nullptr (split-K, grid.z = kz column groups of C): workgroup z
+// covers K steps [z nsz, (z+1) nsz), its waves round-robin inside them, and
+// it stores the raw tile sums to part[z][row][R] for k_mgemm_reduce.
 template <int MT, int NW>
-__global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
+__global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv, float *part) {
     __shared__ floatx4 red[4][MT][NW][64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r0 = blockIdx.x * 16 * NW;
@@ -76,9 +83,9 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[mt][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int nsteps = C / 32;
-    for (int s = w; s < nsteps; s += 4) {
-        const int k0 = 32 * s;
+    const int nsz = C / 32 / gridDim.z, sz0 = blockIdx.z * nsz;
+    for (int s = w; s < nsz; s += 4) {
+        const int k0 = 32 * (sz0 + s);
         bf16x8 bw[NW];
 #pragma unroll
         for (int n = 0; n < NW; ++n) bw[n] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const v4u *>(wr[n] + k0));
@@ -147,6 +154,15 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
         floatx4 v = red[0][mt][n][lane];
         for (int ww = 1; ww < 4; ++ww) v += red[ww][mt][n][lane];
         const int r = r0 + 16 * n + rl;   // C/D: col = lane & 15 (weight row), row = (lane >> 4) * 4 + i (token)
+        if (part) {
+            float *pz = part + ((size_t)blockIdx.z * a.nb + t0) * a.R;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int t = mt * 16 + (lane >> 4) * 4 + i;
+                if (t < M && r < a.R) pz[(size_t)t * a.R + r] = v[i];
+            }
+            continue;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int t = mt * 16 + (lane >> 4) * 4 + i;
@@ -171,13 +187,43 @@ __global__ __launch_bounds__(256) void k_mgemm(GemvArgs a, const float *inv) {
     }
 }
 
+// split-K tail: y[row] = epilogue(sum over z of part[z][row], z in order);
+// grid (outputs / 256, rows)
+__global__ __launch_bounds__(256) void k_mgemm_reduce(GemvArgs a, const float *part, int kz) {
+    const int t = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+    const int nout = a.epi == EPI_SWIGLU ? a.R / 2 : a.R;
+    if (j >= nout) return;
+    const size_t zs = (size_t)a.nb * a.R;
+    const float *p = part + (size_t)t * a.R;
+    float *yr = a.y + (size_t)t * a.ldy;
+    if (a.epi == EPI_SWIGLU) {
+        const int g = (j >> 2) * 8 + (j & 3);
+        float vg = p[g], vu = p[g + 4];
+        for (int z = 1; z < kz; ++z) { vg += p[z * zs + g]; vu += p[z * zs + g + 4]; }
+        yr[j] = (vg / (1.0f + expf(-vg))) * vu;
+        return;
+    }
+    float val = p[j];
+    for (int z = 1; z < kz; ++z) val += p[z * zs + j];
+    switch (a.epi) {
+        case EPI_STORE: yr[j] = val; break;
+        case EPI_BIAS: yr[j] = val + a.bias[j]; break;
+        case EPI_BIAS_SILU: {
+            const float z = val + a.bias[j];
+            yr[j] = z / (1.0f + expf(-z));
+            break;
+        }
+        case EPI_RESID: yr[j] += val; break;
+    }
+}
+
 }  // namespace
 
 // Multi-row projection on the matrix cores, any number of rows (64-row chunks
 // on grid.y of one launch).  `inv_scratch` (>= nb floats) receives the
 // per-row 1/rms when a.norm_w is set.  Returns 1 when the shape is not
 // covered (caller uses qtts_gemv), 0 ok, -1 error.
-int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st) {
+int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st, float *part, size_t part_elems) {
     if (a.nb < 2 || a.C % 32 || a.R % 16 || a.xcopy || a.table_f32 || (a.norm_w && !inv_scratch) ||
         (a.table && a.norm_w) || (!a.table && (a.ldx % 4 || ((uintptr_t)a.x & 15))) || (a.C % 8))
         return 1;
@@ -185,13 +231,29 @@ int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st) {
     const int nch = (a.nb + 63) / 64;
     // > 64 rows: widest weight tile group that still gives >= 256 workgroups
     const int nw = nch < 2 || a.R % 64 ? 1 : a.R / 64 * nch >= 256 ? 4 : a.R % 32 == 0 && a.R / 32 * nch >= 256 ? 2 : 1;
-    const dim3 grid(a.R / (16 * nw), nch);
-    if (nw == 4) hipLaunchKernelGGL((k_mgemm<4, 4>), grid, dim3(256), 0, st, a, inv_scratch);
-    else if (nw == 2) hipLaunchKernelGGL((k_mgemm<4, 2>), grid, dim3(256), 0, st, a, inv_scratch);
-    else if (a.nb <= 16) hipLaunchKernelGGL((k_mgemm<1, 1>), grid, dim3(256), 0, st, a, inv_scratch);
-    else if (a.nb <= 32) hipLaunchKernelGGL((k_mgemm<2, 1>), grid, dim3(256), 0, st, a, inv_scratch);
-    else hipLaunchKernelGGL((k_mgemm<4, 1>), grid, dim3(256), 0, st, a, inv_scratch);
+    // split-K over grid.z while the grid is under 1024 workgroups (one
+    // workgroup per CU leaves one wave per SIMD to wait out every K step's
+    // loads alone), each column group >= 8 K steps per wave pair
+    // (QTTS_HIP_MGEMM_KZ: 1 = no split, n = at most n columns)
+    static const int kzmax = [] { const char *e = getenv("QTTS_HIP_MGEMM_KZ"); const int v = e ? atoi(e) : 8;
+                                  return v >= 1 && v <= 16 ? v : 8; }();
+    int kz = 1;
+    const int wgs = a.R / (16 * nw) * nch;
+    while (part && 2 * kz <= kzmax && wgs * 2 * kz <= 1024 && a.C % (32 * 2 * kz) == 0 &&
+           a.C / 32 / (2 * kz) >= 8 && (size_t)2 * kz * a.nb * a.R <= part_elems)
+        kz *= 2;
+    float *pt = kz > 1 ? part : nullptr;
+    const dim3 grid(a.R / (16 * nw), nch, kz);
+    if (nw == 4) hipLaunchKernelGGL((k_mgemm<4, 4>), grid, dim3(256), 0, st, a, inv_scratch, pt);
+    else if (nw == 2) hipLaunchKernelGGL((k_mgemm<4, 2>), grid, dim3(256), 0, st, a, inv_scratch, pt);
+    else if (a.nb <= 16) hipLaunchKernelGGL((k_mgemm<1, 1>), grid, dim3(256), 0, st, a, inv_scratch, pt);
+    else if (a.nb <= 32) hipLaunchKernelGGL((k_mgemm<2, 1>), grid, dim3(256), 0, st, a, inv_scratch, pt);
+    else hipLaunchKernelGGL((k_mgemm<4, 1>), grid, dim3(256), 0, st, a, inv_scratch, pt);
     qtts_last_kernel = nw == 4 ? "k_mgemm<4,4>" : nw == 2 ? "k_mgemm<4,2>"
                      : a.nb <= 16 ? "k_mgemm<1>" : a.nb <= 32 ? "k_mgemm<2>" : "k_mgemm<4>";
+    if (kz > 1) {
+        const int nout = a.epi == EPI_SWIGLU ? a.R / 2 : a.R;
+        hipLaunchKernelGGL(k_mgemm_reduce, dim3((nout + 255) / 256, a.nb), dim3(256), 0, st, a, pt, kz);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -197,6 +197,8 @@ struct qtts_dev {
     unsigned long long *gm_dbg = nullptr;
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
     int pinv_cap = 0;
+    float *mpart = nullptr;   // split-K partials of the matrix-core projections (k_mgemm_reduce)
+    size_t mpart_elems = 0;
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
     int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
@@ -645,6 +647,12 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     dv->pinv_cap = dv->rows_cap > 64 ? dv->rows_cap : 64;
     A(pinv, float, dv->pinv_cap);
     {
+        // 4 K columns of every prefill row at the widest projection, at most 64 M floats
+        const size_t wide = std::max<size_t>({(size_t)dv->QKV(), (size_t)2 * d.I, (size_t)d.H, (size_t)d.TH});
+        dv->mpart_elems = std::min<size_t>((size_t)4 * std::max<size_t>(R, 64) * wide, (size_t)64 << 20);
+        A(mpart, float, dv->mpart_elems);
+    }
+    {
         const int gph = d.NH / d.KV;
         // partial slots for the smaller split size of the two launch forms
         const int ch = std::min(qtts_attn_keys_per_split(d.HD, false, dv->attn_lpk),
@@ -759,7 +767,7 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
     if (rows > 64 && (!a.norm_w || rows <= dv->pinv_cap)) {
         GemvArgs c = a;
         c.nb = rows;
-        const int rc = qtts_mgemm(c, dv->pinv, dv->st);
+        const int rc = qtts_mgemm(c, dv->pinv, dv->st, dv->mpart, dv->mpart_elems);
         if (rc <= 0) return rc;
     }
     for (int r0 = 0; r0 < rows;) {
@@ -791,7 +799,7 @@ static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
         }
         if (rc == 1 && nr >= 2 && nr <= 16 && pgb) rc = qtts_gemvb(c, dv->st);
         if (rc == 1 && nr >= 2 && nr <= 16) rc = qtts_gemvm(c, dv->st);
-        if (rc == 1 && nr >= 2) rc = qtts_mgemm(c, dv->pinv, dv->st);
+        if (rc == 1 && nr >= 2) rc = qtts_mgemm(c, dv->pinv, dv->st, dv->mpart, dv->mpart_elems);
         if (rc < 0) return -1;
         if (rc == 1) {
             nr = nr < 16 ? nr : 16;
