@@ -649,8 +649,10 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     {
         // 4 K columns of every prefill row at the widest projection, at most 64 M floats
         const size_t wide = std::max<size_t>({(size_t)dv->QKV(), (size_t)2 * d.I, (size_t)d.H, (size_t)d.TH});
-        dv->mpart_elems = std::min<size_t>((size_t)4 * std::max<size_t>(R, 64) * wide, (size_t)64 << 20);
-        A(mpart, float, dv->mpart_elems);
+        // (QTTS_HIP_MGEMM_KZ=0: no scratch, no split)
+        const char *e = getenv("QTTS_HIP_MGEMM_KZ");
+        dv->mpart_elems = e && !strcmp(e, "0") ? 0 : std::min<size_t>((size_t)4 * std::max<size_t>(R, 64) * wide, (size_t)64 << 20);
+        if (dv->mpart_elems) A(mpart, float, dv->mpart_elems);
     }
     {
         const int gph = d.NH / d.KV;
