@@ -237,9 +237,11 @@ int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st, float *par
     // (QTTS_HIP_MGEMM_KZ: 1 = no split, n = at most n columns)
     static const int kzmax = [] { const char *e = getenv("QTTS_HIP_MGEMM_KZ"); const int v = e ? atoi(e) : 8;
                                   return v >= 1 && v <= 16 ? v : 8; }();
+    static const int wgmax = [] { const char *e = getenv("QTTS_HIP_MGEMM_WG"); const int v = e ? atoi(e) : 1024;
+                                  return v >= 256 && v <= 8192 ? v : 1024; }();
     int kz = 1;
     const int wgs = a.R / (16 * nw) * nch;
-    while (part && 2 * kz <= kzmax && wgs * 2 * kz <= 1024 && a.C % (32 * 2 * kz) == 0 &&
+    while (part && 2 * kz <= kzmax && wgs * 2 * kz <= wgmax && a.C % (32 * 2 * kz) == 0 &&
            a.C / 32 / (2 * kz) >= 8 && (size_t)2 * kz * a.nb * a.R <= part_elems)
         kz *= 2;
     float *pt = kz > 1 ? part : nullptr;
