@@ -362,6 +362,36 @@ FRAME_WEIGHT_BYTES = {"1.7b": 3.056e9, "0.6b": 1.107e9}
 KV_BYTES_PER_POS = 114688
 
 
+def eos_frames(eos):
+    """frames per utterance of an EOS / queue line (None: fixed-length)"""
+    if "frames_per_utterance" in eos:
+        return eos["frames_per_utterance"]
+    if "frames_per_utterance_mean" in eos:
+        return eos["frames_per_utterance_mean"]
+    q = eos.get("queue")
+    return q["frames_per_utterance_mean"] if q else None
+
+
+def workload_name(args, eos, wavs, vc):
+    w = (f"Qwen3-TTS-{args.preset} synthetic, P128 prompt, "
+         + (f"fixed {args.frames} frames ({args.frames * 0.08:.2f} s audio), " if not args.eos else "")
+         + f"{'greedy' if args.greedy else 'default sampling'}, batch {args.batch} per GPU")
+    if args.queue:
+        w += (f", work queue of {args.queue} utterances per GPU{' (one shared queue across ranks)' if args.queue_shared else ''}"
+              f" through the {args.batch} slots, freed slots refilled inside the live batch")
+    if wavs is not None:
+        w += (", ICL voice clone from 5 s reference audio (12 Hz codes + x-vector encoded on the GPU inside the "
+              "step) + 20-id reference text, codec over reference ++ generated (reference part cut)")
+    elif vc:
+        w += (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, codec over reference ++ "
+              "generated (reference part cut)")
+    elif args.eos:
+        f = eos_frames(eos) if eos else None
+        w += (f", EOS mode (max_new_tokens 4096, codec-head EOS row x {EOS_GAIN}: the utterances stop at frame {f}"
+              f"{'' if 'frames_per_utterance' in (eos or {}) else ' on average'})")
+    return w
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -391,6 +421,14 @@ def main():
                     help="the reference's default generation mode: max_new_tokens 4096 with the EOS stop, on the "
                          "synthetic model with the codec head's EOS row x EOS_GAIN (its utterance stops at frame 157); "
                          "also times fixed-length decodes of the same length")
+    ap.add_argument("--queue", type=int, default=0,
+                    help="work queue (SURVEY.md 8(e)): this many utterances per GPU per step through --batch "
+                         "lock-step slots, each freed slot refilled inside the live batch (qwen_tts_generate_queue); "
+                         "with --eos the utterances stop at their own EOS")
+    ap.add_argument("--queue-shared", action="store_true",
+                    help="with --queue: one queue of queue x gpus utterances for all ranks, each rank admitting the "
+                         "next index from a counter in the process group's store (a dynamic cross-GPU work queue, "
+                         "no collective in the data path)")
     ap.add_argument("--c1", action="store_true",
                     help="BASELINE C1 only: the reference c/ CLI on the 0.6B synthetic model, short prompt "
                          "(test/tokens_great_power.txt), on the host cores; no GPU")
@@ -435,6 +473,21 @@ def main():
     else:
         m.set_params(max_tokens=args.frames, fixed=args.frames, seed=42 + rank, **samp)
     prompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.batch)]
+    qprompts, qnext, qstep = None, None, [0]
+    if args.queue:
+        if args.queue_shared:   # every rank holds the whole list; a store counter hands out indices
+            qprompts = [prompt_ids("p128", seed=1234 + i) for i in range(args.queue * ws)]
+            if ws > 1:
+                import torch.distributed as dist
+                store = dist.distributed_c10d._get_default_store()
+
+                def qnext():
+                    i = store.add(f"qtts_queue_{qstep[0]}", 1) - 1
+                    return i if i < len(qprompts) else -1
+        else:
+            qprompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.queue)]
+    qstats = []
+    last_audio = [None]
 
     vc = None
     wavs = None
@@ -471,6 +524,14 @@ def main():
             if rc != 0:
                 raise RuntimeError("voice-clone generation failed")
             return sum(len(a) for a in aud)
+        if qprompts is not None:
+            n = len(qprompts)
+            rc, aud = m.generate_queue(qprompts, ["aiden"] * n, ["english"] * n, slots=args.batch, next_fn=qnext)
+            qstep[0] += 1
+            if rc != 0:
+                raise RuntimeError("queue generation failed")
+            qstats.append(m.queue_stats())
+            return sum(len(a) for a in aud if a is not None)
         if args.batch == 1:
             a = m.generate(prompts[0], "aiden", "english")
             if a is None:
@@ -479,10 +540,12 @@ def main():
         rc, aud = m.generate_batch(prompts, ["aiden"] * args.batch, ["english"] * args.batch)
         if rc != 0:
             raise RuntimeError("batch generation failed")
+        last_audio[0] = aud
         return sum(len(a) for a in aud)
 
     for _ in range(args.warmup):
         one_step()
+    qstats.clear()
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -503,7 +566,7 @@ def main():
         # (batch 1 only: the slots of a batch stop at different frames, so one
         # fixed length would be a different workload; there the line reports
         # the mean frames per utterance alone)
-        if args.batch == 1:
+        if args.batch == 1 and not args.queue:
             n_eos = samples // (1920 * args.steps)
             m.set_params(max_tokens=n_eos, fixed=n_eos, seed=42 + rank, **samp)
             one_step()
@@ -516,9 +579,40 @@ def main():
             eos = dict(eos_gain=EOS_GAIN, frames_per_utterance=n_eos, max_new_tokens=4096,
                        fixed_same_length_audio_s_per_s=round(sf / 24000.0 / elf, 3),
                        fixed_same_length_ms_per_step=round(elf / args.steps * 1e3, 2))
-        else:
+        elif not args.queue:
             eos = dict(eos_gain=EOS_GAIN, frames_per_utterance_mean=round(samples / (1920 * args.steps * args.batch), 2),
                        max_new_tokens=4096)
+            # a lock-step batch runs every slot to the longest one (+ the one
+            # frame of the lagged stop poll): useful slot-frames / launched
+            fr = [len(a) // 1920 for a in last_audio[0]] if last_audio[0] else []
+            if fr:
+                eos["slot_occupancy"] = round(sum(fr) / (args.batch * (max(fr) + 1)), 4)
+                eos["frames_per_slot_last_step"] = fr
+        else:
+            eos = dict(eos_gain=EOS_GAIN, max_new_tokens=4096)
+    if qstats:
+        used = sum(q["used"] for q in qstats)
+        launched = sum(q["frames"] for q in qstats)
+        nq_done = sum(sum(1 for f in q["frames_per_utt"] if f > 0) for q in qstats)
+        qd = dict(utterances_per_step=args.queue * (ws if args.queue_shared else 1), slots=args.batch,
+                  shared_across_ranks=bool(args.queue_shared),
+                  utterances_this_rank=nq_done, refills=sum(q["refills"] for q in qstats),
+                  frames_launched=launched, useful_slot_frames=used,
+                  slot_occupancy=round(used / (args.batch * launched), 4) if launched else None,
+                  useful_frames_per_s=round(used / el, 1),
+                  frames_per_utterance_mean=round(used / max(nq_done, 1), 2),
+                  lock_step_occupancy_same_utterances=None)
+        # the same utterances as lock-step batches of `slots` (in queue order):
+        # each batch runs to its longest utterance + the lagged poll's frame
+        q = qstats[-1]
+        fr = [f for f in q["frames_per_utt"] if f > 0]
+        if fr and not args.queue_shared:
+            ls = sum(max(fr[i:i + args.batch]) + 1 for i in range(0, len(fr), args.batch))
+            qd["lock_step_occupancy_same_utterances"] = round(sum(fr) / (args.batch * ls), 4)
+        if eos is not None:
+            eos.update(queue=qd)
+        else:
+            eos = dict(queue=qd)
     el_max = reduce_max(ws, el)
     audio_total = reduce_sum(ws, samples / 24000.0)
     value = audio_total / el_max
@@ -616,20 +710,12 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32 activations x bf16 weights (fp32 accumulate)",
             "data": f"synthetic (seeded random-init weights of the {args.preset.upper()} architecture, tools/synth_model.py)",
-            "config": {"workload": f"Qwen3-TTS-{args.preset} synthetic, P128 prompt, fixed {args.frames} frames "
-                                   f"({args.frames * 0.08:.2f} s audio), {'greedy' if args.greedy else 'default sampling'}, "
-                                   f"batch {args.batch} per GPU"
-                                   + ((", ICL voice clone from 5 s reference audio (12 Hz codes + x-vector encoded "
-                                       "on the GPU inside the step) + 20-id reference text, codec over reference ++ "
-                                       "generated (reference part cut)") if wavs is not None else
-                                      (", ICL voice clone: 63 reference frames + 20-id reference text + x-vector, "
-                                       "codec over reference ++ generated (reference part cut)") if vc else
-                                      (f", EOS mode (max_new_tokens 4096, codec-head EOS row x {EOS_GAIN}: the "
-                                       f"utterances stop at frame {eos.get('frames_per_utterance', eos.get('frames_per_utterance_mean'))}"
-                                       f"{'' if 'frames_per_utterance' in (eos or {}) else ' on average'})") if eos else ""),
-                       "global_batch": args.batch * ws, "frames": (eos.get("frames_per_utterance", eos.get("frames_per_utterance_mean")) if eos
-                                  else args.frames),
-                       "parallelism": f"dp{ws} (independent replicas, no collective in the data path)"},
+            "config": {"workload": workload_name(args, eos, wavs, vc),
+                       "global_batch": (args.queue * ws if args.queue else args.batch * ws),
+                       "frames": eos_frames(eos) if eos and eos_frames(eos) is not None else args.frames,
+                       "parallelism": f"dp{ws} (independent replicas, no collective in the data path"
+                                      + ("; utterance indices from a shared store counter" if args.queue_shared else "")
+                                      + ")"},
         }
         if fp:
             out["first_packet_ms"] = round(fp["first_packet_ms"], 2)

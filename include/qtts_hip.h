@@ -122,6 +122,25 @@ int qtts_dev_poll(qtts_dev_t *dev, int *stopped, int *n_gen, int *stop_step);
  * step + 1 first) and sets *all_stopped when every slot had drawn EOS by then
  * (the sampler mirrors the stops into pinned host memory). */
 int qtts_dev_frame_done(qtts_dev_t *dev, int step, int *all_stopped);
+/* ---- work queue (utterances of EOS-variable length on a
+ * live lock-step batch; no c/ counterpart -- the reference decodes one
+ * utterance per call, Q.c:1059-1443) ---- */
+/* Sizes the per-slot trailing text rows for the longest utterance of the run
+ * (call after qtts_dev_begin, before the first qtts_dev_prompt). */
+int qtts_dev_reserve(qtts_dev_t *dev, int max_trailing);
+/* Slot b takes the utterance the last qtts_dev_prompt(dev, b, ...) assembled,
+ * inside the live batch: its prompt rows but the last are prefilled into slot
+ * b's KV cache, the last row becomes the slot's talker input at position
+ * p_len - 1 (the next frame's talker step runs it, then samples the
+ * utterance's frame 0), and the slot's counters, repetition counts and RNG
+ * states start afresh.  Stream-ordered after the frames already queued. */
+int qtts_dev_refill(qtts_dev_t *dev, int b);
+/* Stops slot b from the next queued frame on (max_new_tokens / fixed length
+ * reached without EOS); stream-ordered. */
+int qtts_dev_retire(qtts_dev_t *dev, int b);
+/* Lagged like qtts_dev_frame_done: waits for frame `step`, then stopped[b] = 1
+ * for every slot that had drawn EOS by then. */
+int qtts_dev_frame_stops(qtts_dev_t *dev, int step, int *stopped);
 /* Copies slot b's codes [n_gen][G] to host. */
 int qtts_dev_get_codes(qtts_dev_t *dev, int b, int *host_codes, int max_frames);
 /* Codec decode of slot b's generated codes (device-resident) into a malloc'd

@@ -178,6 +178,16 @@ typedef struct {
     int last_stop_step;
     double perf_first_packet_ms; /* qwen_tts_generate_stream(): entry -> first audio chunk delivered */
     void *tokenizer;             /* Qwen2 BPE of the model dir, loaded on first text input */
+    /* the last qwen_tts_generate_queue, per utterance in input order */
+    int queue_n;
+    int **queue_codes;           /* [queue_n] [frames][num_code_groups] (NULL: not taken by this ctx) */
+    int *queue_frames;           /* frames generated (-1: not taken) */
+    int *queue_stop_reason;      /* 1 eos, 2 max_tokens */
+    int *queue_slot;             /* the slot it decoded on */
+    int queue_slots;             /* lock-step slots the run used */
+    int queue_frames_launched;   /* lock-step frames launched */
+    int queue_refills;           /* utterances admitted into a slot freed mid-run */
+    long long queue_slot_frames_used; /* sum of frames generated: occupancy = this / (slots * frames launched) */
 } qwen_tts_ctx_t;
 
 qwen_tts_ctx_t *qwen_tts_load(const char *model_dir);
@@ -213,6 +223,27 @@ qwen_tts_ctx_t *qwen_tts_load_on(const char *model_dir, int device);
  * set; returns 0 when every utterance produced audio. */
 int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *speakers,
                             const char *const *languages, float **out_audio, int *out_samples);
+/* Work queue (no c/ counterpart): nq utterances on at most nb
+ * lock-step slots.  When a slot's utterance stops (EOS, or max_new_tokens /
+ * fixed_codec_tokens frames), the next queued utterance is prefilled into that
+ * slot inside the live batch, so a batch of EOS-variable lengths keeps its
+ * slots busy instead of riding stopped rows to the longest one.  Each
+ * utterance decodes as it would alone (own KV positions, counters, repetition
+ * counts, RNG states from sample_seed).  `next` (optional) picks the utterance
+ * to admit: it returns an index in [0, nq) not yet taken, or -1 when there is
+ * none (e.g. a counter shared by the processes of several GPUs); NULL takes
+ * them in order.  out_audio[i] / out_samples[i] (input order) are filled for
+ * the utterances this ctx took (NULL / 0 for the others); codes and stop
+ * reasons stay in ctx->queue_* until the next call.  Returns 0 when every
+ * utterance taken produced audio. */
+typedef int (*qwen_tts_queue_next_cb)(void *userdata);
+int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *texts, const char *const *speakers,
+                            const char *const *languages, int nb, qwen_tts_queue_next_cb next, void *userdata,
+                            float **out_audio, int *out_samples);
+/* codes of utterance i of the last qwen_tts_generate_queue: copies up to
+ * max_frames rows (codes may be NULL to query), returns the frame count, -1 if
+ * this ctx did not decode it */
+int qwen_tts_queue_codes(qwen_tts_ctx_t *ctx, int i, int *codes, int max_frames);
 /* Voice clone (no c/ counterpart: the Python reference's generate_voice_clone,
  * qwen3_tts_model.py:506-630, modeling_qwen3_tts.py:1967-2232) from the 12 Hz
  * codes of the reference audio (ref_codes [n_ref_frames][16]) and/or the

@@ -82,7 +82,30 @@ __global__ void k_copy_rows(float *dst, int ldd, const float *src, int lds, cons
         dst[(size_t)r * ldd + c] = src[(size_t)sr * lds + c];
 }
 
+// one slot's fresh-utterance state (qtts_dev_refill): grid covers max(H, V)
+__global__ __launch_bounds__(256) void k_slot_reset(SlotResetArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < a.H) a.x[(size_t)a.b * a.H + i] = a.row[i];
+    if (i < a.V) a.counts[(size_t)a.b * a.V + i] = 0;
+    if (i == 0) {
+        a.kv_len[a.b] = a.pos;
+        a.n_gen[a.b] = 0;
+        a.cur_row[a.b] = 0;
+        a.stop_step[a.b] = 0;
+        a.last_tok[a.b] = 0;
+        a.rng[a.b] = a.seed_bits;
+        a.st_rng[a.b] = a.seed_bits;
+        a.stopped[a.b] = 0;
+    }
+}
+
 }  // namespace
+
+int qtts_slot_reset(const SlotResetArgs &a, hipStream_t st) {
+    const int n = a.H > a.V ? a.H : a.V;
+    hipLaunchKernelGGL(k_slot_reset, dim3((n + 255) / 256), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int qtts_embed_sum(const EmbedSumArgs &a, hipStream_t st) {
     if (a.G < 2 || a.G > 16) {

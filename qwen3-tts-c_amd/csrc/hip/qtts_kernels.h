@@ -235,3 +235,18 @@ int qtts_prompt_assemble(const PromptArgs &a, hipStream_t st);
 
 int qtts_copy_rows(float *dst, int ldd, const float *src, int lds, const int *src_rows, int nrows, int ncols,
                    hipStream_t st);
+
+// work-queue refill of one slot inside a live batch: the
+// slot's talker input row <- its last prompt row, kv_len <- pos, and a fresh
+// utterance's counters (Q.c:1250-1270: n_gen, rows, stop, repetition counts,
+// both RNG states at the seed)
+struct SlotResetArgs {
+    int b = 0, pos = 0, H = 0, V = 0;
+    const float *row = nullptr;          // [H] the prompt row the slot's next talker step consumes
+    float *x = nullptr;                  // [B][H] talker input
+    int *kv_len = nullptr, *n_gen = nullptr, *cur_row = nullptr, *stopped = nullptr, *stop_step = nullptr;
+    int *last_tok = nullptr, *counts = nullptr;   // counts [B][V]
+    uint32_t *rng = nullptr, *st_rng = nullptr;
+    uint32_t seed_bits = 0;
+};
+int qtts_slot_reset(const SlotResetArgs &a, hipStream_t st);

@@ -1398,20 +1398,22 @@ extern "C" int qtts_dev_prompt(qtts_dev_t *dv, int b, const int *text_ids, int n
     return 0;
 }
 
-// talker prefill over all slots' prompt rows (T.c:254-472)
-extern "C" int qtts_dev_prefill(qtts_dev_t *dv) {
-    if (!dv || dv->nb < 1) return -1;
-    hipSetDevice(dv->device);
+// talker prefill (T.c:254-472) of prompt rows [0, nrows[i]) of slots[i];
+// last[i] = the row index (in px) of slot i's last row
+static int prefill_rows(qtts_dev *dv, const std::vector<int> &slots, const std::vector<int> &nrows,
+                        std::vector<int> &last) {
     const qtts_dims_t &d = dv->d;
     hipStream_t st = dv->st;
-    std::vector<int> rb, pp, src, last(dv->nb);
-    for (int b = 0; b < dv->nb; ++b) {
-        for (int t = 0; t < dv->p_len_h[b]; ++t) {
+    std::vector<int> rb, pp, src;
+    last.assign(slots.size(), 0);
+    for (size_t i = 0; i < slots.size(); ++i) {
+        const int b = slots[i];
+        for (int t = 0; t < nrows[i]; ++t) {
             rb.push_back(b);
             pp.push_back(t);
             src.push_back(b * dv->p_cap + t);
         }
-        last[b] = (int)rb.size() - 1;
+        last[i] = (int)rb.size() - 1;
     }
     const int R = (int)rb.size();
     if (R < 1 || R > dv->rows_cap) return -1;
@@ -1447,12 +1449,82 @@ extern "C" int qtts_dev_prefill(qtts_dev_t *dv) {
             CKI(rows_proj(dv, a, R));
         }
     }
+    return 0;
+}
+
+// talker prefill over all slots' prompt rows (T.c:254-472)
+extern "C" int qtts_dev_prefill(qtts_dev_t *dv) {
+    if (!dv || dv->nb < 1) return -1;
+    hipSetDevice(dv->device);
+    const qtts_dims_t &d = dv->d;
+    hipStream_t st = dv->st;
+    std::vector<int> slots(dv->nb), last;
+    for (int b = 0; b < dv->nb; ++b) slots[b] = b;
+    CKI(prefill_rows(dv, slots, dv->p_len_h, last));
     // last raw hidden of each slot -> x_tk; kv_len = prefill length
     CK(hipMemcpyAsync(dv->plast, last.data(), dv->nb * 4, hipMemcpyHostToDevice, st));
     CKI(qtts_copy_rows(dv->x_tk, d.H, dv->px, d.H, dv->plast, dv->nb, d.H, st));
     CK(hipMemcpyAsync(dv->kv_len, dv->p_len_h.data(), dv->nb * 4, hipMemcpyHostToDevice, st));
     CK(hipStreamSynchronize(st));
     return 0;
+}
+
+// Work queue: slot b of the live batch takes the utterance
+// qtts_dev_prompt(b, ...) just assembled.  Its prompt rows but the last are
+// prefilled (the KV cache positions 0 .. p_len - 2 of slot b); the last prompt
+// row becomes the slot's talker input at kv_len = p_len - 1, so the next
+// lock-step frame (the talker-first graph every running slot replays) runs
+// that row through the talker at position p_len - 1 -- the same arithmetic the
+// reference's prefill applies to it (T.c:254-472 vs T.c:478-533, the last
+// row's hidden feeding codec_head, Q.c:1282-1295) -- then samples the
+// utterance's frame 0.  The slot's counters start afresh (Q.c:1250-1270).
+// Everything is ordered on the context stream after the frames already queued.
+extern "C" int qtts_dev_refill(qtts_dev_t *dv, int b) {
+    if (!dv || b < 0 || b >= dv->nb || dv->p_len_h[b] < 2) return -1;
+    hipSetDevice(dv->device);
+    const qtts_dims_t &d = dv->d;
+    std::vector<int> last;
+    CKI(prefill_rows(dv, std::vector<int>{b}, std::vector<int>{dv->p_len_h[b] - 1}, last));
+    SlotResetArgs r;
+    r.b = b; r.pos = dv->p_len_h[b] - 1; r.H = d.H; r.V = d.V;
+    r.row = dv->prefill + ((size_t)b * dv->p_cap + r.pos) * d.H;
+    r.x = dv->x_tk; r.kv_len = dv->kv_len; r.n_gen = dv->n_gen; r.cur_row = dv->cur_row; r.stopped = dv->stopped;
+    r.stop_step = dv->stop_step; r.last_tok = dv->last_tok; r.counts = dv->counts;
+    r.rng = dv->rng; r.st_rng = dv->st_rng; r.seed_bits = seed_bits(dv->par.seed);
+    CKI(qtts_slot_reset(r, dv->st));
+    CK(hipStreamSynchronize(dv->st));   // (the prefill's row lists are host vectors)
+    // the host's stop mirror: no queued frame writes it for this slot (it was
+    // stopped in all of them)
+    if (dv->hstop && b < dv->hstop_cap) ((volatile int *)dv->hstop)[b] = 0;
+    return 0;
+}
+
+// Work queue: stop slot b from the next queued frame on (its utterance reached
+// max_new_tokens / the fixed length without EOS, Q.c:1282); stream-ordered.
+extern "C" int qtts_dev_retire(qtts_dev_t *dv, int b) {
+    if (!dv || b < 0 || b >= dv->nb) return -1;
+    hipSetDevice(dv->device);
+    CK(hipMemsetD32Async((hipDeviceptr_t)(dv->stopped + b), 1, 1, dv->st));
+    return 0;
+}
+
+// Work queue, lagged as qtts_dev_frame_done: waits until frame `step` has
+// finished and copies every slot's EOS mirror (1: drew EOS by then).
+extern "C" int qtts_dev_frame_stops(qtts_dev_t *dv, int step, int *stopped) {
+    if (!dv || !stopped || !dv->hstop) return -1;
+    hipSetDevice(dv->device);
+    if (dv->graph_key == 1) CK(hipEventSynchronize(dv->fev[step & 1]));
+    else CK(hipStreamSynchronize(dv->st));
+    for (int b = 0; b < dv->nrun; ++b) stopped[b] = ((volatile int *)dv->hstop)[b] != 0;
+    return 0;
+}
+
+// sizes the per-slot trailing text rows for the longest utterance a run will
+// see (a later qtts_dev_prompt never grows them, so the frame graphs stay)
+extern "C" int qtts_dev_reserve(qtts_dev_t *dv, int max_trailing) {
+    if (!dv || max_trailing < 0) return -1;
+    hipSetDevice(dv->device);
+    return ensure_trailing(dv, max_trailing);
 }
 
 extern "C" int qtts_dev_frame(qtts_dev_t *dv, int step) {

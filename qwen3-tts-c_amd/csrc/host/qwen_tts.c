@@ -385,6 +385,23 @@ qwen_tts_ctx_t *qwen_tts_load_on(const char *model_dir, int device) {
     return ctx;
 }
 
+/* the per-utterance results of the last qwen_tts_generate_queue */
+static void queue_clear(qwen_tts_ctx_t *ctx) {
+    if (ctx->queue_codes)
+        for (int i = 0; i < ctx->queue_n; i++) free(ctx->queue_codes[i]);
+    free(ctx->queue_codes);
+    free(ctx->queue_frames);
+    free(ctx->queue_stop_reason);
+    free(ctx->queue_slot);
+    ctx->queue_codes = NULL;
+    ctx->queue_frames = ctx->queue_stop_reason = ctx->queue_slot = NULL;
+    ctx->queue_n = 0;
+    ctx->queue_frames_launched = 0;
+    ctx->queue_slot_frames_used = 0;
+    ctx->queue_refills = 0;
+    ctx->queue_slots = 0;
+}
+
 void qwen_tts_free(qwen_tts_ctx_t *ctx) {
     if (!ctx) return;
     if (ctx->hip) qtts_dev_destroy((qtts_dev_t *)ctx->hip);
@@ -396,6 +413,7 @@ void qwen_tts_free(qwen_tts_ctx_t *ctx) {
     free(ctx->config.language_ids);
     free(ctx->last_codes);
     free(ctx->tk_x);
+    queue_clear(ctx);
     qtok_free((qtok_t *)ctx->tokenizer);
     free(ctx);
 }
@@ -922,6 +940,211 @@ int qwen_tts_generate_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *text
                             const char *const *languages, float **out_audio, int *out_samples) {
     if (!ctx || nb < 1 || !texts || !out_audio || !out_samples) return -1;
     return run_batch(ctx, nb, texts, speakers, languages, out_audio, out_samples, now_ms(), NULL, NULL);
+}
+
+/* ------------------------------------------------------------- work queue */
+/* EOS-mode utterances (Q.c:1282-1330: each stops at its own
+ * EOS) on `nb` lock-step slots.  When a slot's utterance stops, its codes are
+ * collected and the next queued utterance is prefilled into that slot inside
+ * the live batch (qtts_dev_refill), so no slot rides along stopped while
+ * others decode, except for the one frame the lagged stop poll costs.  The
+ * frame loop is run_batch's: frame s + 1 is queued before the host waits for
+ * frame s.  Every utterance decodes exactly as it would alone (its own KV
+ * positions from 0, counters, repetition counts and RNG states from the seed);
+ * the codec passes of all of them run at the end on the codec lanes
+ * (qtts_dev_codec_multi). */
+static int queue_pull(int nq, int *taken, int *next_seq, qwen_tts_queue_next_cb next, void *user) {
+    if (next) {
+        const int i = next(user);
+        if (i < 0 || i >= nq || taken[i]) return -1;
+        taken[i] = 1;
+        return i;
+    }
+    while (*next_seq < nq && taken[*next_seq]) (*next_seq)++;
+    if (*next_seq >= nq) return -1;
+    taken[*next_seq] = 1;
+    return (*next_seq)++;
+}
+
+static void queue_plan_slot(prompt_t *p, int b) {
+    for (int k = 0; k < p->nplan; k++) p->plan[5 * k + 3] = b;
+}
+
+int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *texts, const char *const *speakers,
+                            const char *const *languages, int nb, qwen_tts_queue_next_cb next, void *user,
+                            float **out_audio, int *out_samples) {
+    if (!ctx || !ctx->hip || nq < 1 || nb < 1 || !texts || !out_audio || !out_samples) return -1;
+    qtts_dev_t *dev = (qtts_dev_t *)ctx->hip;
+    const qwen_tts_config_t *c = &ctx->config;
+    const int G = c->num_code_groups;
+    const double t_start = now_ms();
+    int rc = -1;
+    queue_clear(ctx);
+    for (int i = 0; i < nq; i++) { out_audio[i] = NULL; out_samples[i] = 0; }
+    prompt_t *pr = (prompt_t *)calloc(nq, sizeof(prompt_t));
+    int *taken = (int *)calloc(nq, sizeof(int)), next_seq = 0;
+    ctx->queue_codes = (int **)calloc(nq, sizeof(int *));
+    ctx->queue_frames = (int *)malloc(nq * sizeof(int));
+    ctx->queue_stop_reason = (int *)calloc(nq, sizeof(int));
+    ctx->queue_slot = (int *)malloc(nq * sizeof(int));
+    int *cur = (int *)malloc(nb * sizeof(int)), *first = (int *)calloc(nb, sizeof(int));
+    int *retired = (int *)calloc(nb, sizeof(int)), *hst = (int *)calloc(nb, sizeof(int));
+    int *cbuf = NULL;
+    if (!pr || !taken || !ctx->queue_codes || !ctx->queue_frames || !ctx->queue_stop_reason || !ctx->queue_slot ||
+        !cur || !first || !retired || !hst)
+        goto out;
+    ctx->queue_n = nq;
+    for (int i = 0; i < nq; i++) { ctx->queue_frames[i] = -1; ctx->queue_slot[i] = -1; }
+    /* every prompt up front (the prefill and trailing capacities cover all) */
+    int max_p = 0, max_tr = 0;
+    for (int i = 0; i < nq; i++) {
+        int *ids = NULL;
+        const int n = parse_ids(texts[i], &ids);
+        if (n < 8) {
+            if (n >= 0) fprintf(stderr, "Error: need at least 8 text tokens (chat template format)\n");
+            free(ids);
+            goto out;
+        }
+        for (int k = 0; k < n; k++)
+            if (ids[k] < 0 || ids[k] >= c->talker_text_vocab) {
+                fprintf(stderr, "Error: text token id %d out of range\n", ids[k]);
+                free(ids);
+                goto out;
+            }
+        int spk, lang;
+        lookup(ctx, speakers ? speakers[i] : NULL, languages ? languages[i] : NULL, &spk, &lang);
+        build_prompt(ctx, ids, n, spk, lang, 0, &pr[i]);
+        free(ids);
+        if (pr[i].p_len > max_p) max_p = pr[i].p_len;
+        if (pr[i].n_trailing > max_tr) max_tr = pr[i].n_trailing;
+    }
+    const int fixed = ctx->fixed_codec_tokens > 0 ? ctx->fixed_codec_tokens : 0;
+    const int max_tokens = fixed > 0 ? fixed : ctx->max_new_tokens;
+    if (max_tokens < 1) goto out;
+    /* the first nb utterances fill the slots */
+    int ns = 0;
+    while (ns < nb) {
+        const int u = queue_pull(nq, taken, &next_seq, next, user);
+        if (u < 0) break;
+        cur[ns++] = u;
+    }
+    ctx->queue_slots = ns;
+    if (ns == 0) { rc = 0; goto out; }   /* (another puller took everything) */
+    qtts_gen_params_t gp;
+    params_of(ctx, &gp);
+    if (qtts_dev_begin(dev, ns, max_tokens, max_p, &gp) != 0 || qtts_dev_reserve(dev, max_tr) != 0) goto out;
+    /* (a plan row's 4th int is the destination slot: set when the slot is known) */
+#define PROMPT(b, u) (queue_plan_slot(&pr[u], (b)), \
+                      qtts_dev_prompt(dev, (b), pr[u].text, pr[u].n_text, pr[u].plan, pr[u].nplan, pr[u].p_len, \
+                                      pr[u].n_trailing, pr[u].pad_row))
+    for (int b = 0; b < ns; b++)
+        if (PROMPT(b, cur[b]) != 0) goto out;
+    double t_prefill = now_ms();
+    if (qtts_dev_prefill(dev) != 0) goto out;
+    ctx->perf_prefill_ms = now_ms() - t_prefill;
+    cbuf = (int *)malloc((size_t)(max_tokens + 1) * G * sizeof(int));
+    if (!cbuf) goto out;
+    int active = ns, done_n = 0;
+    int step = 0;
+    const double t_gen = now_ms();
+    for (;; step++) {
+        /* a slot whose utterance produced max_tokens frames by frame step - 1
+         * stops before frame step (host count: no EOS draw marks it) */
+        for (int b = 0; b < ns; b++)
+            if (cur[b] >= 0 && !retired[b] && step - first[b] >= max_tokens) {
+                if (qtts_dev_retire(dev, b) != 0) goto out;
+                retired[b] = 1;
+            }
+        if (qtts_dev_frame(dev, step) != 0) goto out;
+        if (step == 0) {
+            qtts_dev_poll(dev, NULL, NULL, NULL);
+            ctx->perf_first_frame_ms = now_ms() - t_start;
+        }
+        if (step < 1) continue;
+        /* frame step is queued: which slots had stopped by frame step - 1 */
+        if (qtts_dev_frame_stops(dev, step - 1, hst) != 0) goto out;
+        for (int b = 0; b < ns; b++) {
+            if (cur[b] < 0) continue;
+            const int capped = step - first[b] >= max_tokens;
+            if (!hst[b] && !capped) continue;
+            /* utterance cur[b] is complete (slot b is a no-op in frame step) */
+            const int u = cur[b];
+            const int n = qtts_dev_get_codes(dev, b, cbuf, max_tokens);
+            if (n < 0) goto out;
+            ctx->queue_codes[u] = (int *)malloc((size_t)(n > 0 ? n : 1) * G * sizeof(int));
+            if (!ctx->queue_codes[u]) goto out;
+            memcpy(ctx->queue_codes[u], cbuf, (size_t)n * G * sizeof(int));
+            ctx->queue_frames[u] = n;
+            ctx->queue_stop_reason[u] = hst[b] ? 1 : 2;
+            ctx->queue_slot[u] = b;
+            ctx->queue_slot_frames_used += n;
+            done_n++;
+            if (qwen_tts_verbose >= 1)
+                fprintf(stderr, "Queue: utterance %d on slot %d: %s at step %d (frame %d)\n", u, b,
+                        hst[b] ? "eos" : "max_tokens", n, step - 1);
+            cur[b] = -1;
+            active--;
+            const int u2 = queue_pull(nq, taken, &next_seq, next, user);
+            if (u2 < 0) continue;
+            if (PROMPT(b, u2) != 0 || qtts_dev_refill(dev, b) != 0) goto out;
+            cur[b] = u2;
+            first[b] = step + 1;   /* its frame 0 is the next frame launched */
+            retired[b] = 0;
+            hst[b] = 0;
+            active++;
+            ctx->queue_refills++;
+        }
+        if (active == 0) break;
+        if (ctx->progress_cb) ctx->progress_cb(done_n, nq, ctx->progress_cb_userdata);
+    }
+#undef PROMPT
+    ctx->queue_frames_launched = step + 1;
+    ctx->perf_talker_ms = now_ms() - t_gen;
+    {
+        /* every finished utterance's codec pass, several side by side */
+        int nj = 0;
+        int *uj = (int *)malloc(nq * sizeof(int)), *tj = (int *)malloc(nq * sizeof(int));
+        int *sl = (int *)calloc(nq, sizeof(int)), *sj = (int *)calloc(nq, sizeof(int));
+        const int **hc = (const int **)calloc(nq, sizeof(int *));
+        float **aj = (float **)calloc(nq, sizeof(float *));
+        if (!uj || !tj || !sl || !sj || !hc || !aj) {
+            free(uj); free(tj); free(sl); free(sj); free(hc); free(aj);
+            goto out;
+        }
+        rc = 0;
+        for (int u = 0; u < nq; u++) {
+            if (ctx->queue_frames[u] < 0) continue;   /* not taken by this ctx */
+            if (ctx->queue_frames[u] == 0) { rc = -1; continue; }
+            uj[nj] = u; tj[nj] = ctx->queue_frames[u]; hc[nj] = ctx->queue_codes[u];
+            nj++;
+        }
+        const double t_codec = now_ms();
+        if (nj > 0 && qtts_dev_codec_multi(dev, nj, hc, sl, tj, aj, sj) != 0) rc = -1;
+        for (int j = 0; j < nj; j++) {
+            out_audio[uj[j]] = aj[j];
+            out_samples[uj[j]] = aj[j] ? sj[j] : 0;
+            if (!aj[j] || sj[j] <= 0) rc = -1;
+        }
+        ctx->perf_codec_ms = now_ms() - t_codec;
+        free(uj); free(tj); free(sl); free(sj); free(hc); free(aj);
+    }
+    ctx->perf_total_ms = now_ms() - t_start;
+    if (qwen_tts_verbose >= 1)
+        fprintf(stderr, "Queue: %d utterances on %d slots, %d frames, %d refills, slot occupancy %.3f\n", done_n, ns,
+                ctx->queue_frames_launched, ctx->queue_refills,
+                (double)ctx->queue_slot_frames_used / ((double)ns * ctx->queue_frames_launched));
+out:
+    if (pr)
+        for (int i = 0; i < nq; i++) { free(pr[i].text); free(pr[i].plan); }
+    free(pr); free(taken); free(cur); free(first); free(retired); free(hst); free(cbuf);
+    return rc;
+}
+
+int qwen_tts_queue_codes(qwen_tts_ctx_t *ctx, int i, int *codes, int max_frames) {
+    if (!ctx || i < 0 || i >= ctx->queue_n || !ctx->queue_codes || !ctx->queue_codes[i] || max_frames < 0) return -1;
+    const int n = ctx->queue_frames[i] < max_frames ? ctx->queue_frames[i] : max_frames;
+    if (codes) memcpy(codes, ctx->queue_codes[i], (size_t)n * ctx->config.num_code_groups * sizeof(int));
+    return n;
 }
 
 static int vclone_run(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, const char *const *ref_texts,

@@ -24,6 +24,7 @@ _fp = C.POINTER(C.c_float)
 _ip = C.POINTER(C.c_int)
 
 PROGRESS_CB = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p)
+QUEUE_NEXT_CB = C.CFUNCTYPE(C.c_int, C.c_void_p)
 AUDIO_CB = C.CFUNCTYPE(None, C.POINTER(C.c_float), C.c_int, C.c_void_p)
 
 
@@ -59,6 +60,9 @@ class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
         ("last_codes", _ip), ("last_frames", C.c_int), ("last_stop_reason", C.c_int), ("last_stop_step", C.c_int),
         ("perf_first_packet_ms", C.c_double),
         ("tokenizer", C.c_void_p),
+        ("queue_n", C.c_int), ("queue_codes", C.POINTER(_ip)), ("queue_frames", _ip), ("queue_stop_reason", _ip),
+        ("queue_slot", _ip), ("queue_slots", C.c_int), ("queue_frames_launched", C.c_int),
+        ("queue_refills", C.c_int), ("queue_slot_frames_used", C.c_longlong),
     ]
 
 
@@ -83,7 +87,8 @@ EXPORTS = [
     "qtts_dev_codec_stream_prime", "qtts_dev_codec_stream_push_slot",
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
     "qtts_dev_codec_async_end", "qtts_dev_codec_multi", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",
-    "qtts_dev_encode_audio",
+    "qtts_dev_encode_audio", "qwen_tts_generate_queue", "qwen_tts_queue_codes", "qtts_dev_reserve", "qtts_dev_refill",
+    "qtts_dev_retire", "qtts_dev_frame_stops",
 ]
 
 _LIB = None
@@ -142,6 +147,12 @@ def lib():
     L.qwen_tts_last_codes.argtypes = [C.POINTER(Ctx), _ip, C.c_int]
     L.qwen_tts_last_codes_slot.restype = C.c_int
     L.qwen_tts_last_codes_slot.argtypes = [C.POINTER(Ctx), C.c_int, _ip, C.c_int]
+    L.qwen_tts_generate_queue.restype = C.c_int
+    L.qwen_tts_generate_queue.argtypes = [C.POINTER(Ctx), C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                          C.POINTER(C.c_char_p), C.c_int, QUEUE_NEXT_CB, C.c_void_p,
+                                          C.POINTER(C.c_void_p), _ip]
+    L.qwen_tts_queue_codes.restype = C.c_int
+    L.qwen_tts_queue_codes.argtypes = [C.POINTER(Ctx), C.c_int, _ip, C.c_int]
     L.qwen_tts_talker_prefill.argtypes = [C.POINTER(Ctx), _fp, C.c_int]
     L.qwen_tts_talker_forward.argtypes = [C.POINTER(Ctx), _fp, _fp]
     L.qwen_tts_subtalker_generate.argtypes = [C.POINTER(Ctx), _fp, C.c_int, _ip]
@@ -432,6 +443,43 @@ class QwenTTS:
         self._last_nb = nb
         audio = [_take_audio(out[i], ns[i]) for i in range(nb)]
         return rc, audio
+
+    def generate_queue(self, id_lists, speakers=None, languages=None, slots=8, next_fn=None):
+        """Work queue (qwen_tts_generate_queue): the utterances on at most
+        `slots` lock-step slots, each freed slot refilled with the next
+        utterance inside the live batch.  next_fn() (optional) returns the index
+        of the next utterance to admit or -1 (e.g. a counter shared by several
+        GPUs' processes); default: in order.  Returns (rc, [audio or None])."""
+        nq = len(id_lists)
+        tx = (C.c_char_p * nq)(*[",".join(str(int(i)) for i in ids).encode() for ids in id_lists])
+        sp = (C.c_char_p * nq)(*[(s.encode() if s else None) for s in (speakers or [None] * nq)])
+        lg = (C.c_char_p * nq)(*[(s.encode() if s else None) for s in (languages or [None] * nq)])
+        out = (C.c_void_p * nq)()
+        ns = (C.c_int * nq)()
+        cb = QUEUE_NEXT_CB(lambda u: int(next_fn())) if next_fn is not None else QUEUE_NEXT_CB()
+        rc = lib().qwen_tts_generate_queue(self.ctx, nq, tx, sp, lg, int(slots), cb, None, out, ns)
+        return rc, [_take_audio(out[i], ns[i]) for i in range(nq)]
+
+    def queue_codes(self, i):
+        """codes [frames, groups] of utterance i of the last generate_queue (None: not decoded here)"""
+        n = lib().qwen_tts_queue_codes(self.ctx, int(i), None, 1 << 30)
+        if n < 0:
+            return None
+        buf = np.zeros((max(n, 1), self.cfg.num_code_groups), np.int32)
+        lib().qwen_tts_queue_codes(self.ctx, int(i), buf.ctypes.data_as(_ip), n)
+        return buf[:n].copy()
+
+    def queue_stats(self):
+        """{slots, frames, refills, used, occupancy, stop_reason[], frames_per_utt[]} of the last generate_queue"""
+        c = self.c
+        n = c.queue_n
+        launched = c.queue_frames_launched
+        return {"slots": c.queue_slots, "frames": launched, "refills": c.queue_refills,
+                "used": int(c.queue_slot_frames_used),
+                "occupancy": (c.queue_slot_frames_used / (c.queue_slots * launched)) if launched and c.queue_slots else 0.0,
+                "stop_reason": [c.queue_stop_reason[i] for i in range(n)] if n else [],
+                "frames_per_utt": [c.queue_frames[i] for i in range(n)] if n else [],
+                "slot": [c.queue_slot[i] for i in range(n)] if n else []}
 
     def generate_stream(self, ids, speaker=None, language=None, chunk_frames=4, on_chunk=None):
         """Streaming generation; on_chunk(np.ndarray) gets each audio chunk as

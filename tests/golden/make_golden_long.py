@@ -76,6 +76,10 @@ EOS_GAIN = 1.4                               # bench.py EOS_GAIN
 EOS_SEEDS = [1234, 1235, 1236]
 EOS_SPEAKERS = ["aiden", "vivian", "serena"]
 EOS_CAP = 1024                               # the fixture asserts every run stopped well before this
+# (the cap bounds a run that would not stop; every fixture run stops well
+# before it, so each result equals the reference's 4096-token run)
+EOS_Q_SEEDS = [1237, 1238, 1239]             # long_eos17q: three more EOS utterances for the slot-refill queue
+EOS_Q_SPEAKERS = ["aiden", "vivian", "serena"]
 
 
 def model_hashes(md):
@@ -210,16 +214,23 @@ def eos_model():
     return ensure_model(os.path.join(MODEL_ROOT, f"1.7b_eos_gain{EOS_GAIN}"), "1.7b", overrides={"eos_gain": EOS_GAIN})
 
 
+def eos_seed_speaker(b):
+    """Utterance b of the EOS set: 0-2 long_eos17, 3-5 long_eos17q."""
+    seeds, spks = EOS_SEEDS + EOS_Q_SEEDS, EOS_SPEAKERS + EOS_Q_SPEAKERS
+    return seeds[b], spks[b]
+
+
 def eos17_slot(b):
-    """One EOS-mode reference run (slot b): codes [stop][G], every 16th sample."""
+    """One EOS-mode reference run (utterance b): codes [stop][G], every 16th sample."""
     ref = RefLib(eos_model())
-    ids = np.array(prompt_ids("p128", EOS_SEEDS[b]), np.int32)
+    seed, spk = eos_seed_speaker(b)
+    ids = np.array(prompt_ids("p128", seed), np.int32)
     # max_tokens is EOS_CAP, not 4096, only to bound a run that would not
     # stop; every fixture run stops well before it (asserted), so the result
     # equals the 4096-token run's
     ref.set_params(max_tokens=EOS_CAP, fixed=0, seed=42, **DEFAULT)
     t = time.time()
-    audio = ref.generate(ids, EOS_SPEAKERS[b], "english")
+    audio = ref.generate(ids, spk, "english")
     c = ref.recorded_codes()
     print(f"1.7b eos slot {b}: stopped after {c.shape[0]} frames, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
     assert 0 < c.shape[0] < EOS_CAP - 1, c.shape
@@ -228,15 +239,16 @@ def eos17_slot(b):
     return c, audio[::AUDIO_STRIDE].copy()
 
 
-def eos17_fixtures(slot_dir=None):
+def eos17_fixtures(slot_dir=None, utts=(0, 1, 2)):
     """slot_dir: the per-slot results of `--eos-slot b --slot-dir D` runs (one
     process per slot: the reference's recording hooks are process-global, and
-    its talker GEMV is single-threaded, so the three runs go in parallel)."""
+    its talker GEMV is single-threaded, so the three runs go in parallel).
+    utts: (0, 1, 2) long_eos17, (3, 4, 5) long_eos17q."""
     md = eos_model()
     g = {}
-    ids_all = [np.array(prompt_ids("p128", s), np.int32) for s in EOS_SEEDS]
+    ids_all = [np.array(prompt_ids("p128", eos_seed_speaker(b)[0]), np.int32) for b in utts]
     stops, codes, sub = [], [], []
-    for b in range(len(EOS_SEEDS)):
+    for b in utts:
         if slot_dir:
             z = np.load(os.path.join(slot_dir, f"eos_slot{b}.npz"))
             c, sb = z["codes"], z["audio_sub"]
@@ -258,7 +270,7 @@ def eos17_fixtures(slot_dir=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["hd128", "1.7b", "0.6b", "b8", "b8bench", "eos17"])
+    ap.add_argument("--only", choices=["hd128", "1.7b", "0.6b", "b8", "b8bench", "eos17", "eos17q"])
     ap.add_argument("--eos-slot", type=int, default=None, help="run one EOS slot into --slot-dir and exit")
     ap.add_argument("--slot-dir", default=None, help="eos17: per-slot results of --eos-slot runs")
     a = ap.parse_args()
@@ -314,10 +326,22 @@ def main():
         man["eos17"] = {"eos_gain": EOS_GAIN, "prompt": "p128", "prompt_seeds": EOS_SEEDS, "seed": 42,
                         "sampling": "default", "speakers": EOS_SPEAKERS, "language": "english",
                         "max_tokens": EOS_CAP, "audio_stride": AUDIO_STRIDE}
+    if a.only == "eos17q":   # (not in the default set: its three reference runs take ~1 h in parallel)
+        g, md = eos17_fixtures(a.slot_dir, utts=(3, 4, 5))
+        np.savez_compressed(os.path.join(HERE, "long_eos17q.npz"), **g)
+        man["models"][f"1.7b_eos_gain{EOS_GAIN}"] = model_hashes(md)
+        man["eos17q"] = {"eos_gain": EOS_GAIN, "prompt": "p128", "prompt_seeds": EOS_Q_SEEDS, "seed": 42,
+                         "sampling": "default", "speakers": EOS_Q_SPEAKERS, "language": "english",
+                         "max_tokens": EOS_CAP, "audio_stride": AUDIO_STRIDE,
+                         "note": "max_tokens is a bound on a run that would not stop; every run stopped well "
+                                 "before it, so the codes equal the reference's 4096-token run"}
+    if "eos17" in man and "note" not in man["eos17"]:
+        man["eos17"]["note"] = ("max_tokens is a bound on a run that would not stop; every run stopped well "
+                                "before it, so the codes equal the reference's 4096-token run")
     with open(mpath, "w") as f:
         json.dump(man, f, indent=1)
     for fn in ("long_hd128.npz", "long_17b.npz", "long_06b.npz", "long_17b_b8.npz", "long_17b_b8bench.npz",
-               "long_eos17.npz", "long_manifest.json"):
+               "long_eos17.npz", "long_eos17q.npz", "long_manifest.json"):
         p = os.path.join(HERE, fn)
         if os.path.exists(p):
             print(fn, os.path.getsize(p))
