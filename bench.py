@@ -593,12 +593,18 @@ def main():
     if qstats:
         used = sum(q["used"] for q in qstats)
         launched = sum(q["frames"] for q in qstats)
+        rows = sum(q["rows_launched"] for q in qstats)
         nq_done = sum(sum(1 for f in q["frames_per_utt"] if f > 0) for q in qstats)
         qd = dict(utterances_per_step=args.queue * (ws if args.queue_shared else 1), slots=args.batch,
                   shared_across_ranks=bool(args.queue_shared),
                   utterances_this_rank=nq_done, refills=sum(q["refills"] for q in qstats),
                   frames_launched=launched, useful_slot_frames=used,
-                  slot_occupancy=round(used / (args.batch * launched), 4) if launched else None,
+                  rows_launched=rows,
+                  slot_occupancy=round(used / rows, 4) if rows else None,
+                  slot_occupancy_full_width=round(used / (args.batch * launched), 4) if launched else None,
+                  occupancy_note="useful slot-frames / slot rows launched (the tail, with nothing left to admit, "
+                                 "moves the running utterances to the first slots and launches those rows only); "
+                                 "full_width: / (slots x frames launched)",
                   useful_frames_per_s=round(used / el, 1),
                   frames_per_utterance_mean=round(used / max(nq_done, 1), 2),
                   lock_step_occupancy_same_utterances=None)

@@ -141,6 +141,14 @@ int qtts_dev_retire(qtts_dev_t *dev, int b);
 /* Lagged like qtts_dev_frame_done: waits for frame `step`, then stopped[b] = 1
  * for every slot that had drawn EOS by then. */
 int qtts_dev_frame_stops(qtts_dev_t *dev, int step, int *stopped);
+/* Tail of a queue run (nothing left to admit): slot `from`'s whole decode
+ * state (KV cache rows, input row, counters, codes, trailing rows, RNG)
+ * moves to the freed slot `to`, so the running slots are the first ones;
+ * set_rows then launches the first `rows` slots only (a graph per row count,
+ * captured on first use).  Both need the stream idle (after frame_stops /
+ * get_codes). */
+int qtts_dev_move_slot(qtts_dev_t *dev, int from, int to);
+int qtts_dev_set_rows(qtts_dev_t *dev, int rows);
 /* Copies slot b's codes [n_gen][G] to host. */
 int qtts_dev_get_codes(qtts_dev_t *dev, int b, int *host_codes, int max_frames);
 /* Codec decode of slot b's generated codes (device-resident) into a malloc'd

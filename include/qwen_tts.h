@@ -187,7 +187,9 @@ typedef struct {
     int queue_slots;             /* lock-step slots the run used */
     int queue_frames_launched;   /* lock-step frames launched */
     int queue_refills;           /* utterances admitted into a slot freed mid-run */
-    long long queue_slot_frames_used; /* sum of frames generated: occupancy = this / (slots * frames launched) */
+    long long queue_slot_frames_used; /* sum of frames generated */
+    long long queue_rows_launched;    /* sum over launched frames of the slot rows they ran (the tail launches
+                                         only the running slots): occupancy = frames_used / rows_launched */
 } qwen_tts_ctx_t;
 
 qwen_tts_ctx_t *qwen_tts_load(const char *model_dir);

@@ -72,6 +72,8 @@ float host_f16(uint16_t h) {
 
 }  // namespace
 
+static constexpr int QTTS_MAX_SLOTS = 64;   // row counts with their own tail graph (qtts_dev_set_rows)
+
 struct qtts_dev {
     qtts_dims_t d{};
     int device = 0;
@@ -146,6 +148,9 @@ struct qtts_dev {
     qtts_gen_params_t par{};
     bool have_par = false;
     hipGraphExec_t g0 = nullptr, gN = nullptr;
+    // work queue, tail of a run: the talker-first frame graph over the first
+    // nrun < nb slots (qtts_dev_set_rows), captured on first use
+    hipGraphExec_t gNr[QTTS_MAX_SLOTS + 1] = {};
     int graph_key = -1;
     // EOS-mode lagged poll: the sampler mirrors each slot's stop into pinned
     // host memory; an event after every frame lets the host wait for frame
@@ -238,9 +243,15 @@ static void *dalloc(qtts_dev *dv, size_t n, bool weight) {
     return p;
 }
 
+static void drop_row_graphs(qtts_dev *dv) {
+    for (auto &g : dv->gNr)
+        if (g) { hipGraphExecDestroy(g); g = nullptr; }
+}
+
 static void free_state(qtts_dev *dv) {
     if (dv->g0) { hipGraphExecDestroy(dv->g0); dv->g0 = nullptr; }
     if (dv->gN) { hipGraphExecDestroy(dv->gN); dv->gN = nullptr; }
+    drop_row_graphs(dv);
     for (void *p : dv->sallocs) hipFree(p);
     dv->sallocs.clear();
     dv->sbytes = 0;
@@ -1278,9 +1289,15 @@ static int ensure_graphs(qtts_dev *dv) {
     if (dv->g0 && dv->gN && dv->graph_key == 1) return 0;
     if (dv->g0) { hipGraphExecDestroy(dv->g0); dv->g0 = nullptr; }
     if (dv->gN) { hipGraphExecDestroy(dv->gN); dv->gN = nullptr; }
+    drop_row_graphs(dv);
     if (getenv("QTTS_HIP_NO_GRAPH")) { dv->graph_key = 0; return 0; }
-    CKI(capture(dv, false, &dv->g0));
-    CKI(capture(dv, true, &dv->gN));
+    // (the two main graphs always cover every slot)
+    const int nrun = dv->nrun;
+    dv->nrun = dv->nb;
+    int rc = capture(dv, false, &dv->g0);
+    if (!rc) rc = capture(dv, true, &dv->gN);
+    dv->nrun = nrun;
+    CKI(rc);
     dv->graph_key = 1;
     return 0;
 }
@@ -1305,6 +1322,7 @@ extern "C" int qtts_dev_begin(qtts_dev_t *dv, int nb, int max_frames, int max_pr
         dv->have_par = true;
         dv->graph_key = -1;
     }
+    dv->nrun = dv->nb;
     CKI(reset_counters(dv));
     return 0;
 }
@@ -1519,6 +1537,54 @@ extern "C" int qtts_dev_frame_stops(qtts_dev_t *dv, int step, int *stopped) {
     return 0;
 }
 
+// Work queue, tail of a run (no utterance left to admit): slot `from`'s
+// whole decode state moves to slot `to` (a freed slot below it), so that the
+// running slots are the first ones and qtts_dev_set_rows can launch fewer
+// rows.  Stream-ordered; the caller has synchronised (no frame in flight
+// writes either slot).
+extern "C" int qtts_dev_move_slot(qtts_dev_t *dv, int from, int to) {
+    if (!dv || from < 0 || to < 0 || from >= dv->nb || to >= dv->nb || from == to) return -1;
+    hipSetDevice(dv->device);
+    const qtts_dims_t &d = dv->d;
+    hipStream_t st = dv->st;
+    int kv = 0;
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(&kv, dv->kv_len + from, 4, hipMemcpyDeviceToHost));
+    if (kv < 0 || kv >= dv->S) return -1;
+    const size_t KVD = (size_t)d.KV * d.HD, lstride = (size_t)dv->nb * dv->S * KVD * 4;
+    const size_t w = (size_t)(kv + 1) * KVD * 4;   // positions 0 .. kv (the next step writes kv)
+    for (float *c : {dv->kc, dv->vc})
+        CK(hipMemcpy2DAsync((char *)c + (size_t)to * dv->S * KVD * 4, lstride,
+                            (const char *)c + (size_t)from * dv->S * KVD * 4, lstride, w, d.L,
+                            hipMemcpyDeviceToDevice, st));
+    auto row = [&](void *base, size_t bytes) {
+        return hipMemcpyAsync((char *)base + (size_t)to * bytes, (const char *)base + (size_t)from * bytes, bytes,
+                              hipMemcpyDeviceToDevice, st);
+    };
+    CK(row(dv->x_tk, (size_t)d.H * 4));
+    CK(row(dv->counts, (size_t)d.V * 4));
+    CK(row(dv->codes, (size_t)(dv->max_frames + 1) * d.G * 4));
+    CK(row(dv->trailing, (size_t)dv->tr_cap * d.H * 4));
+    for (int *p : {dv->kv_len, dv->n_gen, dv->cur_row, dv->stopped, dv->stop_step, dv->last_tok, dv->n_trailing})
+        CK(row(p, 4));
+    CK(row(dv->rng, 4));
+    CK(row(dv->st_rng, 4));
+    CK(hipStreamSynchronize(st));
+    dv->p_len_h[to] = dv->p_len_h[from];
+    dv->n_tr_h[to] = dv->n_tr_h[from];
+    if (dv->hstop && from < dv->hstop_cap && to < dv->hstop_cap)
+        ((volatile int *)dv->hstop)[to] = ((volatile int *)dv->hstop)[from];
+    return 0;
+}
+
+// Work queue: the next frames launch the first `rows` slots only (1 <= rows
+// <= the slots of qtts_dev_begin; their own graph per row count).
+extern "C" int qtts_dev_set_rows(qtts_dev_t *dv, int rows) {
+    if (!dv || rows < 1 || rows > dv->nb || (rows < dv->nb && rows > QTTS_MAX_SLOTS)) return -1;
+    dv->nrun = rows;
+    return 0;
+}
+
 // sizes the per-slot trailing text rows for the longest utterance a run will
 // see (a later qtts_dev_prompt never grows them, so the frame graphs stay)
 extern "C" int qtts_dev_reserve(qtts_dev_t *dv, int max_trailing) {
@@ -1531,8 +1597,15 @@ extern "C" int qtts_dev_frame(qtts_dev_t *dv, int step) {
     if (!dv) return -1;
     hipSetDevice(dv->device);
     CKI(ensure_graphs(dv));
+    if (dv->nrun < dv->nb && step == 0) return -1;   // (frame 0 runs every slot)
     if (dv->graph_key == 0) return record_frame(dv, step > 0);
-    CK(hipGraphLaunch(step == 0 ? dv->g0 : dv->gN, dv->st));
+    hipGraphExec_t g = step == 0 ? dv->g0 : dv->gN;
+    if (dv->nrun < dv->nb) {
+        hipGraphExec_t &gr = dv->gNr[dv->nrun];
+        if (!gr) CKI(capture(dv, true, &gr));
+        g = gr;
+    }
+    CK(hipGraphLaunch(g, dv->st));
     CK(hipEventRecord(dv->fev[step & 1], dv->st));
     return 0;
 }

@@ -398,6 +398,7 @@ static void queue_clear(qwen_tts_ctx_t *ctx) {
     ctx->queue_n = 0;
     ctx->queue_frames_launched = 0;
     ctx->queue_slot_frames_used = 0;
+    ctx->queue_rows_launched = 0;
     ctx->queue_refills = 0;
     ctx->queue_slots = 0;
 }
@@ -1044,7 +1045,11 @@ int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *text
     ctx->perf_prefill_ms = now_ms() - t_prefill;
     cbuf = (int *)malloc((size_t)(max_tokens + 1) * G * sizeof(int));
     if (!cbuf) goto out;
-    int active = ns, done_n = 0;
+    int active = ns, done_n = 0, rows = ns, exhausted = 0;
+    /* tail compaction (nothing left to admit): the running slots move to the
+     * first rows and the frames launch those only (QTTS_QUEUE_COMPACT=0: off) */
+    const char *ce = getenv("QTTS_QUEUE_COMPACT");
+    const int compact = !(ce && !strcmp(ce, "0"));
     int step = 0;
     const double t_gen = now_ms();
     for (;; step++) {
@@ -1056,6 +1061,7 @@ int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *text
                 retired[b] = 1;
             }
         if (qtts_dev_frame(dev, step) != 0) goto out;
+        ctx->queue_rows_launched += rows;
         if (step == 0) {
             qtts_dev_poll(dev, NULL, NULL, NULL);
             ctx->perf_first_frame_ms = now_ms() - t_start;
@@ -1084,8 +1090,8 @@ int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *text
                         hst[b] ? "eos" : "max_tokens", n, step - 1);
             cur[b] = -1;
             active--;
-            const int u2 = queue_pull(nq, taken, &next_seq, next, user);
-            if (u2 < 0) continue;
+            const int u2 = exhausted ? -1 : queue_pull(nq, taken, &next_seq, next, user);
+            if (u2 < 0) { exhausted = 1; continue; }
             if (PROMPT(b, u2) != 0 || qtts_dev_refill(dev, b) != 0) goto out;
             cur[b] = u2;
             first[b] = step + 1;   /* its frame 0 is the next frame launched */
@@ -1095,6 +1101,20 @@ int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *text
             ctx->queue_refills++;
         }
         if (active == 0) break;
+        if (exhausted && compact && active < rows) {
+            /* every freed slot below the last running one takes that one's state */
+            for (int i = 0; i < rows; i++) {
+                if (cur[i] >= 0) continue;
+                int j = rows - 1;
+                while (j > i && cur[j] < 0) j--;
+                if (j <= i) break;
+                if (qtts_dev_move_slot(dev, j, i) != 0) goto out;
+                cur[i] = cur[j]; first[i] = first[j]; retired[i] = retired[j];
+                cur[j] = -1;
+            }
+            rows = active;
+            if (qtts_dev_set_rows(dev, rows) != 0) goto out;
+        }
         if (ctx->progress_cb) ctx->progress_cb(done_n, nq, ctx->progress_cb_userdata);
     }
 #undef PROMPT
@@ -1130,9 +1150,9 @@ int qwen_tts_generate_queue(qwen_tts_ctx_t *ctx, int nq, const char *const *text
     }
     ctx->perf_total_ms = now_ms() - t_start;
     if (qwen_tts_verbose >= 1)
-        fprintf(stderr, "Queue: %d utterances on %d slots, %d frames, %d refills, slot occupancy %.3f\n", done_n, ns,
-                ctx->queue_frames_launched, ctx->queue_refills,
-                (double)ctx->queue_slot_frames_used / ((double)ns * ctx->queue_frames_launched));
+        fprintf(stderr, "Queue: %d utterances on %d slots, %d frames (%lld slot rows), %d refills, occupancy %.3f\n",
+                done_n, ns, ctx->queue_frames_launched, ctx->queue_rows_launched, ctx->queue_refills,
+                (double)ctx->queue_slot_frames_used / (double)ctx->queue_rows_launched);
 out:
     if (pr)
         for (int i = 0; i < nq; i++) { free(pr[i].text); free(pr[i].plan); }

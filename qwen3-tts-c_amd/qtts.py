@@ -62,7 +62,7 @@ class Ctx(C.Structure):  # qwen_tts_ctx_t (include/qwen_tts.h)
         ("tokenizer", C.c_void_p),
         ("queue_n", C.c_int), ("queue_codes", C.POINTER(_ip)), ("queue_frames", _ip), ("queue_stop_reason", _ip),
         ("queue_slot", _ip), ("queue_slots", C.c_int), ("queue_frames_launched", C.c_int),
-        ("queue_refills", C.c_int), ("queue_slot_frames_used", C.c_longlong),
+        ("queue_refills", C.c_int), ("queue_slot_frames_used", C.c_longlong), ("queue_rows_launched", C.c_longlong),
     ]
 
 
@@ -88,7 +88,7 @@ EXPORTS = [
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
     "qtts_dev_codec_async_end", "qtts_dev_codec_multi", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",
     "qtts_dev_encode_audio", "qwen_tts_generate_queue", "qwen_tts_queue_codes", "qtts_dev_reserve", "qtts_dev_refill",
-    "qtts_dev_retire", "qtts_dev_frame_stops",
+    "qtts_dev_retire", "qtts_dev_frame_stops", "qtts_dev_move_slot", "qtts_dev_set_rows",
 ]
 
 _LIB = None
@@ -474,9 +474,12 @@ class QwenTTS:
         c = self.c
         n = c.queue_n
         launched = c.queue_frames_launched
+        rl = int(c.queue_rows_launched)
         return {"slots": c.queue_slots, "frames": launched, "refills": c.queue_refills,
-                "used": int(c.queue_slot_frames_used),
-                "occupancy": (c.queue_slot_frames_used / (c.queue_slots * launched)) if launched and c.queue_slots else 0.0,
+                "used": int(c.queue_slot_frames_used), "rows_launched": rl,
+                "occupancy": (c.queue_slot_frames_used / rl) if rl else 0.0,
+                "occupancy_full_width": (c.queue_slot_frames_used / (c.queue_slots * launched))
+                if launched and c.queue_slots else 0.0,
                 "stop_reason": [c.queue_stop_reason[i] for i in range(n)] if n else [],
                 "frames_per_utt": [c.queue_frames[i] for i in range(n)] if n else [],
                 "slot": [c.queue_slot[i] for i in range(n)] if n else []}

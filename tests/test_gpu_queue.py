@@ -101,6 +101,8 @@ def test_queue_tiny_eos_refill_matches_single_runs(tiny_eos):
     assert st["used"] == sum(st["frames_per_utt"]), st
     # the set mixes EOS stops (5 to 17 frames) and the max_new_tokens cap (utterance 9)
     assert set(st["stop_reason"]) == {1, 2}, st
+    # the tail ran compacted (fewer rows than slots x frames)
+    assert st["rows_launched"] < 3 * st["frames"], st
     _tiny_check(m, o, prompts, audio, 32, 0, 7)
 
 
@@ -174,11 +176,15 @@ def _eos_check(m, audio, g, man, i, u, what):
                  f"{what}: utterance {i} every 16th sample")
 
 
-def test_queue_eos17_two_slots_vs_reference(gpu):
+@pytest.mark.parametrize("compact", ["1", "0"])
+def test_queue_eos17_two_slots_vs_reference(gpu, monkeypatch, compact):
     """The reference's three full-size EOS utterances (stops 157 / 395 / 218)
     on 2 slots: the third starts in the slot the first frees at its step 157,
-    inside the live batch; every utterance's stop step and codes equal its own
-    reference run."""
+    inside the live batch; once it stops, nothing is left to admit, so the
+    second utterance's state moves to slot 0 and its last frames run as a
+    batch of one (QTTS_QUEUE_COMPACT=0: on its own slot in the batch of 2).
+    Every utterance's stop step and codes equal its own reference run."""
+    monkeypatch.setenv("QTTS_QUEUE_COMPACT", compact)
     g = np.load(os.path.join(GOLDEN, "long_eos17.npz"))
     man = _man()["eos17"]
     m = qtts.QwenTTS(model_dir("1.7b", eos_gain=man["eos_gain"]))
@@ -189,6 +195,9 @@ def test_queue_eos17_two_slots_vs_reference(gpu):
         assert rc == 0
         st = m.queue_stats()
         assert st["refills"] == 1 and st["slot"][2] == 0, st
+        # (compacted: utterance 1 finishes on slot 0, its tail frames one row each)
+        assert st["slot"][1] == (0 if compact == "1" else 1), st
+        assert (st["rows_launched"] < 2 * st["frames"]) == (compact == "1"), st
         for i in range(3):
             _eos_check(m, audio, g, man, i, i, "eos17 on 2 slots")
     finally:
