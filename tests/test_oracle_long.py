@@ -55,7 +55,8 @@ def test_long_fixtures_describe_the_bench_workloads():
     """The round-5 reference fixtures hold what bench.py runs (no compute):
     long_17b_b8bench = rank 0's 8 utterances of `bench.py --batch 8`
     (rank_prompt_seeds), long_eos17 = the P128 prompts of bench.py --eos's
-    model with each slot's codes up to the reference's EOS stop."""
+    model with each slot's codes up to the reference's EOS stop (and
+    long_eos17q three more of them)."""
     import bench
     from synth_model import prompt_ids
     man = json.load(open(os.path.join(GOLDEN, "long_manifest.json")))
@@ -74,3 +75,11 @@ def test_long_fixtures_describe_the_bench_workloads():
         np.testing.assert_array_equal(e["prompt_ids"][b, :n], prompt_ids("p128", sd))
         assert (e["codes"][b, :T] >= 0).all() and (e["codes"][b, T:] == -1).all()
     assert len(set(int(x) for x in e["stop_step"])) == len(m["prompt_seeds"])   # the batch test needs rows stopping apart
+    # long_eos17q: three more utterances of the same model for the work-queue test
+    q = np.load(os.path.join(GOLDEN, "long_eos17q.npz"))
+    m = man["eos17q"]
+    assert m["eos_gain"] == bench.EOS_GAIN and m["max_tokens"] > max(int(x) for x in q["stop_step"])
+    for b, sd in enumerate(m["prompt_seeds"]):
+        n, T = int(q["prompt_len"][b]), int(q["stop_step"][b])
+        np.testing.assert_array_equal(q["prompt_ids"][b, :n], prompt_ids("p128", sd))
+        assert (q["codes"][b, :T] >= 0).all() and (q["codes"][b, T:] == -1).all()
