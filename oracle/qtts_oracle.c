@@ -54,6 +54,11 @@ typedef struct {
     /* talker state */
     float *kv_k, *kv_v; int kv_len, kv_max;
     float *tk_x;                       /* post-norm hidden of the last token */
+    /* draw trace (tests/divergence.py): the sampler inputs of ONE draw of a
+     * generation -- frame tr_f, group tr_g (0: the talker's code-0 draw) */
+    int tr_f, tr_g, tr_done, tr_frame, tr_n, tr_xn, tr_result;
+    float tr_rng;
+    float *tr_logits, *tr_x;           /* the logits handed to the sampler, the head's input row */
 } orc_t;
 
 static float bf(uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return f; }
@@ -79,6 +84,7 @@ static float *f32copy(const tens_t *t) {
 
 API orc_t *orc_create(const int *dims, const float *fp) {
     orc_t *m = calloc(1, sizeof(orc_t));
+    m->tr_f = -1;
     memcpy(m->d, dims, sizeof(m->d));
     memcpy(m->f, fp, sizeof(m->f));
     return m;
@@ -95,6 +101,7 @@ API void orc_free(orc_t *m) {
     for (int i = 0; i < 32; i++) free(m->cb_emb[i]);
     for (int i = 0; i < m->n_snake; i++) { free(m->snake_a[i]); free(m->snake_b[i]); }
     free(m->kv_k); free(m->kv_v); free(m->tk_x);
+    free(m->tr_logits); free(m->tr_x);
     free(m);
 }
 
@@ -505,6 +512,31 @@ API void orc_talker_head(orc_t *m, const float *hidden, float *logits) {   /* Q.
 }
 API int orc_kv_len(orc_t *m) { return m->kv_len; }
 
+/* draw trace: keep the sampler's inputs if (frame, group) is the armed draw */
+static void trace_draw(orc_t *m, int g, const float *lg, int n, const float *x, int xn, float rng) {
+    if (m->tr_f != m->tr_frame || m->tr_g != g || m->tr_done) return;
+    m->tr_logits = realloc(m->tr_logits, (size_t)n * sizeof(float));
+    m->tr_x = realloc(m->tr_x, (size_t)xn * sizeof(float));
+    memcpy(m->tr_logits, lg, (size_t)n * sizeof(float));
+    memcpy(m->tr_x, x, (size_t)xn * sizeof(float));
+    m->tr_n = n; m->tr_xn = xn; m->tr_rng = rng; m->tr_done = 1;
+}
+static void trace_result(orc_t *m, int g, int tok) {
+    if (m->tr_f == m->tr_frame && m->tr_g == g && m->tr_done == 1) { m->tr_result = tok; m->tr_done = 2; }
+}
+/* arm the trace for draw (frame, group) of the next generation */
+API void orc_trace_arm(orc_t *m, int frame, int group) { m->tr_f = frame; m->tr_g = group; m->tr_done = 0; }
+/* the traced draw: 1 if it happened; logits [n], x [xn] (caller-sized by
+ * orc_trace_dims), rng state before the draw (float bits), the drawn id */
+API int orc_trace_dims(orc_t *m, int *n, int *xn) { *n = m->tr_n; *xn = m->tr_xn; return m->tr_done == 2; }
+API int orc_trace_get(orc_t *m, float *logits, float *x, float *rng, int *result) {
+    if (m->tr_done != 2) return 0;
+    memcpy(logits, m->tr_logits, (size_t)m->tr_n * sizeof(float));
+    memcpy(x, m->tr_x, (size_t)m->tr_xn * sizeof(float));
+    *rng = m->tr_rng; *result = m->tr_result;
+    return 1;
+}
+
 /* T.c:539-736: sub-talker for one frame */
 API void orc_subtalker(orc_t *m, const float *hidden, int code0, int top_k, float top_p,
                        float temp, int seed, int *codes) {
@@ -537,7 +569,9 @@ API void orc_subtalker(orc_t *m, const float *hidden, int code0, int top_k, floa
         if (g >= 1) {            /* pass g samples code g from lm_head[g-1] (T.c:716-732) */
             const tens_t *hw = findf(m, "talker.code_predictor.lm_head.%d.weight", g - 1, 0);
             mv_t(lg, hw, x, Vs, Hs);
+            trace_draw(m, g, lg, Vs, x, Hs, rng);
             codes[g] = orc_sample(lg, Vs, top_k, top_p, temp, &rng);
+            trace_result(m, g, codes[g]);
         }
     }
     free(kk); free(vv); free(x); free(emb); free(lg);
@@ -949,7 +983,10 @@ API int orc_generate_from_prompt(orc_t *m, const float *prefill, int P, const fl
         else orc_talker_step(m, nx, lg, NULL);
         for (int i = V - 1024; i < V; i++) if (i != eos) lg[i] = -1e9f;     /* Q.c:1273-1305 */
         orc_rep_penalty(lg, hist, ng, V, pp->rep);
+        m->tr_frame = ng;
+        trace_draw(m, 0, lg, V, m->tk_x, H, rng);
         int tok = orc_sample(lg, V, pp->top_k, pp->top_p, pp->temperature, &rng);
+        trace_result(m, 0, tok);
         if (fixed > 0 && tok == eos && ng < fixed) {                         /* Q.c:1315-1321 */
             float keep = lg[eos];
             lg[eos] = -1e9f;

@@ -223,6 +223,30 @@ __global__ __launch_bounds__(256) void k_mgemm_reduce(GemvArgs a, const float *p
 // on grid.y of one launch).  `inv_scratch` (>= nb floats) receives the
 // per-row 1/rms when a.norm_w is set.  Returns 1 when the shape is not
 // covered (caller uses qtts_gemv), 0 ok, -1 error.
+// (QTTS_HIP_MGEMM_KZ: 1 = no split, n = at most n columns; QTTS_HIP_MGEMM_WG:
+// split while the grid stays within n workgroups)
+static int mgemm_kzmax() {
+    static const int v = [] { const char *e = getenv("QTTS_HIP_MGEMM_KZ"); const int x = e ? atoi(e) : 8;
+                              return x >= 1 && x <= 16 ? x : 8; }();
+    return v;
+}
+static int mgemm_wgmax() {
+    static const int v = [] { const char *e = getenv("QTTS_HIP_MGEMM_WG"); const int x = e ? atoi(e) : 1024;
+                              return x >= 256 && x <= 8192 ? x : 1024; }();
+    return v;
+}
+
+// The split-K partials qtts_mgemm can need, from the same rule it splits by:
+// kz columns x nb rows x R outputs with kz <= kzmax and
+// R / (16 nw) x ceil(nb / 64) x kz <= wgmax, i.e. kz x nb x R <=
+// min(kzmax x rows x R_max, 64 x 16 x 4 x wgmax) (nb / ceil(nb / 64) <= 64, nw <= 4).
+size_t qtts_mgemm_part_elems(size_t rows, size_t widest) {
+    if (mgemm_kzmax() < 2) return 0;
+    const size_t by_rows = (size_t)mgemm_kzmax() * rows * widest;
+    const size_t by_grid = (size_t)64 * 16 * 4 * mgemm_wgmax();
+    return by_rows < by_grid ? by_rows : by_grid;
+}
+
 int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st, float *part, size_t part_elems) {
     if (a.nb < 2 || a.C % 32 || a.R % 16 || a.xcopy || a.table_f32 || (a.norm_w && !inv_scratch) ||
         (a.table && a.norm_w) || (!a.table && (a.ldx % 4 || ((uintptr_t)a.x & 15))) || (a.C % 8))
@@ -234,11 +258,7 @@ int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st, float *par
     // split-K over grid.z while the grid is under 1024 workgroups (one
     // workgroup per CU leaves one wave per SIMD to wait out every K step's
     // loads alone), each column group >= 8 K steps per wave pair
-    // (QTTS_HIP_MGEMM_KZ: 1 = no split, n = at most n columns)
-    static const int kzmax = [] { const char *e = getenv("QTTS_HIP_MGEMM_KZ"); const int v = e ? atoi(e) : 8;
-                                  return v >= 1 && v <= 16 ? v : 8; }();
-    static const int wgmax = [] { const char *e = getenv("QTTS_HIP_MGEMM_WG"); const int v = e ? atoi(e) : 1024;
-                                  return v >= 256 && v <= 8192 ? v : 1024; }();
+    const int kzmax = mgemm_kzmax(), wgmax = mgemm_wgmax();
     int kz = 1;
     const int wgs = a.R / (16 * nw) * nch;
     while (part && 2 * kz <= kzmax && wgs * 2 * kz <= wgmax && a.C % (32 * 2 * kz) == 0 &&

@@ -109,6 +109,8 @@ int qtts_gemvm(const GemvArgs &a, hipStream_t st);
 int qtts_gemvb(const GemvArgs &a, hipStream_t st);
 // multi-row (2..64) projection on the bf16 matrix cores (k_mgemm.hip); 1 = not covered
 int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st, float *part = nullptr, size_t part_elems = 0);
+// split-K partial floats qtts_mgemm may use for `rows` activation rows and outputs <= widest
+size_t qtts_mgemm_part_elems(size_t rows, size_t widest);
 
 struct AttnArgs {
     int mode = 0;                  // 0 decode (fused q/k norm + rope + cache write), 1 cached

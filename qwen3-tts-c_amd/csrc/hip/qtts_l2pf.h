@@ -23,9 +23,13 @@ struct L2PfRegs { unsigned v[QTTS_PF_LOADS]; };
 template <int NT, bool NTL = false>
 __device__ __forceinline__ void qtts_l2pf_issue(const L2Prefetch &p, int b, L2PfRegs &r, const void *fallback) {
     // (b is uniform: a scalar select, no branch between loads)
-    const unsigned char *st = p.base && b < p.nwg ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
-                                                  : reinterpret_cast<const unsigned char *>(fallback);
-    const unsigned m = (1u << p.lg) - 1u, n = (unsigned)p.chunks;
+    const bool tgt = p.base && b < p.nwg;
+    const unsigned char *st = tgt ? p.base + (long long)(b % p.pm) * p.pa + (long long)(b / p.pm) * p.pb
+                                  : reinterpret_cast<const unsigned char *>(fallback);
+    // a workgroup without a target slice (past the next launch's grid, or no
+    // prefetch) re-reads the first 4 B of its fallback line n times: chunk
+    // count 0 sends every offset to 0, whatever the target's row geometry
+    const unsigned m = (1u << p.lg) - 1u, n = tgt ? (unsigned)p.chunks : 0u;
     // offsets first (selects, no exec-masked branches: those made the compiler
     // reuse an in-flight load's registers and wait for every load), then the loads
     unsigned off[QTTS_PF_LOADS];

@@ -658,11 +658,12 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
     dv->pinv_cap = dv->rows_cap > 64 ? dv->rows_cap : 64;
     A(pinv, float, dv->pinv_cap);
     {
-        // 4 K columns of every prefill row at the widest projection, at most 64 M floats
+        // the prefill GEMM's split-K partials, sized by the rule its split
+        // follows (qtts_mgemm_part_elems: 4 M floats = 16 MB at the defaults, fewer
+        // for short prompts); QTTS_HIP_MGEMM_KZ=0: no scratch, no split
         const size_t wide = std::max<size_t>({(size_t)dv->QKV(), (size_t)2 * d.I, (size_t)d.H, (size_t)d.TH});
-        // (QTTS_HIP_MGEMM_KZ=0: no scratch, no split)
         const char *e = getenv("QTTS_HIP_MGEMM_KZ");
-        dv->mpart_elems = e && !strcmp(e, "0") ? 0 : std::min<size_t>((size_t)4 * std::max<size_t>(R, 64) * wide, (size_t)64 << 20);
+        dv->mpart_elems = e && !strcmp(e, "0") ? 0 : qtts_mgemm_part_elems(std::max<size_t>(R, 64), wide);
         if (dv->mpart_elems) A(mpart, float, dv->mpart_elems);
     }
     {

@@ -866,8 +866,10 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             samples[b] = 0;
         }
         if (!hc || !slot || !tj || !bj || !aj || !sj) rc = -1;
-        for (int b = 0; b < nb && rc == 0; b++) {
-            if (ngen[b] <= 0) { rc = -1; break; }
+        /* a slot without frames (or whose codes could not be read) gets no
+         * audio and makes the call return -1; the other slots still decode */
+        for (int b = 0; b < nb && hc && slot && tj && bj && aj && sj; b++) {
+            if (ngen[b] <= 0) { rc = -1; continue; }
             const vclone_t *vc = vcs && vcs[b].ref_codes && vcs[b].n_ref > 0 ? &vcs[b] : NULL;
             slot[nj] = b;
             bj[nj] = b;
@@ -875,18 +877,25 @@ static int run_batch(qwen_tts_ctx_t *ctx, int nb, const char *const *texts, cons
             if (vc) {
                 hc[nj] = (int *)malloc((size_t)tj[nj] * G * sizeof(int));
                 if (!hc[nj] || qtts_dev_get_codes(dev, b, hc[nj] + (size_t)vc->n_ref * G, ngen[b]) != ngen[b]) {
+                    free(hc[nj]);
+                    hc[nj] = NULL;
                     rc = -1;
-                    break;
+                    continue;
                 }
                 memcpy(hc[nj], vc->ref_codes, (size_t)vc->n_ref * G * sizeof(int));
             }
-            codec_log_begin(ctx, tj[nj]);
+            /* (-v lines per slot; the -v -v stage times are taken for a lone
+             * decode only: the lanes of a batch run side by side) */
+            if (qwen_tts_verbose >= 1)
+                fprintf(stderr, "Codec decode: %d timesteps, %d quantizers\n", tj[nj], c->codec_num_quantizers);
             nj++;
         }
-        if (rc == 0 && qtts_dev_codec_multi(dev, nj, (const int *const *)hc, slot, tj, aj, sj) != 0) rc = -1;
-        for (int j = 0; j < nj && rc == 0; j++) {
+        if (nj > 0 && qtts_dev_codec_multi(dev, nj, (const int *const *)hc, slot, tj, aj, sj) != 0) rc = -1;
+        for (int j = 0; j < nj; j++) {
             const int b = bj[j];
-            codec_log_end(ctx, sj[j]);
+            if (qwen_tts_verbose >= 1 && aj[j] && sj[j] > 0)
+                fprintf(stderr, "Codec decode complete: %d samples (%.2f seconds)\n", sj[j],
+                        (float)sj[j] / QWEN_TTS_SAMPLE_RATE);
             if (hc[j]) {
                 cut_reference(aj[j], sj[j], vcs[b].n_ref, tj[j], &audio[b], &samples[b]);
                 aj[j] = NULL;

@@ -83,6 +83,11 @@ def _lib_oracle():
     lib.orc_build_icl_prompt.restype = C.c_int
     lib.orc_build_icl_prompt.argtypes = [C.c_void_p, _ip, C.c_int, _ip, C.c_int, _ip, C.c_int, _fp, C.c_int,
                                          C.c_int, _fp, _fp, _ip]
+    lib.orc_trace_arm.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.orc_trace_dims.restype = C.c_int
+    lib.orc_trace_dims.argtypes = [C.c_void_p, _ip, _ip]
+    lib.orc_trace_get.restype = C.c_int
+    lib.orc_trace_get.argtypes = [C.c_void_p, _fp, _fp, _fp, _ip]
     lib.orc_generate_from_prompt.restype = C.c_int
     lib.orc_generate_from_prompt.argtypes = [C.c_void_p, _fp, C.c_int, _fp, C.c_int, C.POINTER(OrcParams),
                                              _ip, C.c_int, _ip]
@@ -200,6 +205,27 @@ class Oracle:
         n = self.lib.orc_generate_from_prompt(self.h, fptr(pre), pre.shape[0], fptr(tr), tr.shape[0], C.byref(p),
                                               iptr(codes), cap, C.byref(stop))
         return codes[:n].copy(), stop.value
+
+    def trace_draw(self, ids, spk, lang, frame, group, **params):
+        """The sampler's inputs at draw (frame, group) of this utterance's
+        generation (group 0: the talker's code-0 draw; 1..15 the sub-talker's):
+        dict(logits, x = the logit head's input row, rng_bits, result), or
+        None if the generation stopped before it."""
+        self.lib.orc_trace_arm(self.h, int(frame), int(group))
+        self.generate_codes(ids, spk, lang, max_frames=int(frame) + 1, **params)
+        n, xn = C.c_int(0), C.c_int(0)
+        ok = self.lib.orc_trace_dims(self.h, C.byref(n), C.byref(xn))
+        if not ok:
+            self.lib.orc_trace_arm(self.h, -1, -1)
+            return None
+        lg = np.zeros(n.value, np.float32)
+        x = np.zeros(xn.value, np.float32)
+        rng = np.zeros(1, np.float32)
+        res = C.c_int(0)
+        got = self.lib.orc_trace_get(self.h, fptr(lg), fptr(x), fptr(rng), C.byref(res))
+        self.lib.orc_trace_arm(self.h, -1, -1)
+        assert got == 1
+        return {"logits": lg, "x": x, "rng_bits": int(rng.view(np.uint32)[0]), "result": res.value}
 
     def generate_codes(self, ids, spk=-1, lang=-1, max_frames=4096, **params):
         ids = np.ascontiguousarray(ids, dtype=np.int32)

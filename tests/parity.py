@@ -1,0 +1,34 @@
+"""The code-parity bar shared by the GPU tests (test infrastructure):
+bit-exact ids, and on the first divergent code a verdict from
+tests/divergence.py -- an fp near-tie (the reference's own draw there sits
+within rounding of a decision boundary) or a bug."""
+import numpy as np
+
+from divergence import classify, describe
+
+# the oracle replays the utterance up to the divergent frame on the CPU; past
+# this frame the verdict is left to tools/classify_divergence.py (offline)
+CLASSIFY_MAX_FRAME = 48
+
+
+def codes_equal(got, want, what, ctx=None):
+    """ctx (optional): dict(oracle, ids, spk, lang, params) of the utterance
+    -- the oracle's keyword parameters -- to classify a divergence."""
+    assert got is not None, what
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    bad = np.argwhere(got != want)
+    if not len(bad):
+        return
+    f, g = (int(v) for v in bad[0])
+    msg = (f"{what}: first divergent code at frame {f} group {g} "
+           f"(got {got[f, g]}, reference {want[f, g]}; {len(bad)} codes differ)")
+    if ctx is not None:
+        if f > ctx.get("max_frame", CLASSIFY_MAX_FRAME):
+            msg += f"; unclassified here (frame {f}: run tools/classify_divergence.py)"
+        else:
+            try:
+                msg += "; " + describe(classify(ctx["oracle"], ctx["ids"], ctx["spk"], ctx["lang"], f, g,
+                                                ctx["params"], got=int(got[f, g])))
+            except Exception as e:   # the verdict is a diagnostic: never mask the failure itself
+                msg += f"; classification failed ({e!r})"
+    raise AssertionError(msg)

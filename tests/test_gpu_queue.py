@@ -23,6 +23,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, manifest, model_dir
+from parity import codes_equal
 from oracle_py import DEFAULT, Oracle
 from qtts_io import lookup_ids
 from synth_model import prompt_ids
@@ -32,14 +33,8 @@ import qtts
 pytestmark = pytest.mark.gpu
 
 
-def _codes_equal(got, want, what):
-    assert got is not None, what
-    assert got.shape == want.shape, (what, got.shape, want.shape)
-    bad = np.argwhere(got != want)
-    if len(bad):
-        f, g = bad[0]
-        raise AssertionError(f"{what}: first divergent code at frame {f} group {g} "
-                             f"(got {got[f, g]}, reference {want[f, g]}; {len(bad)} codes differ)")
+def _codes_equal(got, want, what, ctx=None):
+    codes_equal(got, want, what, ctx)
 
 
 def _audio_close(a, ref, what, mse_bar=1e-4, max_bar=1e-3):
@@ -82,7 +77,10 @@ def _tiny_check(m, o, prompts, audio, max_tokens, fixed, seed):
     st = m.queue_stats()
     for i, ids in enumerate(prompts):
         want, stop, wav = _single(o, ids, max_tokens, fixed, seed)
-        _codes_equal(m.queue_codes(i), want, f"utterance {i} (slot {st['slot'][i]})")
+        s, l = lookup_ids(o.cfg, "aiden", "english")
+        ctx = dict(oracle=o, ids=ids, spk=s, lang=l,
+                   params=dict(max_tokens=max_tokens, fixed=fixed, seed=seed, **DEFAULT))
+        _codes_equal(m.queue_codes(i), want, f"utterance {i} (slot {st['slot'][i]})", ctx)
         assert st["stop_reason"][i] == stop, (i, st["stop_reason"][i], stop)   # 1 eos, 2 max_tokens
         _audio_close(audio[i], wav, f"utterance {i} audio")
 
