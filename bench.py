@@ -680,9 +680,10 @@ def main():
             fp["first_packet_from_audio_ms"] = m.c.perf_first_packet_ms
     # (the 0.6B line reads the 0.6B profile passes: <tag>_06b_kernel_stats.csv / _pmc.json;
     # a batch-B line its own: <tag>_b8_kernel_stats.csv / _b8_pmc.json)
+    # (a voice-clone line reads its own passes: <tag>_vc8_kernel_stats.csv / _vc8_pmc.json)
     pvar = ("" if args.preset == "1.7b" else args.preset.replace(".", "") + "_") + \
-        (f"b{args.batch}_" if args.batch > 1 else "")
-    roof = None if args.no_profile or vc is not None else profile_roofline(m, qtts.lib(), pvar)
+        (f"vc{args.batch}_" if vc is not None else f"b{args.batch}_" if args.batch > 1 else "")
+    roof = None if args.no_profile else profile_roofline(m, qtts.lib(), pvar)
     hbm = None if args.no_profile else hbm_stream_bw(qtts.lib())
     m.close()
 

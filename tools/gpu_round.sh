@@ -40,6 +40,13 @@ if [ "$MODE" = batch ]; then
   cp $O/b8/kernel_stats.csv $R/profiles/${TAG}_b8_kernel_stats.csv
   cp $O/b8/pmc.json $R/profiles/${TAG}_b8_pmc.json
   cp $O/b8_by_grid.txt $R/profiles/${TAG}_b8_by_grid.txt
+  # the batch-16 line's own passes (<tag>_b16_*, read by bench.py --batch 16)
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/b16/prof -o run -- python3 $R/bench.py --batch 16 --steps 2 --warmup 1 --no-cpu-baseline --no-profile > $O/prof_b16.json 2> $O/prof_b16.err
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/b16/pmc_fetch -o run -- python3 $R/bench.py --batch 16 --no-cpu-baseline --no-profile --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch_b16.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $O/b16/pmc_write -o run -- python3 $R/bench.py --batch 16 --no-cpu-baseline --no-profile --steps 1 --warmup 0 --frames 8 > $O/pmc_write_b16.log 2>&1
+  python3 $R/tools/prof_summary.py $O/b16
+  cp $O/b16/kernel_stats.csv $R/profiles/${TAG}_b16_kernel_stats.csv
+  cp $O/b16/pmc.json $R/profiles/${TAG}_b16_pmc.json
   echo $TAG > $R/profiles/LATEST
   cd $R
   timeout -k 10 600 python bench.py --batch 8 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_b8.json 2> $O/bench_b8.err
@@ -85,7 +92,17 @@ cp $O/bench_06b.json $R/profiles/${TAG}_bench_06b.json
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
 fi
 { [ "$MODE" = core ] || [ "$MODE" = prof1 ]; } && { echo done; exit 0; }
-# BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8
+# BASELINE C5 as stated: voice clone from 5 s reference audio (encoders inside the step), batch 8 --
+# its own rocprof / PMC passes first (<tag>_vc8_*, read by the C5 line's roofline)
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/vc8/prof -o run -- python3 $R/bench.py --voice-clone --batch 8 --steps 2 --warmup 1 --no-cpu-baseline --no-profile > $O/prof_vc8.json 2> $O/prof_vc8.err
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $O/vc8/pmc_fetch -o run -- python3 $R/bench.py --voice-clone --batch 8 --no-cpu-baseline --no-profile --steps 1 --warmup 0 --frames 8 > $O/pmc_fetch_vc8.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $O/vc8/pmc_write -o run -- python3 $R/bench.py --voice-clone --batch 8 --no-cpu-baseline --no-profile --steps 1 --warmup 0 --frames 8 > $O/pmc_write_vc8.log 2>&1
+python3 $R/tools/prof_summary.py $O/vc8
+cp $O/vc8/kernel_stats.csv $R/profiles/${TAG}_vc8_kernel_stats.csv
+cp $O/vc8/pmc.json $R/profiles/${TAG}_vc8_pmc.json
+[ -f $R/profiles/LATEST ] || echo $TAG > $R/profiles/LATEST
+cd $R
 timeout -k 10 900 python bench.py --voice-clone --batch 8 --steps 3 --warmup 1 > $O/bench_vc8.json 2> $O/bench_vc8.err
 cp $O/bench_vc8.json $R/profiles/${TAG}_bench_vc8.json
 # the encoders alone: timings, rocprof stats and the per-(kernel, grid) breakdown
