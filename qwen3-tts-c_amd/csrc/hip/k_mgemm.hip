@@ -219,6 +219,17 @@ __global__ __launch_bounds__(256) void k_mgemm_reduce(GemvArgs a, const float *p
 
 }  // namespace
 
+// (also the prefill GEMM's, k_pgemm.hip)
+int qtts_row_rms(const float *x, int ldx, int rows, int C, float eps, float *inv, hipStream_t st) {
+    hipLaunchKernelGGL(k_row_rms, dim3(rows), dim3(256), 0, st, x, ldx, C, eps, inv);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int qtts_mgemm_reduce(const GemvArgs &a, const float *part, int kz, hipStream_t st) {
+    const int nout = a.epi == EPI_SWIGLU ? a.R / 2 : a.R;
+    hipLaunchKernelGGL(k_mgemm_reduce, dim3((nout + 255) / 256, a.nb), dim3(256), 0, st, a, part, kz);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Multi-row projection on the matrix cores, any number of rows (64-row chunks
 // on grid.y of one launch).  `inv_scratch` (>= nb floats) receives the
 // per-row 1/rms when a.norm_w is set.  Returns 1 when the shape is not

@@ -111,6 +111,15 @@ int qtts_gemvb(const GemvArgs &a, hipStream_t st);
 int qtts_mgemm(const GemvArgs &a, float *inv_scratch, hipStream_t st, float *part = nullptr, size_t part_elems = 0);
 // split-K partial floats qtts_mgemm may use for `rows` activation rows and outputs <= widest
 size_t qtts_mgemm_part_elems(size_t rows, size_t widest);
+int qtts_row_rms(const float *x, int ldx, int rows, int C, float eps, float *inv, hipStream_t st);
+// split-K tail of qtts_mgemm / qtts_pgemm: y = epilogue(sum_z part[z][row][R], z in order)
+int qtts_mgemm_reduce(const GemvArgs &a, const float *part, int kz, hipStream_t st);
+// the talker prefill's projections over > 16 rows (k_pgemm.hip): activations
+// split once into 3 bf16 planes (scratch: qtts_pgemm_plane_elems), then an
+// LDS-tiled 128 x 128 MFMA GEMM; 1 = shape not covered
+int qtts_pgemm(const GemvArgs &a, float *inv_scratch, unsigned short *planes, size_t plane_elems, hipStream_t st,
+               float *part, size_t part_elems);
+size_t qtts_pgemm_plane_elems(size_t rows, size_t K);
 
 struct AttnArgs {
     int mode = 0;                  // 0 decode (fused q/k norm + rope + cache write), 1 cached

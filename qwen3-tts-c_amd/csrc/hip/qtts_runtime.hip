@@ -204,6 +204,10 @@ struct qtts_dev {
     int pinv_cap = 0;
     float *mpart = nullptr;   // split-K partials of the matrix-core projections (k_mgemm_reduce)
     size_t mpart_elems = 0;
+    // the prefill GEMM's activation planes [3][rows][K] bf16 (k_pgemm.hip)
+    unsigned short *pplanes = nullptr;
+    size_t pplanes_elems = 0;
+    bool pgemm = true;       // QTTS_HIP_PGEMM=0: the prefill on k_mgemm (rounds 1-5)
 
     int QKV() const { return (d.NH + 2 * d.KV) * d.HD; }
     int QKVs() const { return (d.NHs + 2 * d.KVs) * d.HDs; }
@@ -443,6 +447,8 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_lpk = lk ? atoi(lk) : 0;
     const char *ao = getenv("QTTS_HIP_ATTN_O");
     dv->attn_o = !(ao && !atoi(ao));
+    const char *pg = getenv("QTTS_HIP_PGEMM");
+    dv->pgemm = !(pg && !atoi(pg));
     const char *tb = getenv("QTTS_HIP_TAB0B");
     dv->tab0b = !(tb && !atoi(tb));
     const char *pf = getenv("QTTS_HIP_L2PF");
@@ -664,7 +670,14 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         const size_t wide = std::max<size_t>({(size_t)dv->QKV(), (size_t)2 * d.I, (size_t)d.H, (size_t)d.TH});
         const char *e = getenv("QTTS_HIP_MGEMM_KZ");
         dv->mpart_elems = e && !strcmp(e, "0") ? 0 : qtts_mgemm_part_elems(std::max<size_t>(R, 64), wide);
+        // (k_pgemm splits K while its 128 x 128 tiles x columns stay under 512:
+        // at most 512 x 128 x 128 partials, 8 columns of every row)
+        if (dv->mpart_elems)
+            dv->mpart_elems = std::max(dv->mpart_elems, std::min<size_t>((size_t)512 * 128 * 128, (size_t)8 * R * wide));
         if (dv->mpart_elems) A(mpart, float, dv->mpart_elems);
+        const size_t kmax = std::max<size_t>({(size_t)d.H, (size_t)d.I, (size_t)d.NH * d.HD});
+        dv->pplanes_elems = dv->pgemm ? qtts_pgemm_plane_elems(R, kmax) : 0;
+        if (dv->pplanes_elems) A(pplanes, unsigned short, dv->pplanes_elems);
     }
     {
         const int gph = d.NH / d.KV;
@@ -776,8 +789,17 @@ static int pgemv(qtts_dev *dv, const GemvArgs &a, int kind) {
 // projection): > 64 rows in one matrix-core launch (64-row chunks on its
 // grid.y), else the matrix-core kernel / batch GEMV / GEMV in chunks of 64 /
 // 16.  Row r of x / y / ids is at r*ldx / r*ldy / r*ids_bstride.
-static int rows_proj(qtts_dev *dv, GemvArgs a, int rows) {
+static int rows_proj(qtts_dev *dv, GemvArgs a, int rows, bool prefill = false) {
     const int xs = a.ldx, ys = a.ldy;
+    // the talker prefill over > 16 rows (voice-clone prompts, long prefills):
+    // activations split once, LDS-tiled MFMA GEMM (k_pgemm.hip;
+    // QTTS_HIP_PGEMM=0: k_mgemm as before)
+    if (prefill && dv->pgemm && rows > 16 && (!a.norm_w || rows <= dv->pinv_cap)) {
+        GemvArgs c = a;
+        c.nb = rows;
+        const int rc = qtts_pgemm(c, dv->pinv, dv->pplanes, dv->pplanes_elems, dv->st, dv->mpart, dv->mpart_elems);
+        if (rc <= 0) return rc;
+    }
     if (rows > 64 && (!a.norm_w || rows <= dv->pinv_cap)) {
         GemvArgs c = a;
         c.nb = rows;
@@ -1446,7 +1468,7 @@ static int prefill_rows(qtts_dev *dv, const std::vector<int> &slots, const std::
         {
             GemvArgs a = gv(ly.wqkv, QKV, d.H, dv->px, d.H, dv->pqkv, QKV, 1, EPI_STORE);
             a.norm_w = ly.in; a.eps = d.eps; a.nt = 0;
-            CKI(rows_proj(dv, a, R));
+            CKI(rows_proj(dv, a, R, true));
         }
         AttnArgs t;
         t.mode = 1; t.qkv = dv->pqkv; t.ld_qkv = QKV; t.qn_w = ly.qn; t.kn_w = ly.kn; t.eps = d.eps;
@@ -1459,13 +1481,13 @@ static int prefill_rows(qtts_dev *dv, const std::vector<int> &slots, const std::
         {
             GemvArgs a = gv(ly.wo, d.H, AD, dv->patt, AD, dv->px, d.H, 1, EPI_RESID);
             a.nt = 0;
-            CKI(rows_proj(dv, a, R));
+            CKI(rows_proj(dv, a, R, true));
             a = gv(ly.wgu, 2 * d.I, d.H, dv->px, d.H, dv->ph, d.I, 1, EPI_SWIGLU);
             a.norm_w = ly.post; a.eps = d.eps; a.nt = 0;
-            CKI(rows_proj(dv, a, R));
+            CKI(rows_proj(dv, a, R, true));
             a = gv(ly.wdown, d.H, d.I, dv->ph, d.I, dv->px, d.H, 1, EPI_RESID);
             a.nt = 0;
-            CKI(rows_proj(dv, a, R));
+            CKI(rows_proj(dv, a, R, true));
         }
     }
     return 0;

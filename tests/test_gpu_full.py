@@ -243,3 +243,60 @@ def test_full_voice_clone_b8_vs_oracle_c5(full_tts, full_oracle):
         T = refs[b].shape[0]
         cut = int(T / (T + len(want)) * full.shape[0])
         _audio_close(audio[b], full[cut:])
+
+
+def test_c5_bench_shape_vs_oracle_fixture(full_tts, monkeypatch):
+    """BASELINE C5 at the bench's own shape: exactly the
+    8 voice-clone utterances `bench.py --voice-clone --vc-codes --batch 8`
+    rank 0 decodes -- 63 reference frames + a 20-id reference text + an
+    x-vector per slot (73 prefill rows each, 584 in the batch's prefill
+    GEMM) -- 32 generated frames per slot, against the oracle's ICL layout
+    (tests/golden/vc_c5_b8.npz, tests/golden/make_golden_vc.py; the reference
+    c/ has no voice clone, so this pin is the oracle's restatement): every
+    slot's 32 x 16 codes bit-exact, its audio within the bar.  Also on the
+    round-5 prefill GEMM (QTTS_HIP_PGEMM=0, a fresh context)."""
+    import os
+    from conftest import GOLDEN
+    from parity import codes_equal
+    from make_golden_vc import bench_inputs
+    g = np.load(os.path.join(GOLDEN, "vc_c5_b8.npz"))
+    inp = bench_inputs(full_tts.cfg.num_code_groups, full_tts.cfg.talker_hidden)
+    T = int(g["frames"])
+    for env in ("1", "0"):
+        m = full_tts
+        if env == "0":
+            monkeypatch.setenv("QTTS_HIP_PGEMM", "0")
+            m = qtts.QwenTTS(model_dir("1.7b"))
+        try:
+            m.set_params(max_tokens=4096, fixed=T, seed=42, **DEFAULT)
+            rc, audio = m.generate_voice_clone_batch([x[0] for x in inp], [x[1] for x in inp], [x[2] for x in inp],
+                                                     [x[3] for x in inp], ["english"] * 8)
+            assert rc == 0
+            codes = m.last_codes_batch(8)
+            for b in range(8):
+                codes_equal(codes[b], g["codes"][b], f"C5 bench-shape slot {b} (PGEMM={env})")
+                assert len(audio[b]) == int(g["audio_len"][b]), (b, len(audio[b]))
+                _audio_close(audio[b][::int(g["audio_stride"])], g["audio_sub"][b])
+                _audio_close(audio[b][-1920:], g["audio_last"][b])
+        finally:
+            if m is not full_tts:
+                m.close()
+
+
+def test_prefill_gemm_matches_round5_gemm(gpu, monkeypatch):
+    """The prefill's tiled GEMM over pre-split activations (k_pgemm) against
+    the round-5 GEMM (k_mgemm, QTTS_HIP_PGEMM=0) on the 1.7B talker: 24 / 97 /
+    300 seeded prompt rows (the 16 < rows <= 64 chunk path, the one-tile and
+    the multi-tile-plus-split-K shapes) -- prefill hidden allclose, the same
+    products summed in another order."""
+    outs = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("QTTS_HIP_PGEMM", env)
+        m = qtts.QwenTTS(model_dir("1.7b"))
+        try:
+            outs[env] = [m.prefill((np.random.default_rng(n).standard_normal((n, m.cfg.talker_hidden)) * 0.5)
+                                   .astype(np.float32)) for n in (24, 97, 300)]
+        finally:
+            m.close()
+    for a, b in zip(outs["1"], outs["0"]):
+        np.testing.assert_allclose(a, b, atol=1e-4, rtol=1e-4)
