@@ -184,9 +184,18 @@ def profile_roofline(m, lib, variant=""):
     cnt, tot_ms, tot_b = gemv[dom]
     avg_ms, avg_bytes = tot_ms / cnt, tot_b / cnt
     rp_us, traffic, src = _rocprof_lookup(dom, variant)
+    # the in-graph span of the same kernel from in-kernel stamps
+    # (tools/graph_spans.py on the stamp build; batch-1 lines only)
+    span = None
+    f = _latest_profile("*graph_spans.json") if not variant else None
+    if f:
+        with open(f) as fh:
+            e = json.load(fh).get(dom)
+        if e:
+            span = dict(e, source=os.path.relpath(f, ROOT))
     kind_of = {nm[i]: int(k[i]) for i in range(n)}
     return dict(kernel=dom, kind=kind_of[dom], launches_per_frame=cnt, avg_bytes=avg_bytes, avg_ms=avg_ms,
-                achieved_GBs=avg_bytes / (avg_ms * 1e-3) / 1e9, rocprof_avg_us=rp_us, traffic=traffic,
+                achieved_GBs=avg_bytes / (avg_ms * 1e-3) / 1e9, rocprof_avg_us=rp_us, traffic=traffic, in_graph=span,
                 profile_src=src, frame_kernel_ms=float(t.sum()), share_ms=share, n_kernels=n,
                 kernels={x: {"launches": e[0], "ms": round(e[1], 4), "GBs": round(e[2] / (e[1] * 1e-3) / 1e9, 1)
                              if e[2] else None} for x, e in sorted(per_kernel.items(), key=lambda kv: -kv[1][1])},
@@ -362,6 +371,21 @@ FRAME_WEIGHT_BYTES = {"1.7b": 3.056e9, "0.6b": 1.107e9}
 KV_BYTES_PER_POS = 114688
 
 
+def shared_queue_next(n, step):
+    """The cross-GPU work queue's admission hook (qwen_tts_generate_queue's
+    `next`): every rank holds the same n utterances and takes the next index
+    from one counter in the process group's store (one atomic add per
+    utterance, no collective on the data path; `step` = [queue pass] keys a
+    fresh counter per pass).  Returns -1 once all n are taken."""
+    import torch.distributed as dist
+    store = dist.distributed_c10d._get_default_store()
+
+    def nxt():
+        i = store.add(f"qtts_queue_{step[0]}", 1) - 1
+        return i if i < n else -1
+    return nxt
+
+
 def eos_frames(eos):
     """frames per utterance of an EOS / queue line (None: fixed-length)"""
     if "frames_per_utterance" in eos:
@@ -478,12 +502,7 @@ def main():
         if args.queue_shared:   # every rank holds the whole list; a store counter hands out indices
             qprompts = [prompt_ids("p128", seed=1234 + i) for i in range(args.queue * ws)]
             if ws > 1:
-                import torch.distributed as dist
-                store = dist.distributed_c10d._get_default_store()
-
-                def qnext():
-                    i = store.add(f"qtts_queue_{qstep[0]}", 1) - 1
-                    return i if i < len(qprompts) else -1
+                qnext = shared_queue_next(len(qprompts), qstep)
         else:
             qprompts = [prompt_ids("p128", seed=sd) for sd in rank_prompt_seeds(rank, args.queue)]
     qstats = []
@@ -594,7 +613,7 @@ def main():
         used = sum(q["used"] for q in qstats)
         launched = sum(q["frames"] for q in qstats)
         rows = sum(q["rows_launched"] for q in qstats)
-        nq_done = sum(sum(1 for f in q["frames_per_utt"] if f > 0) for q in qstats)
+        nq_done = sum(sum(1 for f in q["frames_per_utt"] if f >= 0) for q in qstats)
         qd = dict(utterances_per_step=args.queue * (ws if args.queue_shared else 1), slots=args.batch,
                   shared_across_ranks=bool(args.queue_shared),
                   utterances_this_rank=nq_done, refills=sum(q["refills"] for q in qstats),
@@ -623,7 +642,9 @@ def main():
     audio_total = reduce_sum(ws, samples / 24000.0)
     value = audio_total / el_max
     ms_per_step = el_max / args.steps * 1e3
-    ranks = gather_ranks(ws, dict(rank=rank, device=dev, utterances=args.batch * args.steps, samples=samples,
+    n_utt = (sum(sum(1 for f in q["frames_per_utt"] if f >= 0) for q in qstats) if qstats
+             else args.batch * args.steps)
+    ranks = gather_ranks(ws, dict(rank=rank, device=dev, utterances=n_utt, samples=samples,
                                   frames=samples // 1920, wall_ms=round(el * 1e3, 2)))
 
     # ---- first packet (BASELINE.json metric, configs[2]): streaming generation,
@@ -768,6 +789,11 @@ def main():
                                "rocprof_avg_us": None if roof["rocprof_avg_us"] is None
                                else round(roof["rocprof_avg_us"], 2),
                                "avg_launch_bytes": int(roof["avg_bytes"]),
+                               "in_graph_span_us": roof["in_graph"]["span_us"] if roof.get("in_graph") else None,
+                               "in_graph_period_us": roof["in_graph"]["period_us"] if roof.get("in_graph") else None,
+                               "frac_in_graph_span": round(roof["avg_bytes"] / (roof["in_graph"]["span_us"] * 1e-6) / 1e9
+                                                           / HBM_PEAK_GBS, 4) if roof.get("in_graph") else None,
+                               "in_graph_source": roof["in_graph"]["source"] if roof.get("in_graph") else None,
                                "launches_per_frame": roof["launches_per_frame"],
                                "measured_stream": hbm,
                                "frac_of_measured_read": round(roof["achieved_GBs"] / hbm["read_GBs"], 4) if hbm else None,

@@ -579,6 +579,12 @@ __global__ __launch_bounds__(256) void k_attn_o(const float *rsrc, const int *id
     __shared__ __attribute__((aligned(16))) float att[W2];
     __shared__ float sc[2 * 16];
     const int tid = threadIdx.x, kvh = blockIdx.y, rb = blockIdx.x, b = blockIdx.z;   // b: batch row
+#ifdef QTTS_STAMPS
+    // (stamp builds: the in-graph span of this launch, phases 0 start / 2 dot
+    // done / 3 end per workgroup, read by qtts_dev_get_codes' gm_dbg print)
+    const size_t wgl = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (t.dbg && tid == 0) t.dbg[wgl * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int slot = tid / LPS, sub = tid - slot * LPS;
     const int row = rb * RPW + slot, rowc = row < R ? row : R - 1;
     const int AD = t.NH * HD;
@@ -608,8 +614,14 @@ __global__ __launch_bounds__(256) void k_attn_o(const float *rsrc, const int *id
         acc = fmaf(f[6], x1.z, acc); acc = fmaf(f[7], x1.w, acc);
     }
     acc = group_sum<LPS>(acc);
+#ifdef QTTS_STAMPS
+    if (t.dbg && tid == 0) t.dbg[wgl * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (sub == 0 && row < R) part[((size_t)kvh * gridDim.z + b) * R + row] = acc;
     qtts_l2pf_sink(t.pf, pfr);
+#ifdef QTTS_STAMPS
+    if (t.dbg && tid == 0) t.dbg[wgl * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 }  // namespace

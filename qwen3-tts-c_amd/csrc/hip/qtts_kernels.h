@@ -154,6 +154,9 @@ struct AttnArgs {
     // prologue) instead of the last split's
     int defer = 0;
     L2Prefetch pf;                 // k_attn_o: the next launch's weights
+#ifdef QTTS_STAMPS
+    unsigned long long *dbg = nullptr;   // (stamp builds) k_attn_o: [workgroup][8] start / end, 100 MHz clock
+#endif
     // k_attn_short with a q|k|v table (the batch sub-talker's layer 0): kv
     // head 0's workgroup of row r also copies the input row of id(r) (the
     // table ids above) from xc_tab (fp32) or xc_tab16 (bf16) to xc_dst + r

@@ -1199,6 +1199,9 @@ static int subtalker(qtts_dev *dv) {
             if (tab0b) { t.xc_tab = src.table_f32; t.xc_tab16 = src.table; t.xc_dst = xa; t.xc_n = d.Hs; }
             if (pfm & 1) a.pf = pf_attn_o(dv, ly.wo, d.Hs, d.NHs, d.HDs);
             if (pfm & 2) t.pf = kv_only ? first_op_pf(g + 1) : pf_gemvw(dv, ly.wgu, 2 * d.Is, d.Hs);
+#ifdef QTTS_STAMPS
+            if (sdbg) t.dbg = dv->gm_dbg + 2048 * 8;   // (batch 1: the attention + O launch in the "O / -" slot)
+#endif
             if (dv->attn_o && nb == 1) {
                 if (!tab0) CKI(pgemv(dv, a, PK_GEMV_SUB));
                 if (pend) { std::swap(xa, xb); pend = nullptr; }   // the QKV GEMV wrote xa + partials to xb

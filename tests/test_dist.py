@@ -109,6 +109,73 @@ def test_two_rank_generate_gather_gloo(tiny_dir):
     o.close()
 
 
+def _queue_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    import time
+    step = [0]
+    got = {}
+    for p in range(2):                       # two queue passes: a fresh counter each
+        nxt = bench.shared_queue_next(13, step)
+        mine = []
+        while True:
+            i = nxt()
+            if i < 0:
+                break
+            mine.append(i)
+            time.sleep(0.002 * (rank + 1))   # uneven per-utterance cost
+        got[p] = mine
+        step[0] += 1
+        bench.barrier(ws)
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_shared_queue_counter_gloo():
+    """bench.py --queue-shared on world_size 2 gloo: ranks admit utterance
+    indices from one store counter (qwen_tts_generate_queue's `next` hook);
+    every index of every pass is taken exactly once, by whichever rank asks
+    first -- the slower rank takes fewer."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_queue_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(ws))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for pss in range(2):
+        taken = res[0][pss] + res[1][pss]
+        assert sorted(taken) == list(range(13)), (pss, res)
+        assert res[0][pss] and res[1][pss]
+
+
+@pytest.mark.gpu
+def test_bench_shared_queue_two_ranks(gpu):
+    """`bench.py --gpus 2 --queue 5 --queue-shared --batch 2 --eos` on one box
+    (two ranks sharing the GPU over gloo): the two ranks' queues drain ONE list
+    of 10 EOS-mode utterances between them; every utterance is decoded once."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QTTS_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--preset", "tiny", "--eos",
+                        "--batch", "2", "--queue", "5", "--queue-shared", "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline", "--no-profile"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    qd = line["eos_mode"]["queue"]
+    assert qd["shared_across_ranks"] and qd["utterances_per_step"] == 10
+    assert line["config"]["global_batch"] == 10
+    assert sum(x["utterances"] for x in line["ranks"]) == 10, line["ranks"]
+
+
 @pytest.mark.gpu
 def test_bench_gpus2_self_launch(gpu):
     """`bench.py --gpus 2` starts its own 2 ranks (no external launcher); on a

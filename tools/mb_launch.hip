@@ -33,6 +33,7 @@
 //   hipcc -O3 --offload-arch=gfx950 tools/mb_launch.hip -o tools/mb_launch && tools/mb_launch
 //   (add -mllvm -amdgpu-kernarg-preload-count=16 for the preloaded-kernarg build)
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -87,6 +88,18 @@ __global__ __launch_bounds__(256) void k_x4k_big(Big a) {
     __shared__ float red[4];
     const float s = x4k_body(a.in, red);
     if (threadIdx.x < 4) a.out[blockIdx.x * 4 + threadIdx.x] = s * 0.25f + a.pad[threadIdx.x & 31];
+    stamp_end(a.i, t0);
+}
+// the kernarg-size sweep (--kernarg-sweep): the x4k body through a by-value
+// struct of B bytes
+template <int B>
+struct KB { int i; int pad0; const float *in; float *out; float pad[(B - 24) / 4]; };
+template <int B>
+__global__ __launch_bounds__(256) void k_x4k_kb(KB<B> a) {
+    static_assert(sizeof(KB<B>) == B, "kernarg size");
+    const auto t0 = now();
+    float s = wsum(a.in[threadIdx.x + 256 * 0]);
+    if ((threadIdx.x & 63) == 0) a.out[blockIdx.x * 4 + (threadIdx.x >> 6)] = s + a.pad[0];
     stamp_end(a.i, t0);
 }
 __global__ __launch_bounds__(256) void k_x4k_vgpr(int i, const float *in, float *out) {
@@ -204,21 +217,30 @@ int main(int argc, char **argv) {
     // --quiet: no per-call trace; --no-attr: no hipFuncSetAttribute (64 KB of
     // dynamic LDS is within the default limit); --relaxed: capture in relaxed
     // mode instead of global
-    // --skip-big: leave out x4k_big (a 256-B by-value kernel argument): under
-    // rocprofv3 --kernel-trace the 8th hipGraphLaunch of that variant's graph
-    // faults inside the runtime (host SIGSEGV, round 5: profiles/r05d_mb_launch_fault.txt)
+    // (under rocprofv3 --kernel-trace this tool faults in the 4th variant of a
+    // run, whatever it is -- not the kernarg size: profiles/r06i_mb_launch_fault.txt;
+    // profile at most three variants per run with --only)
     // --reps N: timed replays per variant (default 20); --only a,b: just these
     // variants (fewer dispatch records under the profiler)
-    bool no_attr = false, relaxed = false, skip_big = false;
-    int reps_arg = 20;
+    // --kernarg-sweep: only the x4k body through by-value structs of 128..1024 B
+    // (ascending), each in graphs of --nodes N (default NL) launches -- under
+    // rocprofv3 the first size that faults names the boundary (round 6, VERDICT
+    // r05 #7)
+    // --keep-graphs: keep every variant's graph (exec) alive until exit instead
+    // of destroying it after the variant; --desc: the kernarg sweep largest first
+    bool no_attr = false, relaxed = false, kb_sweep = false, keep = false, desc = false;
+    int reps_arg = 20, nodes = NL;
     const char *only = nullptr;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--quiet")) g_trace = 0;
         if (!strcmp(argv[i], "--no-attr")) no_attr = true;
         if (!strcmp(argv[i], "--relaxed")) relaxed = true;
-        if (!strcmp(argv[i], "--skip-big")) skip_big = true;
         if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps_arg = atoi(argv[++i]);
         if (!strcmp(argv[i], "--only") && i + 1 < argc) only = argv[++i];
+        if (!strcmp(argv[i], "--kernarg-sweep")) kb_sweep = true;
+        if (!strcmp(argv[i], "--keep-graphs")) keep = true;
+        if (!strcmp(argv[i], "--desc")) desc = true;
+        if (!strcmp(argv[i], "--nodes") && i + 1 < argc) nodes = std::max(2, std::min(NL, atoi(argv[++i])));
     }
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -237,6 +259,7 @@ int main(int argc, char **argv) {
     if (!no_attr) CK(hipFuncSetAttribute((const void *)k_x4k_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     static unsigned long long hs[NL][MAXG][2];
 
+    std::vector<std::pair<hipGraph_t, hipGraphExec_t>> kept;
     auto run = [&](const char *name, int grid, auto launch) {
         if (only) {   // comma-separated exact names
             bool hit = false;
@@ -252,9 +275,9 @@ int main(int argc, char **argv) {
         }
         hipGraph_t g;
         hipGraphExec_t ge;
-        if (g_trace) fprintf(stderr, "[mb_launch] variant %s grid %d\n", name, grid);
+        if (g_trace) fprintf(stderr, "[mb_launch] variant %s grid %d nodes %d\n", name, grid, nodes);
         CK(hipStreamBeginCapture(st, relaxed ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal));
-        for (int i = 0; i < NL; ++i) launch(i);
+        for (int i = 0; i < nodes; ++i) launch(i);
         CK(hipStreamEndCapture(st, &g));
         CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
         for (int r = 0; r < 3; ++r) CK(hipGraphLaunch(ge, st));
@@ -271,7 +294,7 @@ int main(int argc, char **argv) {
         CK(hipStreamSynchronize(st));
         CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_st), sizeof(hs)));
         std::vector<double> span, gap, ramp;
-        for (int i = 0; i < NL; ++i) {
+        for (int i = 0; i < nodes; ++i) {
             unsigned long long s0 = ~0ull, s1 = 0, e1v = 0;
             for (int b = 0; b < grid; ++b) {
                 s0 = std::min(s0, hs[i][b][0]);
@@ -280,31 +303,59 @@ int main(int argc, char **argv) {
             }
             span.push_back((e1v - s0) * 0.01);
             ramp.push_back((s1 - s0) * 0.01);
-            if (i + 1 < NL) {
+            if (i + 1 < nodes) {
                 unsigned long long n0 = ~0ull;
                 for (int b = 0; b < grid; ++b) n0 = std::min(n0, hs[i + 1][b][0]);
                 gap.push_back(((double)n0 - (double)e1v) * 0.01);
             }
         }
         auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
-        const bool stamped = hs[NL / 2][0][1] != 0;
-        printf("%-12s grid %3d: %6.2f us/kernel", name, grid, ms * 1e3 / (reps * NL));
+        const bool stamped = hs[nodes / 2][0][1] != 0;
+        printf("%-12s grid %3d: %6.2f us/kernel", name, grid, ms * 1e3 / (reps * nodes));
+        fflush(stdout);
         if (stamped) printf("   span %5.2f  ramp %5.2f  gap %5.2f  (span+gap %5.2f)", med(span), med(ramp), med(gap),
                             med(span) + med(gap));
         printf("\n");
         memset(hs, 0, sizeof(hs));
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_st), hs, sizeof(hs)));
-        CK(hipGraphExecDestroy(ge));
-        CK(hipGraphDestroy(g));
+        if (keep) {
+            kept.push_back({g, ge});
+        } else {
+            CK(hipGraphExecDestroy(ge));
+            CK(hipGraphDestroy(g));
+        }
     };
     auto pp = [&](int i, const float *&in, float *&out) { in = (i & 1) ? vb : va; out = (i & 1) ? va : vb; };
+    if (kb_sweep) {
+        auto kb = [&](auto bc) {
+            constexpr int B = decltype(bc)::value;
+            char nm[32];
+            snprintf(nm, sizeof nm, "kb%d", B);
+            run(nm, 256, [&](int i) { KB<B> a{}; a.i = i; pp(i, a.in, a.out);
+                hipLaunchKernelGGL(k_x4k_kb<B>, dim3(256), dim3(256), 0, st, a); });
+        };
+        if (!desc) {
+            kb(std::integral_constant<int, 128>{}); kb(std::integral_constant<int, 192>{});
+            kb(std::integral_constant<int, 224>{}); kb(std::integral_constant<int, 232>{});
+            kb(std::integral_constant<int, 240>{}); kb(std::integral_constant<int, 248>{});
+            kb(std::integral_constant<int, 256>{}); kb(std::integral_constant<int, 264>{});
+            kb(std::integral_constant<int, 288>{}); kb(std::integral_constant<int, 384>{});
+            kb(std::integral_constant<int, 512>{}); kb(std::integral_constant<int, 1024>{});
+        } else {
+            kb(std::integral_constant<int, 1024>{}); kb(std::integral_constant<int, 512>{});
+            kb(std::integral_constant<int, 384>{}); kb(std::integral_constant<int, 288>{});
+            kb(std::integral_constant<int, 264>{}); kb(std::integral_constant<int, 256>{});
+            kb(std::integral_constant<int, 128>{});
+        }
+        for (auto &k : kept) { CK(hipGraphExecDestroy(k.second)); CK(hipGraphDestroy(k.first)); }
+        return 0;
+    }
     for (int grid : {256, 512}) {
         run("empty", grid, [&](int) { hipLaunchKernelGGL(k_empty, dim3(grid), dim3(256), 0, st); });
         run("stamp", grid, [&](int i) { hipLaunchKernelGGL(k_stamp, dim3(grid), dim3(256), 0, st, i); });
         run("x4k", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
             hipLaunchKernelGGL(k_x4k, dim3(grid), dim3(256), 0, st, i, in, out); });
-        if (!skip_big)
-            run("x4k_big", grid, [&](int i) { Big b{}; b.i = i; pp(i, b.in, b.out);
+        run("x4k_big", grid, [&](int i) { Big b{}; b.i = i; pp(i, b.in, b.out);
                 hipLaunchKernelGGL(k_x4k_big, dim3(grid), dim3(256), 0, st, b); });
         run("x4k_vgpr", grid, [&](int i) { const float *in; float *out; pp(i, in, out);
             hipLaunchKernelGGL(k_x4k_vgpr, dim3(grid), dim3(256), 0, st, i, in, out); });
