@@ -1,0 +1,563 @@
+// k_tengine.hip - one talker decoder layer at batch 1 as ONE persistent launch
+// (T.c:478-533 with the attention of T.c:119-248): the weight stream never
+// waits for the layer's hand-offs.
+//
+// The launch-per-op layer (k_gemvw q|k|v -> k_attn_dec -> k_gemvw O with the
+// split merge -> gate|up -> down) leaves HBM idle through the attention
+// (~5 us, no weight bytes) and at every kernel boundary; its in-graph period
+// is ~33 us for 100.7 MB (profiles/r05v_talker_layer_stamps.txt,
+// r06g_graph_spans.json).  Here every workgroup (one per CU, 512 threads)
+// runs two roles side by side:
+//   GEMV waves 0-3   hold their rows' weights in REGISTERS, issued ahead of
+//                    every hand-off they need: q|k|v + O + a third of gate|up
+//                    at the start, the next slices as registers free up; they
+//                    never touch another workgroup's data (their vmcnt queue
+//                    holds weight loads only), so a hand-off never waits
+//                    behind the weight stream.  Inputs come from LDS (flag),
+//                    outputs go to LDS (counter).
+//   comm waves 4-7   gather each op's input vector from 8-byte {tag, value}
+//                    granules (cdna_hip_programming.md Guideline 16 R2: sc1
+//                    stores, relaxed agent-scope sweeps), apply RMSNorm, and
+//                    publish the GEMV waves' outputs as granules; in the
+//                    workgroups of a kv head's splits they also run the
+//                    decode attention (k_attn_dec's arithmetic, 32-key splits,
+//                    partials + ticket, the last split merges in split order
+//                    and publishes the head's output).
+// Every value is computed with the arithmetic of the launch-per-op path
+// (k_gemvw rows: one wave per row, lane chunks l + 64k, wave_sum; its RMS
+// statistic: 256 threads x 2 float4 units, wave sums, red[0..3]; k_attn_dec's
+// QK-norm / RoPE / scores / softmax / P.V; its last-split merge == k_gemvw's
+// deferred merge), so the layer is bit-identical to it.
+// Spins are bounded: a hand-off not seen within ~0.5 s sets *err and the
+// launch runs to its end (garbage, reported by the host), never hangs.
+#include "qtts_common.h"
+#include "qtts_kernels.h"
+
+namespace {
+
+constexpr int H = 2048, NH = 16, KVH = 8, HD = 128, IM = 6144, QKVR = (NH + 2 * KVH) * HD;   // 1.7B talker
+constexpr int GPH = NH / KVH;                       // q heads per kv head
+constexpr int LPK = 8, CH = 256 / LPK, DPL = HD / LPK, D4 = HD / 4, KG = 256 / D4, NO = GPH * HD;
+constexpr int NVC = CH / KG;                        // P.V keys per thread group
+constexpr unsigned SPIN_MAX = 1u << 22;
+
+struct TLds {
+    float xs[H];                  // the GEMV input row: normed x (q|k|v), attention output (O), normed x' (gate|up)
+    float hs[IM];                 // the down projection's input h
+    float hq[4 * HD];             // attention: the head's q0 | q1 | k | v from the q|k|v granules
+    float qk[(GPH + 1) * HD];     // rotated q heads, then k
+    float vv[HD];
+    float sc[GPH][CH];
+    float ml[GPH][2];
+    float red[KG * NO];
+    float cred[4];                // comm RMS partials
+    float outq[16], outo[8], outh[24];
+    int gflag;                    // comm -> GEMV: 1 x staged, 2 attention staged, 3 x' staged, 4 h staged
+    int ocnt;                     // GEMV -> comm: 4 per finished op
+    int cbar;                     // comm waves' own barrier counter
+    int last;
+};
+
+__device__ __forceinline__ float dot8w(const v4u &w, const float *x) {
+    const float4 x0 = *reinterpret_cast<const float4 *>(x);
+    const float4 x1 = *reinterpret_cast<const float4 *>(x + 4);
+    float s = 0.f;
+    s = fmaf(__uint_as_float(w.x << 16), x0.x, s); s = fmaf(__uint_as_float(w.x & 0xFFFF0000u), x0.y, s);
+    s = fmaf(__uint_as_float(w.y << 16), x0.z, s); s = fmaf(__uint_as_float(w.y & 0xFFFF0000u), x0.w, s);
+    s = fmaf(__uint_as_float(w.z << 16), x1.x, s); s = fmaf(__uint_as_float(w.z & 0xFFFF0000u), x1.y, s);
+    s = fmaf(__uint_as_float(w.w << 16), x1.z, s); s = fmaf(__uint_as_float(w.w & 0xFFFF0000u), x1.w, s);
+    return s;
+}
+
+__device__ __forceinline__ int lds_ld(int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void give_up(int *err, int code) {
+    __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// GEMV waves: wait until the comm waves staged input k.  (No global access in
+// here: a store on a divergent path makes the compiler's vmcnt bookkeeping
+// drain the weight loads in flight; a timeout is reported at the end.)
+__device__ __forceinline__ bool gemv_wait(TLds &L, int k) {
+    unsigned n = 0;
+    bool ok = true;
+    while (lds_ld(&L.gflag) < k) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > SPIN_MAX) { ok = false; break; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return ok;
+}
+// GEMV waves: this wave's outputs of the op are in LDS
+__device__ __forceinline__ void gemv_done(TLds &L, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(&L.ocnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// comm waves: barrier among the 4 comm waves only (the GEMV waves keep streaming)
+__device__ __forceinline__ void cbarrier(TLds &L, int &gen, int lane, int *err) {
+    gen += 4;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(&L.cbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    unsigned n = 0;
+    while (lds_ld(&L.cbar) < gen) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > SPIN_MAX) { give_up(err, 2); break; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// comm waves: until the GEMV waves finished op k (4 arrivals per op)
+__device__ __forceinline__ void comm_wait_out(TLds &L, int k, int *err) {
+    unsigned n = 0;
+    while (lds_ld(&L.ocnt) < 4 * k) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > SPIN_MAX) { give_up(err, 20 + k); break; }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// comm waves: every comm wave's LDS writes of input k are done -> the GEMV waves go
+__device__ __forceinline__ void comm_stage(TLds &L, int k, int &gen, int lane, int *err) {
+    cbarrier(L, gen, lane, err);
+    if (threadIdx.x == 256) __hip_atomic_store(&L.gflag, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+typedef unsigned long long u64;
+// diagnostic phase stamps (TLayerArgs::dbg, stamp builds only): 100 MHz wall clock
+__device__ __forceinline__ void te_stamp(const TLayerArgs &a, int k, bool who) {
+#ifdef QTTS_STAMPS
+    if (a.dbg && who) a.dbg[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+__device__ __forceinline__ void put_granule(u64 *g, unsigned tag, float v) {
+    __hip_atomic_store(g, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// comm thread ct sweeps its N granules g[idx(j)] until every tag of the wave
+// is `tag` (the comm waves' vmcnt queue holds no weight loads)
+template <int N, typename Idx>
+__device__ __forceinline__ void sweep(const u64 *g, unsigned tag, Idx idx, float (&v)[N], int *err, int code) {
+    unsigned n = 0;
+    for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const u64 x = __hip_atomic_load(const_cast<u64 *>(g) + idx(j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[j] = __uint_as_float((unsigned)x);
+            ok &= (unsigned)(x >> 32) == tag;
+        }
+        if (__all(ok)) return;
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > SPIN_MAX) { give_up(err, code); return; }
+    }
+}
+
+// RMSNorm of a 2048-float row held as k_gemvw holds it: comm thread ct has
+// units c = 4 (ct + 256 q), q < 2; the statistic in k_gemvw's order
+__device__ __forceinline__ void comm_norm_stage(TLds &L, float4 (&xv)[2], const float *nw, float eps, int ct, int lane,
+                                                int cw, int &gen, int *err) {
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const float4 v = xv[q];
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) L.cred[cw] = ss;
+    cbarrier(L, gen, lane, err);
+    const float inv = rms_inv(L.cred[0] + L.cred[1] + L.cred[2] + L.cred[3], H, eps);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int c = 4 * (ct + 256 * q);
+        const float4 n4 = *reinterpret_cast<const float4 *>(nw + c);
+        float4 v = xv[q];
+        v.x = v.x * inv * n4.x; v.y = v.y * inv * n4.y; v.z = v.z * inv * n4.z; v.w = v.w * inv * n4.w;
+        *reinterpret_cast<float4 *>(L.xs + c) = v;
+    }
+}
+
+// the rows of q|k|v list index i (0..511) of kv head h: q heads 2h, 2h+1, then k h, v h
+__device__ __forceinline__ int qkv_row(int h, int i) {
+    return i < NO ? GPH * HD * h + i : i < NO + HD ? NH * HD + HD * h + (i - NO) : (NH + KVH) * HD + HD * h + (i - NO - HD);
+}
+
+// One decode-attention split of kv head kvh on the comm waves (k_attn_dec<128,
+// 2, 8>'s arithmetic; inputs from L.hq; barriers among the comm waves only).
+// Returns through granules: the head's merged output, by the last split.
+__device__ void comm_attention(TLds &L, const TLayerArgs &a, int kvh, int split, int nact, int p, unsigned tag,
+                               int ct, int lane, int cw, int &gen) {
+    const int n = p + 1;
+    const int t0 = split * CH, t1 = min(n, t0 + CH);
+    const bool owner = (split == nact - 1);
+    const int KVD = KVH * HD;
+    const float *Kc = a.kc + kvh * HD;
+    const float *Vc = a.vc + kvh * HD;
+    // token inputs (from the gathered head) and the RoPE rows, then the cache loads
+    const int hh0 = cw < GPH ? cw : GPH;
+    float hv[2], hw[2], rc[2], rs[2];
+    {
+        const float *src = L.hq + (hh0 < GPH ? hh0 * HD : NO);
+        const float *nw = hh0 < GPH ? a.qn_w : a.kn_w;
+        const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            hv[j] = src[lane + 64 * j];
+            hw[j] = nw[lane + 64 * j];
+            rc[j] = cs[lane + 64 * j];
+            rs[j] = sn[lane + 64 * j];
+        }
+    }
+    const float vtok = L.hq[NO + HD + ct % HD];
+    const int kl = ct / LPK, ksub = ct - kl * LPK;
+    const int tk = t0 + kl;
+    float4 kreg[DPL / 4];
+    {
+        const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(tk < t1 ? tk : t0) * KVD + ksub * DPL);
+#pragma unroll
+        for (int j = 0; j < DPL / 4; ++j) kreg[j] = kp[j];
+    }
+    const int d4 = ct % D4, kg = ct / D4;
+    float4 vreg[NVC];
+#pragma unroll
+    for (int j = 0; j < NVC; ++j) {
+        const int t = t0 + kg + j * KG;
+        const bool ok = kg + j * KG < CH && t < t1;
+        vreg[j] = reinterpret_cast<const float4 *>(Vc + (size_t)(ok ? t : t0) * KVD)[d4];
+    }
+    // QK-norm + RoPE in registers (waves 0..GPH: q heads, then k)
+    if (cw <= GPH) {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) ss += hv[j] * hv[j];
+        ss = wave_sum(ss);
+        const float iv = rms_inv(ss, HD, a.eps);
+        const float n0 = hv[0] * iv * hw[0], n1 = hv[1] * iv * hw[1];
+        L.qk[hh0 * HD + lane] = n0 * rc[0] - n1 * rs[0];
+        L.qk[hh0 * HD + lane + 64] = n1 * rc[1] + n0 * rs[1];
+    }
+    if (owner && ct < HD) L.vv[ct] = vtok;
+    cbarrier(L, gen, lane, a.err);
+    if (owner && ct < HD && !(a.skip && a.skip[0])) {
+        a.kc[(size_t)p * KVD + kvh * HD + ct] = L.qk[GPH * HD + ct];
+        a.vc[(size_t)p * KVD + kvh * HD + ct] = L.vv[ct];
+    }
+    // scores
+    const float scale = div_rn(1.0f, sqrt_rn((float)HD));
+    {
+        float d[GPH];
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) d[g] = 0.f;
+        if (tk < t1) {
+            float4 kv[DPL / 4];
+#pragma unroll
+            for (int j = 0; j < DPL / 4; ++j)
+                kv[j] = (tk == p) ? reinterpret_cast<const float4 *>(L.qk + GPH * HD + ksub * DPL)[j] : kreg[j];
+#pragma unroll
+            for (int g = 0; g < GPH; ++g) {
+                const float4 *q4 = reinterpret_cast<const float4 *>(L.qk + g * HD + ksub * DPL);
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < DPL / 4; ++j) {
+                    const float4 q = q4[j];
+                    s += q.x * kv[j].x + q.y * kv[j].y + q.z * kv[j].z + q.w * kv[j].w;
+                }
+                d[g] = s;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) {
+            d[g] = group_sum<LPK>(d[g]);
+            if (ksub == 0) L.sc[g][kl] = tk < t1 ? d[g] * scale : -INFINITY;
+        }
+    }
+    cbarrier(L, gen, lane, a.err);
+    for (int g = cw; g < GPH; g += 4) {
+        float m = -INFINITY;
+        for (int k = lane; k < CH; k += 64) m = fmaxf(m, L.sc[g][k]);
+        m = wave_max(m);
+        float l = 0.f;
+        for (int k = lane; k < CH; k += 64) {
+            const float e = t0 + k < t1 ? expf(L.sc[g][k] - m) : 0.f;
+            L.sc[g][k] = e;
+            l += e;
+        }
+        l = wave_sum(l);
+        if (lane == 0) { L.ml[g][0] = m; L.ml[g][1] = l; }
+    }
+    cbarrier(L, gen, lane, a.err);
+    {
+        float4 acc[GPH];
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) acc[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < NVC; ++j) {
+            const int k = kg + j * KG;
+            const int t = t0 + k;
+            if (k < CH && t < t1) {
+                const float4 v4 = (t == p) ? reinterpret_cast<const float4 *>(L.vv)[d4] : vreg[j];
+#pragma unroll
+                for (int g = 0; g < GPH; ++g) {
+                    const float pw = L.sc[g][k];
+                    acc[g].x += pw * v4.x; acc[g].y += pw * v4.y; acc[g].z += pw * v4.z; acc[g].w += pw * v4.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < GPH; ++g) reinterpret_cast<float4 *>(L.red + kg * NO + g * HD)[d4] = acc[g];
+    }
+    cbarrier(L, gen, lane, a.err);
+    float res = 0.f;   // NO == 256: one output per comm thread
+    for (int k = 0; k < KG; ++k) res += L.red[k * NO + ct];
+    u64 *gout = a.g_att + (size_t)kvh * NO;
+    if (nact == 1) {
+        put_granule(gout + ct, tag, res / L.ml[ct / HD][1]);
+        return;
+    }
+    // partials (write-through), drained by every comm wave, one ticket per split
+    const int stride = NO + 2 * GPH;
+    float *base = a.part + (size_t)kvh * a.nsplit * stride;
+    float *mine = base + (size_t)split * stride;
+    st_sc1(mine + ct, res);
+    if (ct < GPH) { st_sc1(mine + NO + 2 * ct, L.ml[ct][0]); st_sc1(mine + NO + 2 * ct + 1, L.ml[ct][1]); }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cbarrier(L, gen, lane, a.err);
+    if (ct == 0) {
+        const int old = __hip_atomic_fetch_add(a.cnt + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.last = (old == nact - 1);
+    }
+    cbarrier(L, gen, lane, a.err);
+    if (!L.last) return;
+    // the merge in split order (k_attn_dec's / k_gemvw's deferred merge arithmetic)
+    const int g = ct / HD;
+    float M = -INFINITY;
+    for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, ld_sc1(base + (size_t)s2 * stride + NO + 2 * g));
+    float num = 0.f, den = 0.f;
+    for (int s2 = 0; s2 < nact; ++s2) {
+        const float *ps = base + (size_t)s2 * stride;
+        const float f = expf(ld_sc1(ps + NO + 2 * g) - M);
+        num = fmaf(f, ld_sc1(ps + ct), num);
+        den = fmaf(f, ld_sc1(ps + NO + 2 * g + 1), den);
+    }
+    put_granule(gout + ct, tag, num / den);
+    if (ct == 0) __hip_atomic_store(a.cnt + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the weight slices of the GEMV waves: NR rows x NV 16-B chunks per lane,
+// non-temporal (read once per frame; the sub-talker keeps the Infinity Cache)
+template <int NR, int NV>
+struct Slice {
+    v4u w[NR][NV];
+    __device__ __forceinline__ void load(const bf16_t *W, int C, const int (&rows)[NR], int lane) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const v4u *p = reinterpret_cast<const v4u *>(W + (size_t)rows[r] * C) + lane;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) w[r][k] = __builtin_nontemporal_load(p + 64 * k);
+        }
+    }
+    __device__ __forceinline__ float dot(int r, const float *x, int lane) const {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) s += dot8w(w[r][k], x + 8 * (lane + 64 * k));
+        return wave_sum(s);
+    }
+};
+
+__global__ __launch_bounds__(512, 1) void k_tlayer(TLayerArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    TLds &L = *reinterpret_cast<TLds *>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int b = blockIdx.x;
+    te_stamp(a, 0, threadIdx.x == 0);
+    if (a.err[0]) return;   // an earlier launch timed out: the pass is garbage already, do not wait again
+    if (tid == 0) { L.gflag = 0; L.ocnt = 0; L.cbar = 0; L.last = 0; }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned epoch = (unsigned)a.epoch[0];
+    const unsigned tag = epoch * 32u + (unsigned)a.layer + 1u;   // never 0; unique per (talker pass, layer)
+    const int h = b >> 5, j32 = b & 31;
+
+    if (wv < 4) {
+        // ================= GEMV waves =================
+        const int w = wv;
+        int rq[4], ro[2], rg[3][4], rd[2];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rq[r] = qkv_row(h, 16 * j32 + w + 4 * r);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) { ro[r] = 8 * b + w + 4 * r; rd[r] = 8 * b + w + 4 * r; }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rg[t][r] = 48 * b + w + 4 * (4 * t + r);
+        // the residual rows of the O projection (the layer input), ahead of the weights
+        float yres[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) yres[r] = a.x_in[ro[r]];
+        Slice<4, 4> sq;
+        Slice<2, 4> so;
+        Slice<4, 4> sg0, sg1, sg2;
+        Slice<1, 12> sd0, sd1;
+        const int rd0[1] = {rd[0]}, rd1[1] = {rd[1]};
+        sq.load(a.wqkv, H, rq, lane);
+        so.load(a.wo, H, ro, lane);
+        sg0.load(a.wgu, H, rg[0], lane);
+        // q|k|v rows
+        bool ok = gemv_wait(L, 1);
+        float aq[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) aq[r] = sq.dot(r, L.xs, lane);
+        te_stamp(a, 2, tid == 0);
+        if (lane == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L.outq[w + 4 * r] = aq[r];
+        gemv_done(L, lane);
+        sg1.load(a.wgu, H, rg[1], lane);
+        // O rows + residual
+        ok &= gemv_wait(L, 2);
+        float xm[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) xm[r] = yres[r] + so.dot(r, L.xs, lane);
+        te_stamp(a, 7, tid == 0);
+        if (lane == 0)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) L.outo[w + 4 * r] = xm[r];
+        gemv_done(L, lane);
+        sg2.load(a.wgu, H, rg[2], lane);
+        // gate|up rows, SwiGLU (gate row r and its up row r + 4 in this wave)
+        ok &= gemv_wait(L, 3);
+        float hv[6];
+        {
+            float g0 = sg0.dot(0, L.xs, lane), u0 = sg0.dot(1, L.xs, lane);
+            float g1 = sg0.dot(2, L.xs, lane), u1 = sg0.dot(3, L.xs, lane);
+            hv[0] = (g0 / (1.0f + expf(-g0))) * u0;
+            hv[1] = (g1 / (1.0f + expf(-g1))) * u1;
+        }
+        sd0.load(a.wdown, IM, rd0, lane);   // (the down rows as registers free up)
+        {
+            float g0 = sg1.dot(0, L.xs, lane), u0 = sg1.dot(1, L.xs, lane);
+            float g1 = sg1.dot(2, L.xs, lane), u1 = sg1.dot(3, L.xs, lane);
+            hv[2] = (g0 / (1.0f + expf(-g0))) * u0;
+            hv[3] = (g1 / (1.0f + expf(-g1))) * u1;
+        }
+        sd1.load(a.wdown, IM, rd1, lane);
+        {
+            float g0 = sg2.dot(0, L.xs, lane), u0 = sg2.dot(1, L.xs, lane);
+            float g1 = sg2.dot(2, L.xs, lane), u1 = sg2.dot(3, L.xs, lane);
+            hv[4] = (g0 / (1.0f + expf(-g0))) * u0;
+            hv[5] = (g1 / (1.0f + expf(-g1))) * u1;
+        }
+        te_stamp(a, 10, tid == 0);
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) L.outh[6 * w + k] = hv[k];
+        gemv_done(L, lane);
+        // down rows + residual -> the layer output (read by the next launch)
+        ok &= gemv_wait(L, 4);
+        float xo[2];
+        xo[0] = xm[0] + sd0.dot(0, L.hs, lane);
+        xo[1] = xm[1] + sd1.dot(0, L.hs, lane);
+        if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) a.x_out[rd[r]] = xo[r];
+            if (!ok) give_up(a.err, 10);
+        }
+        te_stamp(a, 12, tid == 0);
+        return;
+    }
+
+    // ================= comm waves =================
+    const int ct = tid - 256, cw = wv - 4;
+    int gen = 0;
+    const int p = a.pos[0];                        // the token's position (kv_len before this step)
+    const int nact = (p + 1 + CH - 1) / CH;
+    // 1. x (the layer input) -> RMSNorm (input_layernorm) -> LDS
+    {
+        float4 xv[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) xv[q] = *reinterpret_cast<const float4 *>(a.x_in + 4 * (ct + 256 * q));
+        comm_norm_stage(L, xv, a.in_norm, a.eps, ct, lane, cw, gen, a.err);
+        comm_stage(L, 1, gen, lane, a.err);
+        te_stamp(a, 1, ct == 0);
+    }
+    // 2. this workgroup's 16 q|k|v rows -> granules
+    comm_wait_out(L, 1, a.err);
+    if (ct < 16) put_granule(a.g_qkv + qkv_row(h, 16 * j32 + ct), tag, L.outq[ct]);
+    te_stamp(a, 3, ct == 0);
+    // 3. the attention splits of kv head h this workgroup runs (split j32, j32 + 32, ...)
+    if (j32 < nact) {
+        float v[2];   // the head's 512 q|k|v values (index ct + 256 j of the head's list)
+        sweep<2>(a.g_qkv, tag, [&](int j) { return qkv_row(h, ct + 256 * j); }, v, a.err, 3);
+        L.hq[ct] = v[0];
+        L.hq[ct + 256] = v[1];
+        cbarrier(L, gen, lane, a.err);
+        te_stamp(a, 4, ct == 0);
+        for (int s = j32; s < nact; s += 32) {
+            comm_attention(L, a, h, s, nact, p, tag, ct, lane, cw, gen);
+            cbarrier(L, gen, lane, a.err);
+        }
+        te_stamp(a, 5, ct == 0);
+    }
+    // 4. the attention output of every head -> LDS (the O projection's input, no
+    //    norm); granule o = kvh * 256 + g * 128 + d is attention element o itself
+    {
+        float v[8];
+        sweep<8>(a.g_att, tag, [&](int j) { return ct + 256 * j; }, v, a.err, 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) L.xs[ct + 256 * j] = v[j];
+        comm_stage(L, 2, gen, lane, a.err);
+        te_stamp(a, 6, ct == 0);
+    }
+    // 5. this workgroup's 8 x' rows -> granules
+    comm_wait_out(L, 2, a.err);
+    if (ct < 8) put_granule(a.g_x + 8 * b + ct, tag, L.outo[ct]);
+    // 6. x' of every row, in k_gemvw's unit mapping (thread ct: elements
+    //    4 (ct + 256 q) + e) -> RMSNorm (post_attention_layernorm) -> LDS
+    //    (the GEMV waves finished reading xs: this workgroup's O rows are in)
+    {
+        float v[8];
+        sweep<8>(a.g_x, tag, [&](int j) { return 4 * (ct + 256 * (j >> 2)) + (j & 3); }, v, a.err, 5);
+        te_stamp(a, 8, ct == 0);
+        float4 xv[2];
+        xv[0] = make_float4(v[0], v[1], v[2], v[3]);
+        xv[1] = make_float4(v[4], v[5], v[6], v[7]);
+        comm_norm_stage(L, xv, a.post_norm, a.eps, ct, lane, cw, gen, a.err);
+        comm_stage(L, 3, gen, lane, a.err);
+        te_stamp(a, 9, ct == 0);
+    }
+    // 7. this workgroup's 24 h values -> granules (wave w, pair k: gate row 48 b + w + 8 k)
+    comm_wait_out(L, 3, a.err);
+    if (ct < 24) {
+        const int w = ct / 6, k = ct - 6 * (ct / 6);
+        const int r = 48 * b + w + 8 * k;
+        put_granule(a.g_h + (r >> 3) * 4 + (r & 3), tag, L.outh[ct]);
+    }
+    // 8. h of every row -> LDS (the down projection's input)
+    {
+        float v[24];
+        sweep<24>(a.g_h, tag, [&](int j) { return ct + 256 * j; }, v, a.err, 6);
+#pragma unroll
+        for (int j = 0; j < 24; ++j) L.hs[ct + 256 * j] = v[j];
+        comm_stage(L, 4, gen, lane, a.err);
+        te_stamp(a, 11, ct == 0);
+    }
+    // the next talker pass gets new tags (every workgroup read the epoch long ago:
+    // this one waited for all of their h granules)
+    if (a.last_layer && b == 0 && ct == 0)
+        __hip_atomic_store(a.epoch, (int)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace
+
+bool qtts_tlayer_dims_ok(int H_, int NH_, int KV_, int HD_, int I_) {
+    return H_ == H && NH_ == NH && KV_ == KVH && HD_ == HD && I_ == IM;
+}
+size_t qtts_tlayer_lds() { return sizeof(TLds); }
+
+int qtts_tlayer(const TLayerArgs &a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void *)k_tlayer, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(TLds)) !=
+            hipSuccess)
+            return -1;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_tlayer, dim3(256), dim3(512), sizeof(TLds), st, a);
+    qtts_last_kernel = "k_tlayer";
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -121,6 +121,33 @@ int qtts_pgemm(const GemvArgs &a, float *inv_scratch, unsigned short *planes, si
                float *part, size_t part_elems);
 size_t qtts_pgemm_plane_elems(size_t rows, size_t K);
 
+// one 1.7B talker decoder layer at batch 1 as one persistent launch
+// (k_tengine.hip): 256 workgroups x 512 threads, hand-offs through 8-byte
+// {tag, value} granules; x_out may alias x_in
+struct TLayerArgs {
+    const float *x_in = nullptr;
+    float *x_out = nullptr;
+    const bf16_t *wqkv = nullptr, *wo = nullptr, *wgu = nullptr, *wdown = nullptr;
+    const float *in_norm = nullptr, *post_norm = nullptr, *qn_w = nullptr, *kn_w = nullptr;
+    const float *rope_cos = nullptr, *rope_sin = nullptr;
+    float *kc = nullptr, *vc = nullptr;          // this layer's cache, [S][KV*HD]
+    const int *pos = nullptr;                    // kv_len before the step
+    const int *skip = nullptr;                   // stopped: no cache write
+    float eps = 1e-6f;
+    float *part = nullptr;                       // [KV][nsplit][NO + 2 GPH] split partials
+    int *cnt = nullptr;                          // [KV] tickets (0 between launches)
+    int nsplit = 0;
+    unsigned long long *g_qkv = nullptr, *g_att = nullptr, *g_x = nullptr, *g_h = nullptr;
+    int *epoch = nullptr;                        // talker passes so far (tags); bumped by the last layer
+    int *err = nullptr;                          // != 0: a hand-off timed out (code)
+    int layer = 0, last_layer = 0;
+    unsigned long long *dbg = nullptr;           // (QTTS_STAMPS builds) [256][16] phase stamps
+};
+constexpr int QTTS_TE_GRANULES = 4096 + 2048 + 2048 + 6144;   // q|k|v, attention, x', h
+bool qtts_tlayer_dims_ok(int H, int NH, int KV, int HD, int I);
+size_t qtts_tlayer_lds();
+int qtts_tlayer(const TLayerArgs &a, hipStream_t st);
+
 struct AttnArgs {
     int mode = 0;                  // 0 decode (fused q/k norm + rope + cache write), 1 cached
     const float *qkv = nullptr;    // row r: [q NH*HD | k KV*HD | v KV*HD]

@@ -200,6 +200,11 @@ struct qtts_dev {
     // (q|k|v, O, gate|up, down), printed by qtts_dev_get_codes
     int gm_dbg_layer = -1;
     unsigned long long *gm_dbg = nullptr;
+    // QTTS_HIP_TENGINE=1: the batch-1 1.7B talker layer as one persistent
+    // launch (k_tengine.hip); its {tag, value} granules, [epoch, error]
+    bool tengine = false;
+    unsigned long long *te_g = nullptr;
+    int *te_ctl = nullptr;
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
     int pinv_cap = 0;
     float *mpart = nullptr;   // split-K partials of the matrix-core projections (k_mgemm_reduce)
@@ -449,6 +454,14 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     dv->attn_o = !(ao && !atoi(ao));
     const char *pg = getenv("QTTS_HIP_PGEMM");
     dv->pgemm = !(pg && !atoi(pg));
+    const char *te = getenv("QTTS_HIP_TENGINE");
+    if (te && atoi(te)) {
+        // every workgroup of the launch must be resident at once: one per CU, 256 of them
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 256)
+            dv->tengine = true;
+    }
     const char *tb = getenv("QTTS_HIP_TAB0B");
     dv->tab0b = !(tb && !atoi(tb));
     const char *pf = getenv("QTTS_HIP_L2PF");
@@ -691,6 +704,12 @@ static int alloc_state(qtts_dev *dv, int nb, int max_frames, int max_prefill) {
         CK(hipMemsetAsync(dv->att_cnt, 0, B * kvmax * sizeof(int), dv->st));
         A(pf_sink, unsigned, 1);
         A(btick, int, QTTS_GM_TICKS);
+        if (dv->tengine) {
+            A(te_g, unsigned long long, QTTS_TE_GRANULES);
+            CK(hipMemsetAsync(dv->te_g, 0, QTTS_TE_GRANULES * 8, dv->st));
+            A(te_ctl, int, 2);
+            CK(hipMemsetAsync(dv->te_ctl, 0, 2 * sizeof(int), dv->st));
+        }
         CK(hipMemsetAsync(dv->btick, 0, QTTS_GM_TICKS * sizeof(int), dv->st));
         if (dv->gm_dbg_layer >= 0) {
             A(gm_dbg, unsigned long long, 4 * 2048 * 8);
@@ -1004,6 +1023,39 @@ static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH,
     return p;
 }
 
+// the talker layers at batch 1 as persistent launches (k_tengine.hip), each
+// bit-identical to the launch-per-op layer below
+static bool tengine_ok(qtts_dev *dv, int kzo, int kzd) {
+    const qtts_dims_t &d = dv->d;
+    return dv->tengine && dv->te_g && dv->nrun == 1 && !kzo && !kzd && dv->attn_defer &&
+           qtts_tlayer_dims_ok(d.H, d.NH, d.KV, d.HD, d.I) && dv->S > 16 && dv->S % 32 == 0 &&
+           dv->att_nsplit * 32 >= dv->S;
+}
+static int talker_layers_te(qtts_dev *dv) {
+    const qtts_dims_t &d = dv->d;
+    const int NBA = dv->nb, KVD = d.KV * d.HD;
+    for (int l = 0; l < d.L; ++l) {
+        Layer &ly = dv->tl[l];
+        TLayerArgs a;
+        a.x_in = dv->x_tk; a.x_out = dv->x_tk;
+        a.wqkv = ly.wqkv; a.wo = ly.wo; a.wgu = ly.wgu; a.wdown = ly.wdown;
+        a.in_norm = ly.in; a.post_norm = ly.post; a.qn_w = ly.qn; a.kn_w = ly.kn;
+        a.rope_cos = dv->rope_cos; a.rope_sin = dv->rope_sin;
+        a.kc = dv->kc + (size_t)l * NBA * dv->S * KVD; a.vc = dv->vc + (size_t)l * NBA * dv->S * KVD;
+        a.pos = dv->kv_len; a.skip = dv->stopped; a.eps = d.eps;
+        a.part = dv->att_part; a.cnt = dv->att_cnt; a.nsplit = dv->att_nsplit;
+        a.g_qkv = dv->te_g; a.g_att = dv->te_g + 4096; a.g_x = a.g_att + 2048; a.g_h = a.g_x + 2048;
+        a.epoch = dv->te_ctl; a.err = dv->te_ctl + 1;
+        a.layer = l; a.last_layer = l == d.L - 1;
+        if (dv->gm_dbg && (l == dv->gm_dbg_layer || l == dv->gm_dbg_layer + 1))
+            a.dbg = dv->gm_dbg + (size_t)(l - dv->gm_dbg_layer) * 256 * 16;
+        ProfScope ps(dv, PK_GEMV_TALKER, 2.0 * ((double)dv->QKV() * d.H + (double)d.H * d.NH * d.HD + 3.0 * d.I * d.H));
+        CKI(qtts_tlayer(a, dv->st));
+    }
+    dv->tk_xfin = dv->x_tk; dv->tk_pend = nullptr; dv->tk_npend = 0;
+    return 0;
+}
+
 static int talker_layers(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     const int nb = dv->nrun, NBA = dv->nb, QKV = dv->QKV(), AD = d.NH * d.HD, KVD = d.KV * d.HD;
@@ -1011,6 +1063,7 @@ static int talker_layers(qtts_dev *dv) {
     // (the talker's O without split-K at batch 8: 142.0 / 142.6 vs 140.7 / 142.1
     // audio-s/s, within noise; its down without: 135.9 / 135.6, gpurun_out/tkz)
     const int kzo = bsplit_kz(dv, d.H, AD), kzd = bsplit_kz(dv, d.H, d.I);
+    if (tengine_ok(dv, kzo, kzd)) return talker_layers_te(dv);
     float *xa = dv->x_tk, *xb = dv->x_tk2;
     const float *pend = nullptr;
     int npend = 0;
@@ -1669,7 +1722,38 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
     int n = 0;
     CK(hipMemcpyAsync(&n, dv->n_gen + b, 4, hipMemcpyDeviceToHost, dv->st));
     CK(hipStreamSynchronize(dv->st));
-    if (dv->gm_dbg) {   // QTTS_HIP_GM_DBG: phase spans of the chosen talker layer's GEMVs, last frame
+    if (dv->te_ctl) {   // the persistent talker layer gave up waiting on a hand-off: its codes are garbage
+        int ctl[2] = {0, 0};
+        CK(hipMemcpy(ctl, dv->te_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+        if (ctl[1]) {
+            fprintf(stderr, "qtts: talker layer engine hand-off timed out (code %d, epoch %d)\n", ctl[1], ctl[0]);
+            return -1;
+        }
+    }
+    if (dv->gm_dbg && dv->te_g) {   // QTTS_HIP_GM_DBG + engine: k_tlayer phase stamps of two layers, last frame
+        std::vector<unsigned long long> h(2 * 256 * 16);
+        CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+        static const char *ph[13] = {"start", "x staged", "qkv dot", "qkv put", "head got", "attn done", "att staged",
+                                     "O dot", "x' got", "x' staged", "gu dot", "h staged", "down dot"};
+        unsigned long long t00 = ~0ull;
+        for (int i = 0; i < 256; ++i) if (h[i * 16] && h[i * 16] < t00) t00 = h[i * 16];
+        for (int g = 0; g < 2; ++g) {
+            const unsigned long long *b = h.data() + (size_t)g * 256 * 16;
+            unsigned long long t0 = ~0ull;
+            for (int i = 0; i < 256; ++i) if (b[i * 16] && b[i * 16] < t0) t0 = b[i * 16];
+            if (t0 == ~0ull) continue;
+            fprintf(stderr, "[te_dbg] layer +%d starts %7.2f us after layer +0\n", g, (t0 - t00) * 0.01);
+            for (int k = 0; k < 13; ++k) {
+                std::vector<double> v;
+                for (int i = 0; i < 256; ++i) if (b[i * 16 + k]) v.push_back((b[i * 16 + k] - t0) * 0.01);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                fprintf(stderr, "[te_dbg] +%d %-10s n %3zu  min %6.2f  med %6.2f  max %6.2f us\n", g, ph[k], v.size(), v[0],
+                        v[v.size() / 2], v.back());
+            }
+        }
+        hipMemsetAsync(dv->gm_dbg, 0, h.size() * 8, dv->st);
+    } else if (dv->gm_dbg) {   // QTTS_HIP_GM_DBG: phase spans of the chosen talker layer's GEMVs, last frame
         std::vector<unsigned long long> h(4 * 2048 * 8);
         CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
         static const char *op[4] = {"q|k|v", "O / -", "gate|up", "down"};
