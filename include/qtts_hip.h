@@ -262,6 +262,9 @@ int qtts_hip_snake_beta(float *out_dev, const float *x_dev, const float *alpha_d
 /* glibc-exact expf replica used by the sampler (for the libm cross-check test) */
 int qtts_hip_expf_glibc(float *out_dev, const float *in_dev, int n, void *stream);
 int qtts_hip_sync(void);
+/* Talker layers enqueued (or captured into a frame graph) on the persistent
+ * one-launch layer (QTTS_HIP_TENGINE=1) since the library loaded. */
+long long qtts_hip_tengine_layers(void);
 
 /* Diagnostics: run ONE frame eagerly on the current generation state with an
  * event pair around every kernel launch on the context stream.  kind[i]:

@@ -56,6 +56,8 @@ struct TLds {
     int ocnt;                     // GEMV -> comm: 4 per finished op
     int cbar;                     // comm waves' own barrier counter
     int last;
+    int full;                     // (ring engine) weight slots landed in the ring, in order
+    int done[4];                  // (ring engine) slots released by consumer wave w
 };
 
 __device__ __forceinline__ float dot8w(const v4u &w, const float *x) {
@@ -359,6 +361,92 @@ struct Slice {
     }
 };
 
+// the comm waves (threads 256..511): input gathers, RMSNorm, the decode
+// attention of this workgroup's kv head splits, the output granules
+__device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid, int lane, int wv, int b) {
+    const unsigned epoch = (unsigned)a.epoch[0];
+    const unsigned tag = epoch * 32u + (unsigned)a.layer + 1u;
+    const int h = b >> 5, j32 = b & 31;
+    const int ct = tid - 256, cw = wv - 4;
+    int gen = 0;
+    const int p = a.pos[0];                        // the token's position (kv_len before this step)
+    const int nact = (p + 1 + CH - 1) / CH;
+    // 1. x (the layer input) -> RMSNorm (input_layernorm) -> LDS
+    {
+        float4 xv[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) xv[q] = *reinterpret_cast<const float4 *>(a.x_in + 4 * (ct + 256 * q));
+        comm_norm_stage(L, xv, a.in_norm, a.eps, ct, lane, cw, gen, a.err);
+        comm_stage(L, 1, gen, lane, a.err);
+        te_stamp(a, 1, ct == 0);
+    }
+    // 2. this workgroup's 16 q|k|v rows -> granules
+    comm_wait_out(L, 1, a.err);
+    if (ct < 16) put_granule(a.g_qkv + qkv_row(h, 16 * j32 + ct), tag, L.outq[ct]);
+    te_stamp(a, 3, ct == 0);
+    // 3. the attention splits of kv head h this workgroup runs (split j32, j32 + 32, ...)
+    if (j32 < nact) {
+        float v[2];   // the head's 512 q|k|v values (index ct + 256 j of the head's list)
+        sweep<2>(a.g_qkv, tag, [&](int j) { return qkv_row(h, ct + 256 * j); }, v, a.err, 3);
+        L.hq[ct] = v[0];
+        L.hq[ct + 256] = v[1];
+        cbarrier(L, gen, lane, a.err);
+        te_stamp(a, 4, ct == 0);
+        for (int s = j32; s < nact; s += 32) {
+            comm_attention(L, a, h, s, nact, p, tag, ct, lane, cw, gen);
+            cbarrier(L, gen, lane, a.err);
+        }
+        te_stamp(a, 5, ct == 0);
+    }
+    // 4. the attention output of every head -> LDS (the O projection's input, no
+    //    norm); granule o = kvh * 256 + g * 128 + d is attention element o itself
+    {
+        float v[8];
+        sweep<8>(a.g_att, tag, [&](int j) { return ct + 256 * j; }, v, a.err, 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) L.xs[ct + 256 * j] = v[j];
+        comm_stage(L, 2, gen, lane, a.err);
+        te_stamp(a, 6, ct == 0);
+    }
+    // 5. this workgroup's 8 x' rows -> granules
+    comm_wait_out(L, 2, a.err);
+    if (ct < 8) put_granule(a.g_x + 8 * b + ct, tag, L.outo[ct]);
+    // 6. x' of every row, in k_gemvw's unit mapping (thread ct: elements
+    //    4 (ct + 256 q) + e) -> RMSNorm (post_attention_layernorm) -> LDS
+    //    (the GEMV waves finished reading xs: this workgroup's O rows are in)
+    {
+        float v[8];
+        sweep<8>(a.g_x, tag, [&](int j) { return 4 * (ct + 256 * (j >> 2)) + (j & 3); }, v, a.err, 5);
+        te_stamp(a, 8, ct == 0);
+        float4 xv[2];
+        xv[0] = make_float4(v[0], v[1], v[2], v[3]);
+        xv[1] = make_float4(v[4], v[5], v[6], v[7]);
+        comm_norm_stage(L, xv, a.post_norm, a.eps, ct, lane, cw, gen, a.err);
+        comm_stage(L, 3, gen, lane, a.err);
+        te_stamp(a, 9, ct == 0);
+    }
+    // 7. this workgroup's 24 h values -> granules (wave w, pair k: gate row 48 b + w + 8 k)
+    comm_wait_out(L, 3, a.err);
+    if (ct < 24) {
+        const int w = ct / 6, k = ct - 6 * (ct / 6);
+        const int r = 48 * b + w + 8 * k;
+        put_granule(a.g_h + (r >> 3) * 4 + (r & 3), tag, L.outh[ct]);
+    }
+    // 8. h of every row -> LDS (the down projection's input)
+    {
+        float v[24];
+        sweep<24>(a.g_h, tag, [&](int j) { return ct + 256 * j; }, v, a.err, 6);
+#pragma unroll
+        for (int j = 0; j < 24; ++j) L.hs[ct + 256 * j] = v[j];
+        comm_stage(L, 4, gen, lane, a.err);
+        te_stamp(a, 11, ct == 0);
+    }
+    // the next talker pass gets new tags (every workgroup read the epoch long ago:
+    // this one waited for all of their h granules)
+    if (a.last_layer && b == 0 && ct == 0)
+        __hip_atomic_store(a.epoch, (int)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(512, 1) void k_tlayer(TLayerArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     TLds &L = *reinterpret_cast<TLds *>(smem);
@@ -461,85 +549,250 @@ __global__ __launch_bounds__(512, 1) void k_tlayer(TLayerArgs a) {
         return;
     }
 
-    // ================= comm waves =================
-    const int ct = tid - 256, cw = wv - 4;
-    int gen = 0;
-    const int p = a.pos[0];                        // the token's position (kv_len before this step)
-    const int nact = (p + 1 + CH - 1) / CH;
-    // 1. x (the layer input) -> RMSNorm (input_layernorm) -> LDS
-    {
-        float4 xv[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) xv[q] = *reinterpret_cast<const float4 *>(a.x_in + 4 * (ct + 256 * q));
-        comm_norm_stage(L, xv, a.in_norm, a.eps, ct, lane, cw, gen, a.err);
-        comm_stage(L, 1, gen, lane, a.err);
-        te_stamp(a, 1, ct == 0);
-    }
-    // 2. this workgroup's 16 q|k|v rows -> granules
-    comm_wait_out(L, 1, a.err);
-    if (ct < 16) put_granule(a.g_qkv + qkv_row(h, 16 * j32 + ct), tag, L.outq[ct]);
-    te_stamp(a, 3, ct == 0);
-    // 3. the attention splits of kv head h this workgroup runs (split j32, j32 + 32, ...)
-    if (j32 < nact) {
-        float v[2];   // the head's 512 q|k|v values (index ct + 256 j of the head's list)
-        sweep<2>(a.g_qkv, tag, [&](int j) { return qkv_row(h, ct + 256 * j); }, v, a.err, 3);
-        L.hq[ct] = v[0];
-        L.hq[ct + 256] = v[1];
-        cbarrier(L, gen, lane, a.err);
-        te_stamp(a, 4, ct == 0);
-        for (int s = j32; s < nact; s += 32) {
-            comm_attention(L, a, h, s, nact, p, tag, ct, lane, cw, gen);
-            cbarrier(L, gen, lane, a.err);
+    comm_role(L, a, tid, lane, wv, b);
+}
+
+// ---------------------------------------------------------------------------
+// The ring engine (QTTS_HIP_TENGINE=2|3): the same layer with the weight stream
+// moved off the GEMV waves' registers onto one LDS-DMA loader wave.
+//
+// r06l's stamps of the register form (profiles/r06l_tengine_stamps.txt) show
+// where it lost: the GEMV waves issue ~160 KB of weight loads per CU at launch
+// start, and every load the comm waves issue after that (the layer input, the
+// granule sweeps, the K/V rows) waits behind them in the CU's memory queue --
+// x staged 7.6 us into the launch, each gather 2.3-5.8 us.  Here the loader
+// keeps at most INFL 16-KB slots in flight (MI355X_MICROARCH.md gather-pass /
+// ldsdma-fill: thin the loader so the gathers are not queued behind it) and
+// runs up to RING slots ahead of the consumers, through every hand-off
+// (prefetch-credit).  A CU's 24 slots per layer, in consumption order:
+//   0-3    q|k|v   4 rows x 4 KB each (the head-grouped rows of k_tlayer)
+//   4-5    O       rows 8b + 4s + w
+//   6-17   gate|up rows 48b + 4m + w (m even: gate, m odd: its up row)
+//   18-23  down    columns [1024 j, 1024 j + 1024) of rows 8b..8b+7, 2 KB each
+// Consumer wave w (0..3) takes row w of every H-wide slot and rows w, w + 4 of
+// the down slots: lane l's chunks l + 64 k in k order, so every row is summed
+// exactly as k_gemvw / k_tlayer sum it (bit-identical outputs).
+constexpr int RING = 6, SLOT = 16384, NSLOT = 24;
+constexpr int RING_THREADS = 576;   // 4 consumer + 4 comm + 1 loader waves
+
+__device__ __forceinline__ unsigned char *ring_base(unsigned char *smem) {
+    return smem + ((sizeof(TLds) + 15) & ~size_t(15));
+}
+// The loader's own LDS words go through inline asm: the compiler counts an
+// LDS-DMA as a pending LDS write, so any LDS access it sees in the loader wave
+// gets an s_waitcnt vmcnt(0) first -- which would drain the stream at every
+// publish.  (The consumers and comm waves issue no LDS-DMA; their LDS accesses
+// stay plain.)
+__device__ __forceinline__ unsigned lds_addr(const void *p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ int min_done(TLds &L) {
+    int d0, d1, d2, d3;
+    asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %4 offset:4\n\tds_read_b32 %2, %4 offset:8\n\t"
+                 "ds_read_b32 %3, %4 offset:12\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(d0), "=v"(d1), "=v"(d2), "=v"(d3)
+                 : "v"(lds_addr(&L.done[0]))
+                 : "memory");
+    return min(min(d0, d1), min(d2, d3));
+}
+__device__ __forceinline__ void publish_full(TLds &L, int n) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(&L.full)), "v"(n) : "memory");
+}
+template <int INFL>
+__device__ __forceinline__ void loader_role(TLds &L, unsigned char *ring, const TLayerArgs &a, int b, int lane) {
+    const int h = b >> 5, j32 = b & 31;
+    bool ok = true;
+    for (int i = 0; i < NSLOT; ++i) {
+        if (i >= RING && min_done(L) < i - RING + 1) {
+            // the ring is full: publish what landed, then wait for slot i - RING's release
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            publish_full(L, i);
+            unsigned n = 0;
+            while (min_done(L) < i - RING + 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++n > SPIN_MAX) { ok = false; break; }
+            }
         }
-        te_stamp(a, 5, ct == 0);
-    }
-    // 4. the attention output of every head -> LDS (the O projection's input, no
-    //    norm); granule o = kvh * 256 + g * 128 + d is attention element o itself
-    {
-        float v[8];
-        sweep<8>(a.g_att, tag, [&](int j) { return ct + 256 * j; }, v, a.err, 4);
+        unsigned char *dst = ring + (i % RING) * SLOT;
+        if (i < 18) {
+            // 4 whole H-wide rows, 4 KB each: piece p = quarter p & 3 of row p >> 2
+            const bf16_t *rb[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) L.xs[ct + 256 * j] = v[j];
-        comm_stage(L, 2, gen, lane, a.err);
-        te_stamp(a, 6, ct == 0);
-    }
-    // 5. this workgroup's 8 x' rows -> granules
-    comm_wait_out(L, 2, a.err);
-    if (ct < 8) put_granule(a.g_x + 8 * b + ct, tag, L.outo[ct]);
-    // 6. x' of every row, in k_gemvw's unit mapping (thread ct: elements
-    //    4 (ct + 256 q) + e) -> RMSNorm (post_attention_layernorm) -> LDS
-    //    (the GEMV waves finished reading xs: this workgroup's O rows are in)
-    {
-        float v[8];
-        sweep<8>(a.g_x, tag, [&](int j) { return 4 * (ct + 256 * (j >> 2)) + (j & 3); }, v, a.err, 5);
-        te_stamp(a, 8, ct == 0);
-        float4 xv[2];
-        xv[0] = make_float4(v[0], v[1], v[2], v[3]);
-        xv[1] = make_float4(v[4], v[5], v[6], v[7]);
-        comm_norm_stage(L, xv, a.post_norm, a.eps, ct, lane, cw, gen, a.err);
-        comm_stage(L, 3, gen, lane, a.err);
-        te_stamp(a, 9, ct == 0);
-    }
-    // 7. this workgroup's 24 h values -> granules (wave w, pair k: gate row 48 b + w + 8 k)
-    comm_wait_out(L, 3, a.err);
-    if (ct < 24) {
-        const int w = ct / 6, k = ct - 6 * (ct / 6);
-        const int r = 48 * b + w + 8 * k;
-        put_granule(a.g_h + (r >> 3) * 4 + (r & 3), tag, L.outh[ct]);
-    }
-    // 8. h of every row -> LDS (the down projection's input)
-    {
-        float v[24];
-        sweep<24>(a.g_h, tag, [&](int j) { return ct + 256 * j; }, v, a.err, 6);
+            for (int r = 0; r < 4; ++r)
+                rb[r] = i < 4 ? a.wqkv + (size_t)qkv_row(h, 16 * j32 + 4 * i + r) * H
+                      : i < 6 ? a.wo + (size_t)(8 * b + 4 * (i - 4) + r) * H
+                              : a.wgu + (size_t)(48 * b + 4 * (i - 6) + r) * H;
 #pragma unroll
-        for (int j = 0; j < 24; ++j) L.hs[ct + 256 * j] = v[j];
-        comm_stage(L, 4, gen, lane, a.err);
-        te_stamp(a, 11, ct == 0);
+            for (int p = 0; p < 16; ++p)
+                __builtin_amdgcn_global_load_lds((const void *)(rb[p >> 2] + 512 * (p & 3) + 8 * lane),
+                                                 (__attribute__((address_space(3))) void *)(dst + 1024 * p), 16, 0, 2);
+        } else {
+            // columns [1024 j, 1024 j + 1024) of the 8 down rows: piece p = half p & 1 of row p >> 1
+            const bf16_t *db = a.wdown + (size_t)(8 * b) * IM + 1024 * (i - 18);
+#pragma unroll
+            for (int p = 0; p < 16; ++p)
+                __builtin_amdgcn_global_load_lds((const void *)(db + (size_t)(p >> 1) * IM + 512 * (p & 1) + 8 * lane),
+                                                 (__attribute__((address_space(3))) void *)(dst + 1024 * p), 16, 0, 2);
+        }
+        if (i >= INFL - 1) {
+            // slots <= i - INFL + 1 landed: at most INFL - 1 slots stay in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(16 * (INFL - 1)) : "memory");
+            publish_full(L, i - INFL + 2);
+        }
     }
-    // the next talker pass gets new tags (every workgroup read the epoch long ago:
-    // this one waited for all of their h granules)
-    if (a.last_layer && b == 0 && ct == 0)
-        __hip_atomic_store(a.epoch, (int)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    te_stamp(a, 13, lane == 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    publish_full(L, NSLOT);
+    if (!ok && lane == 0) give_up(a.err, 11);
+}
+
+__device__ __forceinline__ bool slot_wait(TLds &L, int i) {
+    unsigned n = 0;
+    while (lds_ld(&L.full) <= i) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > SPIN_MAX) return false;
+    }
+    asm volatile("" ::: "memory");
+    return true;
+}
+// the slot's reads have returned to registers: the loader may refill it
+__device__ __forceinline__ void slot_release(TLds &L, int w, int i, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&L.done[w], i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ float dot8r(const v4u &w, const float *x) {   // x: 8 floats in registers
+    float s = 0.f;
+    s = fmaf(__uint_as_float(w.x << 16), x[0], s); s = fmaf(__uint_as_float(w.x & 0xFFFF0000u), x[1], s);
+    s = fmaf(__uint_as_float(w.y << 16), x[2], s); s = fmaf(__uint_as_float(w.y & 0xFFFF0000u), x[3], s);
+    s = fmaf(__uint_as_float(w.z << 16), x[4], s); s = fmaf(__uint_as_float(w.z & 0xFFFF0000u), x[5], s);
+    s = fmaf(__uint_as_float(w.w << 16), x[6], s); s = fmaf(__uint_as_float(w.w & 0xFFFF0000u), x[7], s);
+    return s;
+}
+// x chunks l + 64 k (k < 4) of a 2048-float LDS row into registers
+__device__ __forceinline__ void load_xr(const float *xs, float (&xr)[32], int lane) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 a0 = *reinterpret_cast<const float4 *>(xs + 8 * (lane + 64 * k));
+        const float4 a1 = *reinterpret_cast<const float4 *>(xs + 8 * (lane + 64 * k) + 4);
+        xr[8 * k + 0] = a0.x; xr[8 * k + 1] = a0.y; xr[8 * k + 2] = a0.z; xr[8 * k + 3] = a0.w;
+        xr[8 * k + 4] = a1.x; xr[8 * k + 5] = a1.y; xr[8 * k + 6] = a1.z; xr[8 * k + 7] = a1.w;
+    }
+}
+// row w of the H-wide slot i, dotted with x
+__device__ __forceinline__ float ring_row(TLds &L, const unsigned char *ring, int i, int w, const float (&xr)[32], int lane,
+                                          bool &ok) {
+    ok &= slot_wait(L, i);
+    const v4u *row = reinterpret_cast<const v4u *>(ring + (i % RING) * SLOT + 4096 * w);
+    v4u wr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wr[k] = row[lane + 64 * k];
+    slot_release(L, w, i, lane);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += dot8r(wr[k], xr + 8 * k);
+    return wave_sum(s);
+}
+
+template <int INFL>
+__global__ __launch_bounds__(RING_THREADS, 1) void k_tlayer_ring(TLayerArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    TLds &L = *reinterpret_cast<TLds *>(smem);
+    unsigned char *ring = ring_base(smem);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int b = blockIdx.x;
+    te_stamp(a, 0, threadIdx.x == 0);
+    if (a.err[0]) return;   // an earlier launch timed out: the pass is garbage already, do not wait again
+    if (tid == 0) {
+        L.gflag = 0; L.ocnt = 0; L.cbar = 0; L.last = 0; L.full = 0;
+        L.done[0] = L.done[1] = L.done[2] = L.done[3] = 0;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wv == 8) {
+        loader_role<INFL>(L, ring, a, b, lane);
+        te_stamp(a, 14, lane == 0);
+        return;
+    }
+    if (wv >= 4) {
+        comm_role(L, a, tid, lane, wv, b);
+        return;
+    }
+    // ================= consumer waves =================
+    const int w = wv;
+    float yres[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) yres[r] = a.x_in[8 * b + w + 4 * r];
+    float xr[32];
+    // q|k|v rows
+    bool ok = gemv_wait(L, 1);
+    load_xr(L.xs, xr, lane);
+    float aq[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) aq[s] = ring_row(L, ring, s, w, xr, lane, ok);
+    te_stamp(a, 2, tid == 0);
+    if (lane == 0)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) L.outq[w + 4 * s] = aq[s];
+    gemv_done(L, lane);
+    // O rows + residual
+    ok &= gemv_wait(L, 2);
+    load_xr(L.xs, xr, lane);
+    float xm[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) xm[s] = yres[s] + ring_row(L, ring, 4 + s, w, xr, lane, ok);
+    te_stamp(a, 7, tid == 0);
+    if (lane == 0)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) L.outo[w + 4 * s] = xm[s];
+    gemv_done(L, lane);
+    // gate|up rows, SwiGLU: pair k = (gate slot 6 + 2k, up slot 7 + 2k)
+    ok &= gemv_wait(L, 3);
+    load_xr(L.xs, xr, lane);
+    float hv[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const float g = ring_row(L, ring, 6 + 2 * k, w, xr, lane, ok);
+        const float u = ring_row(L, ring, 7 + 2 * k, w, xr, lane, ok);
+        hv[k] = (g / (1.0f + expf(-g))) * u;
+    }
+    te_stamp(a, 10, tid == 0);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) L.outh[6 * w + k] = hv[k];
+    gemv_done(L, lane);
+    // down rows w, w + 4 + residual -> the layer output (read by the next launch)
+    ok &= gemv_wait(L, 4);
+    float sd[2] = {0.f, 0.f};
+#pragma unroll 1
+    for (int j = 0; j < 6; ++j) {
+        const int i = 18 + j;
+        ok &= slot_wait(L, i);
+        const unsigned char *sl = ring + (i % RING) * SLOT;
+        v4u wr[2][2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) wr[r][k] = reinterpret_cast<const v4u *>(sl + 2048 * (w + 4 * r))[lane + 64 * k];
+        slot_release(L, w, i, lane);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const float *hx = L.hs + 8 * (lane + 64 * (2 * j + k));
+            float x8[8];
+            const float4 a0 = *reinterpret_cast<const float4 *>(hx), a1 = *reinterpret_cast<const float4 *>(hx + 4);
+            x8[0] = a0.x; x8[1] = a0.y; x8[2] = a0.z; x8[3] = a0.w; x8[4] = a1.x; x8[5] = a1.y; x8[6] = a1.z; x8[7] = a1.w;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) sd[r] += dot8r(wr[r][k], x8);
+        }
+    }
+    float xo[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) xo[r] = xm[r] + wave_sum(sd[r]);
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) a.x_out[8 * b + w + 4 * r] = xo[r];
+        if (!ok) give_up(a.err, 12);
+    }
+    te_stamp(a, 12, tid == 0);
 }
 
 }  // namespace
@@ -548,16 +801,29 @@ bool qtts_tlayer_dims_ok(int H_, int NH_, int KV_, int HD_, int I_) {
     return H_ == H && NH_ == NH && KV_ == KVH && HD_ == HD && I_ == IM;
 }
 size_t qtts_tlayer_lds() { return sizeof(TLds); }
+static size_t ring_lds() { return ((sizeof(TLds) + 15) & ~size_t(15)) + (size_t)RING * SLOT; }
 
-int qtts_tlayer(const TLayerArgs &a, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void *)k_tlayer, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(TLds)) !=
-            hipSuccess)
-            return -1;
-        attr = true;
+// mode 1: the register form (k_tlayer); 2 / 3: the ring engine with 1 / 2
+// slots left in flight after each issue (k_tlayer_ring<2> / <3>)
+int qtts_tlayer(const TLayerArgs &a, hipStream_t st, int mode) {
+    static bool attr[4] = {false, false, false, false};
+    const void *fn = mode == 1 ? (const void *)k_tlayer : mode == 2 ? (const void *)k_tlayer_ring<2>
+                                                                    : (const void *)k_tlayer_ring<3>;
+    const size_t lds = mode == 1 ? sizeof(TLds) : ring_lds();
+    if (mode < 1 || mode > 3) return -1;
+    if (!attr[mode]) {
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -1;
+        attr[mode] = true;
     }
-    hipLaunchKernelGGL(k_tlayer, dim3(256), dim3(512), sizeof(TLds), st, a);
-    qtts_last_kernel = "k_tlayer";
+    if (mode == 1) {
+        hipLaunchKernelGGL(k_tlayer, dim3(256), dim3(512), lds, st, a);
+        qtts_last_kernel = "k_tlayer";
+    } else if (mode == 2) {
+        hipLaunchKernelGGL(k_tlayer_ring<2>, dim3(256), dim3(RING_THREADS), lds, st, a);
+        qtts_last_kernel = "k_tlayer_ring<2>";
+    } else {
+        hipLaunchKernelGGL(k_tlayer_ring<3>, dim3(256), dim3(RING_THREADS), lds, st, a);
+        qtts_last_kernel = "k_tlayer_ring<3>";
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -146,7 +146,7 @@ struct TLayerArgs {
 constexpr int QTTS_TE_GRANULES = 4096 + 2048 + 2048 + 6144;   // q|k|v, attention, x', h
 bool qtts_tlayer_dims_ok(int H, int NH, int KV, int HD, int I);
 size_t qtts_tlayer_lds();
-int qtts_tlayer(const TLayerArgs &a, hipStream_t st);
+int qtts_tlayer(const TLayerArgs &a, hipStream_t st, int mode);
 
 struct AttnArgs {
     int mode = 0;                  // 0 decode (fused q/k norm + rope + cache write), 1 cached

@@ -25,6 +25,7 @@
 #include <map>
 #include <set>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "qtts_common.h"
@@ -202,7 +203,7 @@ struct qtts_dev {
     unsigned long long *gm_dbg = nullptr;
     // QTTS_HIP_TENGINE=1: the batch-1 1.7B talker layer as one persistent
     // launch (k_tengine.hip); its {tag, value} granules, [epoch, error]
-    bool tengine = false;
+    int tengine = 0;          // 1 register form, 2 / 3 ring engine (slots in flight 1 / 2)
     unsigned long long *te_g = nullptr;
     int *te_ctl = nullptr;
     float *pinv = nullptr;   // per-row 1/rms scratch of the matrix-core projections
@@ -460,7 +461,7 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
         int dev = 0, ncu = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 256)
-            dv->tengine = true;
+            dv->tengine = std::min(3, std::max(1, atoi(te)));
     }
     const char *tb = getenv("QTTS_HIP_TAB0B");
     dv->tab0b = !(tb && !atoi(tb));
@@ -1027,10 +1028,14 @@ static L2Prefetch pf_attn_o(const qtts_dev *dv, const bf16_t *Wo, int R, int NH,
 // bit-identical to the launch-per-op layer below
 static bool tengine_ok(qtts_dev *dv, int kzo, int kzd) {
     const qtts_dims_t &d = dv->d;
+    // (the launch's 32-key splits need nsplit * 32 >= S partial slots; any S)
     return dv->tengine && dv->te_g && dv->nrun == 1 && !kzo && !kzd && dv->attn_defer &&
-           qtts_tlayer_dims_ok(d.H, d.NH, d.KV, d.HD, d.I) && dv->S > 16 && dv->S % 32 == 0 &&
-           dv->att_nsplit * 32 >= dv->S;
+           qtts_tlayer_dims_ok(d.H, d.NH, d.KV, d.HD, d.I) && dv->S > 16 && dv->att_nsplit * 32 >= dv->S;
 }
+// layer launches enqueued (or captured) on the engine since the library
+// loaded: a test's proof that the engine, not the launch-per-op layer, ran
+static std::atomic<long long> g_tengine_layers{0};
+extern "C" long long qtts_hip_tengine_layers(void) { return g_tengine_layers.load(); }
 static int talker_layers_te(qtts_dev *dv) {
     const qtts_dims_t &d = dv->d;
     const int NBA = dv->nb, KVD = d.KV * d.HD;
@@ -1050,7 +1055,8 @@ static int talker_layers_te(qtts_dev *dv) {
         if (dv->gm_dbg && (l == dv->gm_dbg_layer || l == dv->gm_dbg_layer + 1))
             a.dbg = dv->gm_dbg + (size_t)(l - dv->gm_dbg_layer) * 256 * 16;
         ProfScope ps(dv, PK_GEMV_TALKER, 2.0 * ((double)dv->QKV() * d.H + (double)d.H * d.NH * d.HD + 3.0 * d.I * d.H));
-        CKI(qtts_tlayer(a, dv->st));
+        CKI(qtts_tlayer(a, dv->st, dv->tengine));
+        g_tengine_layers.fetch_add(1);
     }
     dv->tk_xfin = dv->x_tk; dv->tk_pend = nullptr; dv->tk_npend = 0;
     return 0;
@@ -1733,8 +1739,9 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
     if (dv->gm_dbg && dv->te_g) {   // QTTS_HIP_GM_DBG + engine: k_tlayer phase stamps of two layers, last frame
         std::vector<unsigned long long> h(2 * 256 * 16);
         CK(hipMemcpy(h.data(), dv->gm_dbg, h.size() * 8, hipMemcpyDeviceToHost));
-        static const char *ph[13] = {"start", "x staged", "qkv dot", "qkv put", "head got", "attn done", "att staged",
-                                     "O dot", "x' got", "x' staged", "gu dot", "h staged", "down dot"};
+        static const char *ph[15] = {"start", "x staged", "qkv dot", "qkv put", "head got", "attn done", "att staged",
+                                     "O dot", "x' got", "x' staged", "gu dot", "h staged", "down dot", "ld issued",
+                                     "ld landed"};
         unsigned long long t00 = ~0ull;
         for (int i = 0; i < 256; ++i) if (h[i * 16] && h[i * 16] < t00) t00 = h[i * 16];
         for (int g = 0; g < 2; ++g) {
@@ -1743,7 +1750,7 @@ extern "C" int qtts_dev_get_codes(qtts_dev_t *dv, int b, int *host_codes, int ma
             for (int i = 0; i < 256; ++i) if (b[i * 16] && b[i * 16] < t0) t0 = b[i * 16];
             if (t0 == ~0ull) continue;
             fprintf(stderr, "[te_dbg] layer +%d starts %7.2f us after layer +0\n", g, (t0 - t00) * 0.01);
-            for (int k = 0; k < 13; ++k) {
+            for (int k = 0; k < 15; ++k) {
                 std::vector<double> v;
                 for (int i = 0; i < 256; ++i) if (b[i * 16 + k]) v.push_back((b[i * 16 + k] - t0) * 0.01);
                 if (v.empty()) continue;

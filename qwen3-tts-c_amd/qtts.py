@@ -88,7 +88,7 @@ EXPORTS = [
     "qtts_dev_codec_stream_push_host", "qtts_dev_codec_async_begin", "qtts_dev_codec_async_push",
     "qtts_dev_codec_async_end", "qtts_dev_codec_multi", "qtts_dev_enc_config", "qtts_dev_enc_available", "qtts_dev_speaker_embed",
     "qtts_dev_encode_audio", "qwen_tts_generate_queue", "qwen_tts_queue_codes", "qtts_dev_reserve", "qtts_dev_refill",
-    "qtts_dev_retire", "qtts_dev_frame_stops", "qtts_dev_move_slot", "qtts_dev_set_rows",
+    "qtts_dev_retire", "qtts_dev_frame_stops", "qtts_dev_move_slot", "qtts_dev_set_rows", "qtts_hip_tengine_layers",
 ]
 
 _LIB = None
@@ -208,6 +208,7 @@ def lib():
     L.qtts_dev_encode_audio.restype = C.c_int
     L.qtts_dev_encode_audio.argtypes = [C.c_void_p, C.c_int, C.POINTER(_fp), _ip, _ip, C.c_int, _ip, _fp]
     L.qtts_hip_device_count.restype = C.c_int
+    L.qtts_hip_tengine_layers.restype = C.c_longlong
     vp = C.c_void_p
     L.qtts_hip_matvec_bf16.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
     L.qtts_hip_rmsnorm_matvec_bf16.argtypes = [vp, vp, vp, vp, C.c_float, C.c_int, C.c_int, C.c_int, vp]

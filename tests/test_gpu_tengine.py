@@ -1,4 +1,4 @@
-"""The batch-1 talker layer as ONE persistent launch (QTTS_HIP_TENGINE=1,
+"""The batch-1 talker layer as ONE persistent launch (QTTS_HIP_TENGINE=1|2|3,
 k_tengine.hip) against the reference's own outputs.
 
 The engine computes every value with the launch-per-op layer's arithmetic
@@ -37,14 +37,27 @@ def _audio_close(a, ref, what):
     assert mse < 1e-4 and mx < 1e-3, (what, mse, mx)
 
 
-def test_tengine_bench_workload_vs_reference(gpu, monkeypatch):
-    monkeypatch.setenv("QTTS_HIP_TENGINE", "1")
+def _engine_layers():
+    return int(qtts.lib().qtts_hip_tengine_layers())
+
+
+# 1: the register form (k_tlayer); 2 / 3: the LDS-DMA ring engine with 1 / 2
+# weight slots left in flight after each issue (k_tlayer_ring<2> / <3>)
+MODES = [m for m in os.environ.get("QTTS_TEST_TENGINE", "2,3").split(",") if m]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_tengine_bench_workload_vs_reference(gpu, monkeypatch, mode):
+    monkeypatch.setenv("QTTS_HIP_TENGINE", mode)
     g = np.load(os.path.join(GOLDEN, "long_17b.npz"))
     man = _man()["1.7b"]
     m = qtts.QwenTTS(model_dir("1.7b"))
     try:
         m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        n0 = _engine_layers()
         a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
+        # the decode frames ran on the engine (28 layers per captured / enqueued talker pass)
+        assert _engine_layers() - n0 >= 28, "the talker layer engine was not selected"
         codes_equal(m.last_codes(), g["codes"], "engine: 1.7B bench workload")
         _audio_close(a, g["audio"], "engine: 1.7B bench workload waveform")
         # a second utterance on the same context: new tags (epoch), same codes
@@ -55,11 +68,13 @@ def test_tengine_bench_workload_vs_reference(gpu, monkeypatch):
         m.close()
 
 
-def test_tengine_eos_batch_1_vs_reference(gpu, monkeypatch):
-    monkeypatch.setenv("QTTS_HIP_TENGINE", "1")
+@pytest.mark.parametrize("mode", MODES)
+def test_tengine_eos_batch_1_vs_reference(gpu, monkeypatch, mode):
+    monkeypatch.setenv("QTTS_HIP_TENGINE", mode)
     g = np.load(os.path.join(GOLDEN, "long_eos17.npz"))
     man = _man()["eos17"]
     m = qtts.QwenTTS(model_dir("1.7b", eos_gain=man["eos_gain"]))
+    n0 = _engine_layers()
     try:
         for b in range(g["prompt_ids"].shape[0]):
             ids = g["prompt_ids"][b, :int(g["prompt_len"][b])]
@@ -71,5 +86,6 @@ def test_tengine_eos_batch_1_vs_reference(gpu, monkeypatch):
             assert a is not None and len(a) == n * 1920
             sub = a[::man["audio_stride"]]
             _audio_close(sub, g["audio_sub"][b, :len(sub)], f"engine: EOS utterance {b} every 16th sample")
+        assert _engine_layers() - n0 >= 28, "the talker layer engine was not selected"
     finally:
         m.close()
