@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void k_conv(XGemm g) {
 // 8-row groups: conflict-free ds_read_b128 fragments.  The weight planes
 // follow the fp32 relayout in the same allocation (wt_planes).
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int CB_SNAKE_MAX = 1536;   // input channels per split whose SnakeBeta parameters k_convb stages
+constexpr int CB_SNAKE_MAX = 1536;   // input channels per split k_convb takes with SnakeBeta (larger: k_conv)
 
 __device__ __forceinline__ int cb_swz(int row, int half) { return row * 16 + 8 * (half ^ ((row >> 3) & 1)); }
 
@@ -335,8 +335,14 @@ __device__ __forceinline__ void cb_split8(const float (&v)[8], uint4 &p1, uint4 
 
 // WN waves along t (2 or 4): a 64 x 64*WN tile per workgroup of 128*WN
 // threads; the staged weights serve WN waves per 32-row half.
+// (a 128-VGPR bound lets two 8-wave k_convb<7,4> workgroups share a CU now
+// that its LDS fits twice: batch-8 codec 53.1-53.4 -> 51.9-52.0 ms, batch 1
+// 7.87 -> 7.65 ms, one spilled VGPR; profiles/r06p_ab_convb.txt)
+#ifndef QTTS_CONVB_MINB
+#define QTTS_CONVB_MINB 4
+#endif
 template <int KW, int WN>
-__global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
+__global__ __launch_bounds__(128 * WN, QTTS_CONVB_MINB) void k_convb(XGemm g) {
     constexpr int NT = 128 * WN, BNT = 64 * WN;
     const int nzk = g.kz > 1 ? g.kz : 1, ph = blockIdx.z / nzk, kzi = blockIdx.z - ph * nzk;
     const int nph = gridDim.z / nzk, ci = g.K / KW;
@@ -381,13 +387,11 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
     };
     load(cbeg);
     // SnakeBeta of the input channels is applied when a stage is written to
-    // LDS (its loads have landed by then), its parameters staged once
-    __shared__ float Ssa[CB_SNAKE_MAX], Ssb[CB_SNAKE_MAX];
+    // LDS (its loads have landed by then).  Its parameters come through the
+    // scalar cache: an item's 8 channels are wave-uniform (NBW is a multiple
+    // of 64), so no LDS copy of them (12 KB at 1536 channels) is needed.
+    static_assert(NBW % 64 == 0, "k_convb: staged window columns must be whole waves");
     const bool snake = g.sa != nullptr;
-    if (snake) {
-        for (int c = tid; c < cpz; c += NT) { Ssa[c] = g.sa[cbeg + c]; Ssb[c] = g.sb[cbeg + c]; }
-        __syncthreads();
-    }
     const int r = lane & 31, hh = lane >> 5;
     for (int c0 = cbeg; c0 < cend; c0 += CV_BC) {
 #pragma unroll
@@ -403,9 +407,9 @@ __global__ __launch_bounds__(128 * WN) void k_convb(XGemm g) {
             const int e = tid + NT * j, h = e / NBW, x = e - h * NBW;
             if (h < 2) {
                 if (snake) {
-                    const int cl = c0 - cbeg + 8 * h;
+                    const int cu = __builtin_amdgcn_readfirstlane(c0 + 8 * h);
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) rb[j][q] = snake1(rb[j][q], Ssa[cl + q], Ssb[cl + q]);
+                    for (int q = 0; q < 8; ++q) rb[j][q] = snake1(rb[j][q], g.sa[cu + q], g.sb[cu + q]);
                 }
                 uint4 p1, p2, p3;
                 cb_split8(rb[j], p1, p2, p3);

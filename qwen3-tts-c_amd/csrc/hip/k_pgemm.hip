@@ -15,8 +15,9 @@
 //   k_split3  one pass: x (+ RMSNorm, its statistic formed in the same
 //             launch) -> planes [3][Mp][K] (Mp: rows rounded up to the 128-row
 //             tile, pad rows zero).
-//   k_pgemm   a 128 x 128 (rows x weight rows) tile per 256-thread workgroup,
-//             2 x 2 waves of 64 x 64 (2 x 2 MFMA 32x32 tiles each); 32-deep K
+//   k_pgemm   a 128 x 256 (rows x weight rows) tile per 512-thread workgroup,
+//             2 x 4 waves of 64 x 64 (2 x 2 MFMA 32x32 tiles each), or
+//             128 x 128 on 2 x 2 waves for a single row tile; 32-deep K
 //             stages, the loads of the stage after next (8 16-B loads per
 //             thread, two register sets) in flight while this one's 24 MFMAs
 //             run; both operands in LDS, rows of 4
@@ -99,15 +100,23 @@ __global__ __launch_bounds__(256) void k_split3(const float *x, int ldx, int M, 
     }
 }
 
-constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int BM = 128, BK = 32;
 constexpr int A_CH = 3 * BM * (BK / 8);   // 16-B chunks of the three A tiles per stage (1536)
-constexpr int W_CH = BN * (BK / 8);       // of the W tile (512)
-constexpr int A_PT = A_CH / 256, W_PT = W_CH / 256;
 
 // swizzled 16-B chunk index of (row, chunk) in a [rows][4 chunks] tile
 __device__ __forceinline__ int swz(int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); }
 
-__global__ __launch_bounds__(256) void k_pgemm(GemvArgs a, const unsigned short *planes, int Mp, float *part) {
+// WN waves along the weight rows: a 128 x 64 WN tile per workgroup of 2 WN
+// waves (WN = 2: 128 x 128, 256 threads; WN = 4: 128 x 256, 512 threads --
+// every activation stage staged once serves twice the weight rows, which
+// halves the launch's activation-plane reads from L2, the bulk of its traffic
+// while the planes are re-read once per weight tile)
+template <int WN>
+__global__ __launch_bounds__(128 * WN) void k_pgemm(GemvArgs a, const unsigned short *planes, int Mp, float *part) {
+    constexpr int NT = 128 * WN, BN = 64 * WN;
+    constexpr int W_CH = BN * (BK / 8);   // 16-B chunks of the W tile per stage
+    constexpr int A_PT = A_CH / NT, W_PT = W_CH / NT;
+    static_assert(A_CH % NT == 0 && W_CH % NT == 0, "k_pgemm: stage chunks per thread");
     __shared__ __attribute__((aligned(16))) v4u As[2][3 * BM * 4];
     __shared__ __attribute__((aligned(16))) v4u Ws[2][BN * 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -121,7 +130,7 @@ __global__ __launch_bounds__(256) void k_pgemm(GemvArgs a, const unsigned short 
     int la[A_PT];
 #pragma unroll
     for (int j = 0; j < A_PT; ++j) {
-        const int q = tid + 256 * j, p = q / (BM * 4), r = (q / 4) % BM, c = q % 4;
+        const int q = tid + NT * j, p = q / (BM * 4), r = (q / 4) % BM, c = q % 4;
         ga[j] = reinterpret_cast<const v4u *>(planes + ((size_t)p * Mp + m0 + r) * K + (size_t)st0 * BK + 8 * c);
         la[j] = p * BM * 4 + swz(r, c);
     }
@@ -129,7 +138,7 @@ __global__ __launch_bounds__(256) void k_pgemm(GemvArgs a, const unsigned short 
     int lw[W_PT];
 #pragma unroll
     for (int j = 0; j < W_PT; ++j) {
-        const int q = tid + 256 * j, r = q / 4, c = q % 4;
+        const int q = tid + NT * j, r = q / 4, c = q % 4;
         const int row = n0 + r < N ? n0 + r : N - 1;
         gw[j] = reinterpret_cast<const v4u *>(a.W + (size_t)row * K + (size_t)st0 * BK + 8 * c);
         lw[j] = swz(r, c);
@@ -259,14 +268,27 @@ int qtts_pgemm(const GemvArgs &a, float *inv_scratch, unsigned short *planes, si
     hipLaunchKernelGGL(k_split3, dim3(Mp), dim3(256), 0, st, a.x, a.ldx, a.nb, a.C, a.norm_w, a.eps, planes, Mp);
     // split-K while the tiles would not fill the chip (one workgroup per CU
     // cannot hide its own stage loads), each column >= 8 stages
+    // The weight-row width of a workgroup's tile: 256 once there are several
+    // 128-row tiles (the plane re-reads dominate: voice-clone batch-8 prefill
+    // 10.1 -> 9.15 ms), 128 for one row tile (half the weight tiles would need
+    // twice the split-K partials: voice-clone batch-1 prefill 6.87 vs 7.16 ms;
+    // profiles/r06q_ab_pgemm_bn.txt).  QTTS_HIP_PGEMM_BN=128|256 forces one
+    // (read per call: a test switches it between contexts of one process).
+    const char *bne = getenv("QTTS_HIP_PGEMM_BN");
+    const int BN = bne && atoi(bne) == 128 ? 128 : bne && atoi(bne) == 256 ? 256 : Mp >= 2 * BM ? 256 : 128;
     const int tiles = (a.R + BN - 1) / BN * (Mp / BM);
     int kz = 1;
     while (part && tiles * kz < 256 && kz < 8 && (a.C / BK) % (4 * kz) == 0 && a.C / BK / (2 * kz) >= 8 &&
            (size_t)2 * kz * a.nb * a.R <= part_elems)
         kz *= 2;
-    hipLaunchKernelGGL(k_pgemm, dim3((a.R + BN - 1) / BN, Mp / BM, kz), dim3(256), 0, st, a, planes, Mp,
-                       kz > 1 ? part : nullptr);
-    qtts_last_kernel = "k_pgemm";
+    const dim3 grid((a.R + BN - 1) / BN, Mp / BM, kz);
+    if (BN == 256) {
+        hipLaunchKernelGGL(k_pgemm<4>, grid, dim3(512), 0, st, a, planes, Mp, kz > 1 ? part : nullptr);
+        qtts_last_kernel = "k_pgemm<4>";
+    } else {
+        hipLaunchKernelGGL(k_pgemm<2>, grid, dim3(256), 0, st, a, planes, Mp, kz > 1 ? part : nullptr);
+        qtts_last_kernel = "k_pgemm<2>";
+    }
     if (kz > 1 && qtts_mgemm_reduce(a, part, kz, st) != 0) return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

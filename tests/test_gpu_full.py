@@ -254,7 +254,8 @@ def test_c5_bench_shape_vs_oracle_fixture(full_tts, monkeypatch):
     (tests/golden/vc_c5_b8.npz, tests/golden/make_golden_vc.py; the reference
     c/ has no voice clone, so this pin is the oracle's restatement): every
     slot's 32 x 16 codes bit-exact, its audio within the bar.  Also on the
-    round-5 prefill GEMM (QTTS_HIP_PGEMM=0, a fresh context)."""
+    round-5 prefill GEMM (QTTS_HIP_PGEMM=0, a fresh context) and on k_pgemm's
+    128 x 128 tile form (QTTS_HIP_PGEMM_BN=128, read per launch)."""
     import os
     from conftest import GOLDEN
     from parity import codes_equal
@@ -262,9 +263,12 @@ def test_c5_bench_shape_vs_oracle_fixture(full_tts, monkeypatch):
     g = np.load(os.path.join(GOLDEN, "vc_c5_b8.npz"))
     inp = bench_inputs(full_tts.cfg.num_code_groups, full_tts.cfg.talker_hidden)
     T = int(g["frames"])
-    for env in ("1", "0"):
+    for env in ("1", "bn128", "0"):
         m = full_tts
+        if env == "bn128":   # the 128 x 128 tile form of k_pgemm (the default takes 128 x 256 at 584 rows)
+            monkeypatch.setenv("QTTS_HIP_PGEMM_BN", "128")
         if env == "0":
+            monkeypatch.delenv("QTTS_HIP_PGEMM_BN", raising=False)
             monkeypatch.setenv("QTTS_HIP_PGEMM", "0")
             m = qtts.QwenTTS(model_dir("1.7b"))
         try:
@@ -290,13 +294,18 @@ def test_prefill_gemm_matches_round5_gemm(gpu, monkeypatch):
     the multi-tile-plus-split-K shapes) -- prefill hidden allclose, the same
     products summed in another order."""
     outs = {}
-    for env in ("1", "0"):
-        monkeypatch.setenv("QTTS_HIP_PGEMM", env)
+    for env in ("1", "bn128", "bn256", "0"):   # "1": the tile width by row count
+        monkeypatch.setenv("QTTS_HIP_PGEMM", "0" if env == "0" else "1")
+        monkeypatch.setenv("QTTS_HIP_PGEMM_BN", env[2:] if env.startswith("bn") else "auto")
         m = qtts.QwenTTS(model_dir("1.7b"))
         try:
             outs[env] = [m.prefill((np.random.default_rng(n).standard_normal((n, m.cfg.talker_hidden)) * 0.5)
                                    .astype(np.float32)) for n in (24, 97, 300)]
         finally:
             m.close()
-    for a, b in zip(outs["1"], outs["0"]):
+    for a, b, b2, c in zip(outs["1"], outs["bn128"], outs["bn256"], outs["0"]):
+        np.testing.assert_allclose(a, c, atol=1e-4, rtol=1e-4)
+        np.testing.assert_allclose(b2, c, atol=1e-4, rtol=1e-4)
+        # (the tile widths split K into different column counts where the tiles
+        # alone would not fill the chip: the same products, grouped otherwise)
         np.testing.assert_allclose(a, b, atol=1e-4, rtol=1e-4)
