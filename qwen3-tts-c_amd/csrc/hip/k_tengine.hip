@@ -182,46 +182,65 @@ __device__ __forceinline__ int qkv_row(int h, int i) {
 // One decode-attention split of kv head kvh on the comm waves (k_attn_dec<128,
 // 2, 8>'s arithmetic; inputs from L.hq; barriers among the comm waves only).
 // Returns through granules: the head's merged output, by the last split.
-__device__ void comm_attention(TLds &L, const TLayerArgs &a, int kvh, int split, int nact, int p, unsigned tag,
-                               int ct, int lane, int cw, int &gen) {
-    const int n = p + 1;
-    const int t0 = split * CH, t1 = min(n, t0 + CH);
-    const bool owner = (split == nact - 1);
+// The split's inputs that do not depend on this step's q|k|v: its cached key
+// and value rows, the QK-norm weights and the RoPE row of position p.  Loaded
+// at the comm role's start, so the attention after the head gather waits on
+// no memory but the gather itself.  (Position p's own row is never read from
+// the cache: it comes from LDS.)
+struct AttnPre {
+    float4 kreg[DPL / 4];
+    float4 vreg[NVC];
+    float hw[2], rc[2], rs[2];
+};
+__device__ __forceinline__ void attn_preload(AttnPre &q, const TLayerArgs &a, int kvh, int split, int p, int ct,
+                                             int lane, int cw) {
+    const int t0 = split * CH, t1 = min(p + 1, t0 + CH);
     const int KVD = KVH * HD;
     const float *Kc = a.kc + kvh * HD;
     const float *Vc = a.vc + kvh * HD;
-    // token inputs (from the gathered head) and the RoPE rows, then the cache loads
     const int hh0 = cw < GPH ? cw : GPH;
-    float hv[2], hw[2], rc[2], rs[2];
-    {
-        const float *src = L.hq + (hh0 < GPH ? hh0 * HD : NO);
-        const float *nw = hh0 < GPH ? a.qn_w : a.kn_w;
-        const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
+    const float *nw = hh0 < GPH ? a.qn_w : a.kn_w;
+    const float *cs = a.rope_cos + (size_t)p * HD, *sn = a.rope_sin + (size_t)p * HD;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            hv[j] = src[lane + 64 * j];
-            hw[j] = nw[lane + 64 * j];
-            rc[j] = cs[lane + 64 * j];
-            rs[j] = sn[lane + 64 * j];
-        }
+    for (int j = 0; j < 2; ++j) {
+        q.hw[j] = nw[lane + 64 * j];
+        q.rc[j] = cs[lane + 64 * j];
+        q.rs[j] = sn[lane + 64 * j];
     }
-    const float vtok = L.hq[NO + HD + ct % HD];
     const int kl = ct / LPK, ksub = ct - kl * LPK;
     const int tk = t0 + kl;
-    float4 kreg[DPL / 4];
-    {
-        const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(tk < t1 ? tk : t0) * KVD + ksub * DPL);
+    const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)(tk < t1 ? tk : t0) * KVD + ksub * DPL);
 #pragma unroll
-        for (int j = 0; j < DPL / 4; ++j) kreg[j] = kp[j];
-    }
+    for (int j = 0; j < DPL / 4; ++j) q.kreg[j] = kp[j];
     const int d4 = ct % D4, kg = ct / D4;
-    float4 vreg[NVC];
 #pragma unroll
     for (int j = 0; j < NVC; ++j) {
         const int t = t0 + kg + j * KG;
         const bool ok = kg + j * KG < CH && t < t1;
-        vreg[j] = reinterpret_cast<const float4 *>(Vc + (size_t)(ok ? t : t0) * KVD)[d4];
+        q.vreg[j] = reinterpret_cast<const float4 *>(Vc + (size_t)(ok ? t : t0) * KVD)[d4];
     }
+}
+
+__device__ void comm_attention(TLds &L, const TLayerArgs &a, int kvh, int split, int nact, int p, unsigned tag,
+                               int ct, int lane, int cw, int &gen, const AttnPre &pre) {
+    const int n = p + 1;
+    const int t0 = split * CH, t1 = min(n, t0 + CH);
+    const bool owner = (split == nact - 1);
+    const int KVD = KVH * HD;
+    // token inputs (from the gathered head); the rest came with the preload
+    const int hh0 = cw < GPH ? cw : GPH;
+    float hv[2];
+    {
+        const float *src = L.hq + (hh0 < GPH ? hh0 * HD : NO);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) hv[j] = src[lane + 64 * j];
+    }
+    const float *hw = pre.hw, *rc = pre.rc, *rs = pre.rs;
+    const float4 *kreg = pre.kreg, *vreg = pre.vreg;
+    const float vtok = L.hq[NO + HD + ct % HD];
+    const int kl = ct / LPK, ksub = ct - kl * LPK;
+    const int tk = t0 + kl;
+    const int d4 = ct % D4, kg = ct / D4;
     // QK-norm + RoPE in registers (waves 0..GPH: q heads, then k)
     if (cw <= GPH) {
         float ss = 0.f;
@@ -325,16 +344,37 @@ __device__ void comm_attention(TLds &L, const TLayerArgs &a, int kvh, int split,
     }
     cbarrier(L, gen, lane, a.err);
     if (!L.last) return;
-    // the merge in split order (k_attn_dec's / k_gemvw's deferred merge arithmetic)
+    // the merge in split order (k_attn_dec's / k_gemvw's deferred merge
+    // arithmetic), its loads issued 8 splits at a time (one dependent round
+    // trip per 8 splits, not one per split)
     const int g = ct / HD;
+    constexpr int MB = 8;
     float M = -INFINITY;
-    for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, ld_sc1(base + (size_t)s2 * stride + NO + 2 * g));
+    for (int s0 = 0; s0 < nact; s0 += MB) {
+        float mv[MB];
+#pragma unroll
+        for (int j = 0; j < MB; ++j)
+            mv[j] = s0 + j < nact ? ld_sc1(base + (size_t)(s0 + j) * stride + NO + 2 * g) : -INFINITY;
+#pragma unroll
+        for (int j = 0; j < MB; ++j) M = fmaxf(M, mv[j]);
+    }
     float num = 0.f, den = 0.f;
-    for (int s2 = 0; s2 < nact; ++s2) {
-        const float *ps = base + (size_t)s2 * stride;
-        const float f = expf(ld_sc1(ps + NO + 2 * g) - M);
-        num = fmaf(f, ld_sc1(ps + ct), num);
-        den = fmaf(f, ld_sc1(ps + NO + 2 * g + 1), den);
+    for (int s0 = 0; s0 < nact; s0 += MB) {
+        float mv[MB], pv[MB], lv[MB];
+#pragma unroll
+        for (int j = 0; j < MB; ++j) {
+            const float *ps = base + (size_t)min(s0 + j, nact - 1) * stride;
+            mv[j] = ld_sc1(ps + NO + 2 * g);
+            pv[j] = ld_sc1(ps + ct);
+            lv[j] = ld_sc1(ps + NO + 2 * g + 1);
+        }
+#pragma unroll
+        for (int j = 0; j < MB; ++j) {
+            if (s0 + j >= nact) break;
+            const float f = expf(mv[j] - M);
+            num = fmaf(f, pv[j], num);
+            den = fmaf(f, lv[j], den);
+        }
     }
     put_granule(gout + ct, tag, num / den);
     if (ct == 0) __hip_atomic_store(a.cnt + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -363,6 +403,10 @@ struct Slice {
 
 // the comm waves (threads 256..511): input gathers, RMSNorm, the decode
 // attention of this workgroup's kv head splits, the output granules
+// DIRECT (the ring engine): the consumer waves publish their own output
+// granules (no LDS hop through the comm waves); the comm waves still wait for
+// the consumers' local done signal before each sweep (see step 2).
+template <bool DIRECT>
 __device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid, int lane, int wv, int b) {
     const unsigned epoch = (unsigned)a.epoch[0];
     const unsigned tag = epoch * 32u + (unsigned)a.layer + 1u;
@@ -371,6 +415,8 @@ __device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid,
     int gen = 0;
     const int p = a.pos[0];                        // the token's position (kv_len before this step)
     const int nact = (p + 1 + CH - 1) / CH;
+    AttnPre pre;                                   // this workgroup's first split's cache rows, ahead of everything
+    if (j32 < nact) attn_preload(pre, a, h, j32, p, ct, lane, cw);
     // 1. x (the layer input) -> RMSNorm (input_layernorm) -> LDS
     {
         float4 xv[2];
@@ -380,9 +426,13 @@ __device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid,
         comm_stage(L, 1, gen, lane, a.err);
         te_stamp(a, 1, ct == 0);
     }
-    // 2. this workgroup's 16 q|k|v rows -> granules
+    // 2. this workgroup's 16 q|k|v rows -> granules (DIRECT: the consumers
+    //    published them; waiting for their local signal still keeps the sweep
+    //    below from polling the whole phase -- polling beside the weight stream
+    //    slows the stream, MI355X_MICROARCH.md polling-cost: gate|up 5 -> 15 us
+    //    when the h sweep started at once, profiles/r06r_ring_engine_stamps.txt)
     comm_wait_out(L, 1, a.err);
-    if (ct < 16) put_granule(a.g_qkv + qkv_row(h, 16 * j32 + ct), tag, L.outq[ct]);
+    if (!DIRECT && ct < 16) put_granule(a.g_qkv + qkv_row(h, 16 * j32 + ct), tag, L.outq[ct]);
     te_stamp(a, 3, ct == 0);
     // 3. the attention splits of kv head h this workgroup runs (split j32, j32 + 32, ...)
     if (j32 < nact) {
@@ -393,7 +443,8 @@ __device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid,
         cbarrier(L, gen, lane, a.err);
         te_stamp(a, 4, ct == 0);
         for (int s = j32; s < nact; s += 32) {
-            comm_attention(L, a, h, s, nact, p, tag, ct, lane, cw, gen);
+            if (s != j32) attn_preload(pre, a, h, s, p, ct, lane, cw);   // (beyond 1024 keys)
+            comm_attention(L, a, h, s, nact, p, tag, ct, lane, cw, gen, pre);
             cbarrier(L, gen, lane, a.err);
         }
         te_stamp(a, 5, ct == 0);
@@ -410,7 +461,7 @@ __device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid,
     }
     // 5. this workgroup's 8 x' rows -> granules
     comm_wait_out(L, 2, a.err);
-    if (ct < 8) put_granule(a.g_x + 8 * b + ct, tag, L.outo[ct]);
+    if (!DIRECT && ct < 8) put_granule(a.g_x + 8 * b + ct, tag, L.outo[ct]);
     // 6. x' of every row, in k_gemvw's unit mapping (thread ct: elements
     //    4 (ct + 256 q) + e) -> RMSNorm (post_attention_layernorm) -> LDS
     //    (the GEMV waves finished reading xs: this workgroup's O rows are in)
@@ -427,7 +478,7 @@ __device__ __forceinline__ void comm_role(TLds &L, const TLayerArgs &a, int tid,
     }
     // 7. this workgroup's 24 h values -> granules (wave w, pair k: gate row 48 b + w + 8 k)
     comm_wait_out(L, 3, a.err);
-    if (ct < 24) {
+    if (!DIRECT && ct < 24) {
         const int w = ct / 6, k = ct - 6 * (ct / 6);
         const int r = 48 * b + w + 8 * k;
         put_granule(a.g_h + (r >> 3) * 4 + (r & 3), tag, L.outh[ct]);
@@ -549,7 +600,7 @@ __global__ __launch_bounds__(512, 1) void k_tlayer(TLayerArgs a) {
         return;
     }
 
-    comm_role(L, a, tid, lane, wv, b);
+    comm_role<false>(L, a, tid, lane, wv, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -714,11 +765,13 @@ __global__ __launch_bounds__(RING_THREADS, 1) void k_tlayer_ring(TLayerArgs a) {
         return;
     }
     if (wv >= 4) {
-        comm_role(L, a, tid, lane, wv, b);
+        comm_role<true>(L, a, tid, lane, wv, b);
         return;
     }
     // ================= consumer waves =================
     const int w = wv;
+    const unsigned tag = (unsigned)a.epoch[0] * 32u + (unsigned)a.layer + 1u;   // (comm_role's tag)
+    const int h = b >> 5, j32 = b & 31;
     float yres[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) yres[r] = a.x_in[8 * b + w + 4 * r];
@@ -729,22 +782,22 @@ __global__ __launch_bounds__(RING_THREADS, 1) void k_tlayer_ring(TLayerArgs a) {
     float aq[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) aq[s] = ring_row(L, ring, s, w, xr, lane, ok);
-    te_stamp(a, 2, tid == 0);
-    if (lane == 0)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) L.outq[w + 4 * s] = aq[s];
+    // (lane s publishes row 4 s + w of the workgroup's q|k|v list)
+    if (lane < 4) {
+        const float v = lane == 0 ? aq[0] : lane == 1 ? aq[1] : lane == 2 ? aq[2] : aq[3];
+        put_granule(a.g_qkv + qkv_row(h, 16 * j32 + 4 * lane + w), tag, v);
+    }
     gemv_done(L, lane);
+    te_stamp(a, 2, tid == 0);
     // O rows + residual
     ok &= gemv_wait(L, 2);
     load_xr(L.xs, xr, lane);
     float xm[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) xm[s] = yres[s] + ring_row(L, ring, 4 + s, w, xr, lane, ok);
-    te_stamp(a, 7, tid == 0);
-    if (lane == 0)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) L.outo[w + 4 * s] = xm[s];
+    if (lane < 2) put_granule(a.g_x + 8 * b + w + 4 * lane, tag, lane == 0 ? xm[0] : xm[1]);
     gemv_done(L, lane);
+    te_stamp(a, 7, tid == 0);
     // gate|up rows, SwiGLU: pair k = (gate slot 6 + 2k, up slot 7 + 2k)
     ok &= gemv_wait(L, 3);
     load_xr(L.xs, xr, lane);
@@ -755,11 +808,16 @@ __global__ __launch_bounds__(RING_THREADS, 1) void k_tlayer_ring(TLayerArgs a) {
         const float u = ring_row(L, ring, 7 + 2 * k, w, xr, lane, ok);
         hv[k] = (g / (1.0f + expf(-g))) * u;
     }
-    te_stamp(a, 10, tid == 0);
-    if (lane == 0)
+    // (lane k publishes pair k: gate row 48 b + w + 8 k)
+    if (lane < 6) {
+        float v = hv[0];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) L.outh[6 * w + k] = hv[k];
+        for (int k = 1; k < 6; ++k) v = lane == k ? hv[k] : v;
+        const int r = 48 * b + w + 8 * lane;
+        put_granule(a.g_h + (r >> 3) * 4 + (r & 3), tag, v);
+    }
     gemv_done(L, lane);
+    te_stamp(a, 10, tid == 0);
     // down rows w, w + 4 + residual -> the layer output (read by the next launch)
     ok &= gemv_wait(L, 4);
     float sd[2] = {0.f, 0.f};
