@@ -43,6 +43,22 @@ Fixtures
                    with aiden / vivian / serena, seed 42, default sampling --
                    each one reference run: the stop step (= frames emitted),
                    all codes, every 16th sample.
+  long_hd128_max.npz  the reference's full decode capacity on the `hd128`
+                   model: max_new_tokens 4096 frames, fixed (P128 prompt,
+                   seed 42, default sampling) -- talker positions to ~4200,
+                   i.e. > 128 splits of 32 keys in the decode attention and
+                   its merge (the maximum-size edge case of T.c:119-248).
+                   Codes, every 256th sample, first and last frame.
+  long_hd128_steps4k.npz  the `hd128` model's stage functions near the
+                   capacity: a 4000-row prefill of seeded embeddings, then 4
+                   decode steps at positions 4000-4003 (> 125 splits of 32
+                   keys): the prefill's last hidden row, per-step logits and
+                   hidden.
+  long_17b_1100.npz  the synthetic 1.7B past 1024 keys: P128 prompt, fixed
+                   1100 frames (positions to ~1140: > 32 splits of 32 keys per
+                   kv head -- the talker layer engine's second split round),
+                   seed 42, default sampling; codes, every 256th sample,
+                   first and last frame.
   long_manifest.json  SHA-256 of the model files the fixtures were made from.
 """
 import argparse
@@ -102,6 +118,52 @@ def prefill_inputs(H, seed=PREFILL_SEED):
     return emb, steps
 
 
+MAX_FRAMES = 4096       # the reference's max_new_tokens default: the decode capacity
+MAX_STRIDE = 256
+
+
+def hd128_max_fixture():
+    md = ensure_model(os.path.join(MODEL_ROOT, "hd128"), "hd128")
+    ref = RefLib(md)
+    ids = np.array(prompt_ids("p128"), np.int32)
+    ref.set_params(max_tokens=MAX_FRAMES, fixed=MAX_FRAMES, seed=42, **DEFAULT)
+    t = time.time()
+    audio = ref.generate(ids, "aiden", "english")
+    print(f"hd128 decode {MAX_FRAMES} frames: {time.time() - t:.1f} s", file=sys.stderr)
+    codes = ref.recorded_codes()
+    assert codes.shape == (MAX_FRAMES, ref.cfg["cq"]), codes.shape
+    g = {"prompt_ids": ids, "codes": codes, "audio_sub": audio[::MAX_STRIDE].copy(),
+         "audio_first": audio[:1920].copy(), "audio_last": audio[-1920:].copy(),
+         "audio_len": np.array(len(audio), np.int64)}
+    return g, md
+
+
+STEPS4K_ROWS = 4000     # hd128 stage prefill near the decode capacity, then decode steps
+STEPS4K_SEED = 20261019
+
+
+def hd128_steps4k_fixture():
+    """A 4000-row prefill of seeded embeddings, then 4 decode steps at
+    positions 4000-4003 (125+ splits of 32 keys): prefill hidden (last row),
+    per-step logits and hidden -- the decode attention near the capacity,
+    compared with a tolerance (no sampling, so no near-tie can flip it)."""
+    md = ensure_model(os.path.join(MODEL_ROOT, "hd128"), "hd128")
+    ref = RefLib(md)
+    rng = np.random.Generator(np.random.PCG64(STEPS4K_SEED))
+    emb = (rng.standard_normal((STEPS4K_ROWS, ref.cfg["H"])) * 0.5).astype(np.float32)
+    steps = (rng.standard_normal((PREFILL_STEPS, ref.cfg["H"])) * 0.5).astype(np.float32)
+    t = time.time()
+    hid = ref.prefill(emb)
+    lg, hd = [], []
+    for i in range(PREFILL_STEPS):
+        l, h = ref.step(steps[i])
+        lg.append(l)
+        hd.append(h)
+    print(f"hd128 {STEPS4K_ROWS}-row prefill + {PREFILL_STEPS} steps: {time.time() - t:.1f} s", file=sys.stderr)
+    g = {"prefill_hidden": np.asarray(hid).copy(), "step_logits": np.stack(lg), "step_hidden": np.stack(hd)}
+    return g, md
+
+
 def hd128_fixtures():
     md = ensure_model(os.path.join(MODEL_ROOT, "hd128"), "hd128")
     ref = RefLib(md)
@@ -144,6 +206,25 @@ def bench_fixtures():
     assert codes.shape == (BENCH_FRAMES, ref.cfg["cq"]), codes.shape
     ref.close()
     return {"prompt_ids": ids, "codes": codes, "audio": audio}, md
+
+
+K1100_FRAMES = 1100     # 1.7B past 1024 keys: > 32 splits of 32 keys per kv head
+
+
+def k1100_fixture():
+    md = ensure_model(os.path.join(MODEL_ROOT, "1.7b"), "1.7b")
+    ref = RefLib(md)
+    ids = np.array(prompt_ids("p128"), np.int32)
+    ref.set_params(max_tokens=K1100_FRAMES, fixed=K1100_FRAMES, seed=42, **DEFAULT)
+    t = time.time()
+    audio = ref.generate(ids, "aiden", "english")
+    print(f"1.7b {K1100_FRAMES} frames: {time.time() - t:.1f} s", file=sys.stderr)
+    codes = ref.recorded_codes()
+    assert codes.shape == (K1100_FRAMES, ref.cfg["cq"]), codes.shape
+    ref.close()
+    return {"prompt_ids": ids, "codes": codes, "audio_sub": audio[::MAX_STRIDE].copy(),
+            "audio_first": audio[:1920].copy(), "audio_last": audio[-1920:].copy(),
+            "audio_len": np.array(len(audio), np.int64)}, md
 
 
 def c2_fixtures():
@@ -270,7 +351,7 @@ def eos17_fixtures(slot_dir=None, utts=(0, 1, 2)):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["hd128", "1.7b", "0.6b", "b8", "b8bench", "eos17", "eos17q"])
+    ap.add_argument("--only", choices=["hd128", "hd128max", "steps4k", "k1100", "1.7b", "0.6b", "b8", "b8bench", "eos17", "eos17q"])
     ap.add_argument("--eos-slot", type=int, default=None, help="run one EOS slot into --slot-dir and exit")
     ap.add_argument("--slot-dir", default=None, help="eos17: per-slot results of --eos-slot runs")
     a = ap.parse_args()
@@ -293,6 +374,23 @@ def main():
         man["hd128"] = {"frames": LONG_FRAMES, "prompt": "p128", "seed": 42, "sampling": "default",
                         "audio_stride": AUDIO_STRIDE, "prefill_rows": PREFILL_ROWS, "prefill_steps": PREFILL_STEPS,
                         "prefill_seed": PREFILL_SEED}
+    if a.only == "hd128max":   # (not in the default set: a 4096-frame reference run)
+        g, md = hd128_max_fixture()
+        np.savez_compressed(os.path.join(HERE, "long_hd128_max.npz"), **g)
+        man["models"]["hd128"] = model_hashes(md)
+        man["hd128max"] = {"frames": MAX_FRAMES, "prompt": "p128", "seed": 42, "sampling": "default",
+                           "speaker": "aiden", "language": "english", "audio_stride": MAX_STRIDE}
+    if a.only == "steps4k":
+        g, md = hd128_steps4k_fixture()
+        np.savez_compressed(os.path.join(HERE, "long_hd128_steps4k.npz"), **g)
+        man["models"]["hd128"] = model_hashes(md)
+        man["steps4k"] = {"prefill_rows": STEPS4K_ROWS, "prefill_seed": STEPS4K_SEED, "steps": PREFILL_STEPS}
+    if a.only == "k1100":   # (not in the default set: a 1100-frame 1.7B reference run, ~30 min)
+        g, md = k1100_fixture()
+        np.savez_compressed(os.path.join(HERE, "long_17b_1100.npz"), **g)
+        man["models"]["1.7b"] = model_hashes(md)
+        man["k1100"] = {"frames": K1100_FRAMES, "prompt": "p128", "seed": 42, "sampling": "default",
+                        "speaker": "aiden", "language": "english", "audio_stride": MAX_STRIDE}
     if a.only in (None, "1.7b"):
         g, md = bench_fixtures()
         np.savez_compressed(os.path.join(HERE, "long_17b.npz"), **g)
@@ -340,7 +438,7 @@ def main():
                                 "before it, so the codes equal the reference's 4096-token run")
     with open(mpath, "w") as f:
         json.dump(man, f, indent=1)
-    for fn in ("long_hd128.npz", "long_17b.npz", "long_06b.npz", "long_17b_b8.npz", "long_17b_b8bench.npz",
+    for fn in ("long_hd128.npz", "long_hd128_max.npz", "long_hd128_steps4k.npz", "long_17b_1100.npz", "long_17b.npz", "long_06b.npz", "long_17b_b8.npz", "long_17b_b8bench.npz",
                "long_eos17.npz", "long_eos17q.npz", "long_manifest.json"):
         p = os.path.join(HERE, fn)
         if os.path.exists(p):

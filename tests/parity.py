@@ -32,3 +32,25 @@ def codes_equal(got, want, what, ctx=None):
             except Exception as e:   # the verdict is a diagnostic: never mask the failure itself
                 msg += f"; classification failed ({e!r})"
     raise AssertionError(msg)
+
+
+def codes_equal_upto_classified(got, want, what, known):
+    """The bar for very long runs, where some draw of tens of thousands sits
+    within rounding of a boundary: the codes are bit-exact up to the first
+    divergence, and that divergence is one recorded in the fixture's manifest
+    entry (`known`: [{frame, group, got, verdict, record}]) with an
+    "fp near-tie" verdict from tools/classify_divergence.py.  Any other
+    divergence fails (a kernel change that moves it must be re-classified).
+    Returns the first divergent frame (None: no divergence)."""
+    assert got is not None, what
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    bad = np.argwhere(got != want)
+    if not len(bad):
+        return None
+    f, g = (int(v) for v in bad[0])
+    for k in known or []:
+        if (k["frame"], k["group"], k["got"]) == (f, g, int(got[f, g])) and k["verdict"].startswith("fp near-tie"):
+            return f
+    raise AssertionError(f"{what}: first divergent code at frame {f} group {g} (got {got[f, g]}, reference "
+                         f"{want[f, g]}; {len(bad)} codes differ) -- not a recorded near-tie: run "
+                         f"tools/classify_divergence.py")

@@ -83,3 +83,25 @@ def test_long_fixtures_describe_the_bench_workloads():
         n, T = int(q["prompt_len"][b]), int(q["stop_step"][b])
         np.testing.assert_array_equal(q["prompt_ids"][b, :n], prompt_ids("p128", sd))
         assert (q["codes"][b, :T] >= 0).all() and (q["codes"][b, T:] == -1).all()
+
+
+def test_long_capacity_fixtures_extend_the_shorter_runs():
+    """The long-capacity reference fixtures (no compute): long_hd128_max (4096
+    frames, fixed) starts with the 640-frame run of long_hd128, and
+    long_17b_1100 (1100 frames, fixed) with the bench workload of long_17b --
+    the same prompt, seed and sampling, so the reference drew the same codes
+    for the shared frames (fixed mode only re-draws an EOS, never a code)."""
+    man = json.load(open(os.path.join(GOLDEN, "long_manifest.json")))
+    p = os.path.join(GOLDEN, "long_hd128_max.npz")
+    if os.path.exists(p):
+        a, b = np.load(p), np.load(os.path.join(GOLDEN, "long_hd128.npz"))
+        assert a["codes"].shape == (man["hd128max"]["frames"], 16)
+        np.testing.assert_array_equal(a["codes"][:man["hd128"]["frames"]], b["decode_codes"])
+        np.testing.assert_array_equal(a["audio_first"], b["decode_audio_first"])
+        np.testing.assert_array_equal(a["prompt_ids"], b["prompt_ids"])
+    p = os.path.join(GOLDEN, "long_17b_1100.npz")
+    if os.path.exists(p):
+        a, b = np.load(p), np.load(os.path.join(GOLDEN, "long_17b.npz"))
+        assert a["codes"].shape == (man["k1100"]["frames"], 16)
+        np.testing.assert_array_equal(a["codes"][:man["1.7b"]["frames"]], b["codes"])
+        np.testing.assert_array_equal(a["audio_first"], b["audio"][:1920])

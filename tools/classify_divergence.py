@@ -19,7 +19,8 @@ from oracle_py import DEFAULT, Oracle  # noqa: E402
 from qtts_io import lookup_ids  # noqa: E402
 
 KEYS = {"long_eos17": ("eos17", "1.7b"), "long_eos17q": ("eos17q", "1.7b"), "long_17b_b8": ("b8", "1.7b"),
-        "long_17b_b8bench": ("b8bench", "1.7b")}
+        "long_17b_b8bench": ("b8bench", "1.7b"), "long_hd128_max": ("hd128max", "hd128"),
+        "long_17b_1100": ("k1100", "1.7b")}
 
 
 def main():
@@ -33,16 +34,17 @@ def main():
     key, preset = KEYS[a.fixture]
     g = np.load(os.path.join(ROOT, "tests", "golden", a.fixture + ".npz"))
     man = json.load(open(os.path.join(ROOT, "tests", "golden", "long_manifest.json")))[key]
-    ids = g["prompt_ids"][a.utt, :int(g["prompt_len"][a.utt])]
+    single = g["prompt_ids"].ndim == 1   # one-utterance fixtures (codes [frames][groups])
+    ids = g["prompt_ids"] if single else g["prompt_ids"][a.utt, :int(g["prompt_len"][a.utt])]
     ovr = {"eos_gain": man["eos_gain"]} if "eos_gain" in man else {}
     md = model_dir(preset, **ovr)
     o = Oracle(md)
-    spk = man["speakers"][a.utt]
+    spk = man["speaker"] if single else man["speakers"][a.utt]
     s, l = lookup_ids(o.cfg, spk, man.get("language", "english"))
     fixed = 0 if "eos_gain" in man else man["frames"]
     params = dict(max_tokens=4096, fixed=fixed, seed=man["seed"], **DEFAULT)
     c = classify(o, ids, s, l, a.frame, a.group, params, got=a.got)
-    want = int(g["codes"][a.utt, a.frame, a.group])
+    want = int(g["codes"][a.frame, a.group] if single else g["codes"][a.utt, a.frame, a.group])
     c["fixture_code"] = want
     print(json.dumps({k: (float(v) if isinstance(v, (np.floating,)) else v) for k, v in c.items()}))
     print(describe(c))
