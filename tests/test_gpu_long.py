@@ -11,6 +11,9 @@ Fixtures (tests/golden/make_golden_long.py, from the reference c/ build):
   (batch 1 merging its own 64-key splits) runs all 640 frames, so batch 1
   also reaches > 8 splits of 64 keys.  The codes must be bit-exact all the
   way.  A 600-row prefill (> 512 rows) and 4 decode steps over 600+ keys.
+* `long_hd128_max.npz` -- the same model over the reference's whole decode
+  capacity (4096 frames, positions to ~4200: > 128 key splits).
+* `long_17b_1100.npz` -- the synthetic 1.7B past 1024 keys (fixed 1100 frames).
 * `long_17b.npz` -- the benchmark workload itself (bench.py): synthetic 1.7B,
   P128 prompt, fixed 128 frames, default sampling, seed 42.
 * `long_06b.npz` -- BASELINE configs[1] (C2): synthetic 0.6B (H = H_s = 1024,
@@ -37,7 +40,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, model_dir
-from parity import codes_equal
+from parity import codes_equal, codes_equal_upto_classified
 from make_golden_long import prefill_inputs
 from oracle_py import DEFAULT, GREEDY, Oracle
 from qtts_io import lookup_ids
@@ -89,6 +92,56 @@ def test_hd128_640_frames_vs_reference(hd128):
         o.close()
 
 
+def test_hd128_max_capacity_vs_reference(hd128):
+    """The reference's whole decode capacity (max_new_tokens 4096, fixed): talker
+    positions to ~4200, i.e. > 128 key splits per kv head in the decode
+    attention and the O prologue's merge of them (the maximum-size edge case),
+    codes bit-exact against the reference's own 4096-frame run
+    (long_hd128_max.npz) up to a recorded fp near-tie, the waveform against
+    its samples before it."""
+    path = os.path.join(GOLDEN, "long_hd128_max.npz")
+    if not os.path.exists(path):
+        pytest.skip("long_hd128_max.npz not generated (make_golden_long.py --only hd128max)")
+    m, md, _, _ = hd128
+    g = np.load(path)
+    man = _man()["hd128max"]
+    m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+    a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
+    # 65,536 draws: bit-exact up to the first divergence, which must be the
+    # recorded, classified fp near-tie (profiles/r06_classify_hd128max.txt)
+    f = codes_equal_upto_classified(m.last_codes(), g["codes"], "hd128 4096-frame decode",
+                                    man.get("near_ties"))
+    assert a.shape[0] == int(g["audio_len"])
+    n = len(a) if f is None else f * 1920   # (the codec is causal: samples before frame f see only equal codes)
+    st = man["audio_stride"]
+    _audio_close(a[:n:st], g["audio_sub"][:(n + st - 1) // st], "every 256th sample (before any divergence)")
+    _audio_close(a[:1920], g["audio_first"], "first frame")
+    if f is None:
+        _audio_close(a[-1920:], g["audio_last"], "last frame")
+
+
+def test_17b_past_1024_keys_vs_reference(gpu):
+    """The synthetic 1.7B past 1024 keys (fixed 1100 frames, P128): > 32 splits
+    of 32 keys per kv head in the talker's decode attention and its merge in
+    the O prologue; codes bit-exact against the reference's own run
+    (long_17b_1100.npz)."""
+    path = os.path.join(GOLDEN, "long_17b_1100.npz")
+    if not os.path.exists(path):
+        pytest.skip("long_17b_1100.npz not generated (make_golden_long.py --only k1100)")
+    g = np.load(path)
+    man = _man()["k1100"]
+    m = qtts.QwenTTS(model_dir("1.7b"))
+    try:
+        m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
+        _codes_equal(m.last_codes(), g["codes"], "1.7B 1100-frame decode")
+        assert a.shape[0] == int(g["audio_len"])
+        _audio_close(a[::man["audio_stride"]], g["audio_sub"], "every 256th sample")
+        _audio_close(a[-1920:], g["audio_last"], "last frame")
+    finally:
+        m.close()
+
+
 def test_hd128_640_frames_lock_step_batch(hd128):
     """The same utterance as slot 0 and 2 of a lock-step batch of 3 (batch
     attention rows through the same split merges): bit-equal to the reference."""
@@ -112,6 +165,29 @@ def test_hd128_600_row_prefill_and_steps_vs_reference(hd128):
     h = m.prefill(emb)
     np.testing.assert_allclose(h, g["prefill_hidden"], atol=1e-4, rtol=1e-4)
     for i in range(man["prefill_steps"]):
+        lg, hid = m.step(steps[i])
+        np.testing.assert_allclose(lg, g["step_logits"][i], atol=1e-4, rtol=1e-4)
+        np.testing.assert_allclose(hid, g["step_hidden"][i], atol=1e-4, rtol=1e-4)
+
+
+def test_hd128_4000_row_prefill_and_steps_vs_reference(hd128):
+    """Near the decode capacity: a 4000-row prefill of seeded embeddings, then
+    decode steps at positions 4000-4003 -- 125+ splits of 32 keys per kv head
+    and their merge in the O prologue -- hidden and logits within the stage
+    bar against the reference's (long_hd128_steps4k.npz; no sampling, so no
+    near-tie can turn a rounding difference into a different id)."""
+    path = os.path.join(GOLDEN, "long_hd128_steps4k.npz")
+    if not os.path.exists(path):
+        pytest.skip("long_hd128_steps4k.npz not generated (make_golden_long.py --only steps4k)")
+    m, md, _, _ = hd128
+    g = np.load(path)
+    man = _man()["steps4k"]
+    rng = np.random.Generator(np.random.PCG64(man["prefill_seed"]))
+    emb = (rng.standard_normal((man["prefill_rows"], m.cfg.talker_hidden)) * 0.5).astype(np.float32)
+    steps = (rng.standard_normal((man["steps"], m.cfg.talker_hidden)) * 0.5).astype(np.float32)
+    h = m.prefill(emb)
+    np.testing.assert_allclose(h, g["prefill_hidden"], atol=1e-4, rtol=1e-4)
+    for i in range(man["steps"]):
         lg, hid = m.step(steps[i])
         np.testing.assert_allclose(lg, g["step_logits"][i], atol=1e-4, rtol=1e-4)
         np.testing.assert_allclose(hid, g["step_hidden"][i], atol=1e-4, rtol=1e-4)

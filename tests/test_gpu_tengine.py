@@ -89,3 +89,28 @@ def test_tengine_eos_batch_1_vs_reference(gpu, monkeypatch, mode):
         assert _engine_layers() - n0 >= 28, "the talker layer engine was not selected"
     finally:
         m.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_tengine_past_1024_keys_vs_reference(gpu, monkeypatch, mode):
+    """Positions past 1024 (fixed 1100 frames): the engine's attention runs a
+    second round of splits (split j32 + 32) in the workgroups of each kv head,
+    with the cache rows loaded inside the loop; codes bit-exact against the
+    reference's own run (long_17b_1100.npz)."""
+    path = os.path.join(GOLDEN, "long_17b_1100.npz")
+    if not os.path.exists(path):
+        pytest.skip("long_17b_1100.npz not generated (make_golden_long.py --only k1100)")
+    monkeypatch.setenv("QTTS_HIP_TENGINE", mode)
+    g = np.load(path)
+    man = _man()["k1100"]
+    m = qtts.QwenTTS(model_dir("1.7b"))
+    n0 = _engine_layers()
+    try:
+        m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        a = m.generate(g["prompt_ids"], man["speaker"], man["language"])
+        assert _engine_layers() - n0 >= 28, "the talker layer engine was not selected"
+        codes_equal(m.last_codes(), g["codes"], f"engine {mode}: 1.7B 1100-frame decode")
+        sub = a[::man["audio_stride"]]
+        _audio_close(sub, g["audio_sub"], f"engine {mode}: every 256th sample")
+    finally:
+        m.close()
