@@ -600,6 +600,9 @@ __global__ __launch_bounds__(256) void k_attn_o(const float *rsrc, const int *id
     };
     attn_short_wg<HD, false>(t, kvh, b, lq, sc, att, rb == 0, issue, rsrc, ids);
     __syncthreads();
+#ifdef QTTS_STAMPS
+    if (t.dbg && tid == 0) t.dbg[wgl * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+#endif
     float acc = 0.f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {

@@ -27,6 +27,14 @@
 // wcache = false: the token's k / v are used but not stored (another
 // workgroup of the launch stores them).
 struct NoIssue { __device__ __forceinline__ void operator()() const {} };
+// (stamp builds: phase stamps of the attention inside k_attn_o -- slots 1 / 5 /
+// 6 of the gm_dbg record: q|k staged, scores, softmax)
+__device__ __forceinline__ void as_stamp(const AttnArgs &a, int k) {
+#ifdef QTTS_STAMPS
+    if (a.dbg && threadIdx.x == 0)
+        a.dbg[(blockIdx.x + (size_t)gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
 // `issue` runs right after the attention's own loads are issued (k_attn_o
 // issues its O-weight fragment there: loads retire in issue order, so the
 // attention's inputs must not queue behind the weights)
@@ -116,6 +124,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
         }
     }
     __syncthreads();
+    as_stamp(a, 1);
 
     // ---- scores q.k_t / sqrt(HD) (T.c:662-665)
     {
@@ -133,6 +142,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
         if (sub == 0 && gs < 2) sc[gs][ts] = ts < n ? d * div_rn(1.0f, sqrt_rn((float)HD)) : -INFINITY;
     }
     __syncthreads();
+    as_stamp(a, 5);
 
     // ---- softmax per head over its <= 16 keys
     if (tid < 2 * NK) {
@@ -146,6 +156,7 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
         sc[g][t] = e * div_rn(1.0f, sum);
     }
     __syncthreads();
+    as_stamp(a, 6);
 
     // ---- P.V, keys in order (T.c:667-671)
     if (go < 2) {
