@@ -79,16 +79,24 @@ __device__ __forceinline__ void attn_short_wg(const AttnArgs &a, int kvh, int r,
         s4 = reinterpret_cast<const float4 *>(a.rope_sin + (size_t)p * HD)[l];
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the K / V / W_o loads behind these
+    // K / V rows: unconditional loads from rows clamped below a.S (the slot's
+    // cache capacity), whose values are read only for keys t < p below.
+    // (Loads under a per-element condition compiled to one branch-wrapped
+    // dword load each -- 16 + 16 of them -- and the wait for x counted them
+    // all: the q|k|v row was staged 2.2 us into k_attn_o,
+    // profiles/r06x_attn_o_phases.txt.)
     const int dI = tid / LPK, sub = tid - dI * LPK, gs = dI / NK, ts = dI - gs * NK;
-    const bool kld = gs < 2 && ts < p;
     float4 kr[4];
+    {
+        const int tr = gs < 2 && ts < a.S ? ts : 0;
+        const float4 *kp = reinterpret_cast<const float4 *>(Kc + (size_t)tr * KVD + 16 * sub);
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-        kr[c] = kld ? reinterpret_cast<const float4 *>(Kc + (size_t)ts * KVD + 16 * sub)[c] : zero4;
+        for (int c = 0; c < 4; ++c) kr[c] = kp[c];
+    }
     const int go = tid / HD, dd = tid - go * HD;
     float vr[NK];
 #pragma unroll
-    for (int t = 0; t < NK; ++t) vr[t] = (go < 2 && t < p) ? Vc[(size_t)t * KVD + dd] : 0.f;
+    for (int t = 0; t < NK; ++t) vr[t] = Vc[(size_t)(t < a.S ? t : a.S - 1) * KVD + dd];
     issue();
 
     // ---- per-head RMSNorm (T.c:646-649) + RoPE (T.c:650-653) -> LDS; k, v -> cache (T.c:654-655)
