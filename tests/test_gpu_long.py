@@ -315,6 +315,32 @@ def test_c4_bench_workload_batch8_vs_reference(gpu, monkeypatch, env):
         m.close()
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_BKZ_WIDE": "0"}])
+def test_c4_bench_workload_batch16_vs_reference(gpu, monkeypatch, env):
+    """`bench.py --batch 16`'s shape: the bench workload's 8 utterances twice
+    in ONE lock-step batch of 16 -- above 8 rows the split-K producers reduce
+    their own partials, and the 1.7B talker's down projection runs on 4
+    split-K columns (bsplit_kz; BKZ_WIDE=0: 2 columns on k_gemvm) -- slots b
+    and b + 8 bit-exact against reference run b (long_17b_b8bench.npz)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = np.load(os.path.join(GOLDEN, "long_17b_b8bench.npz"))
+    man = _man()["b8bench"]
+    m = qtts.QwenTTS(model_dir("1.7b"))
+    try:
+        m.set_params(max_tokens=man["frames"], fixed=man["frames"], seed=man["seed"], **DEFAULT)
+        rc, audio = m.generate_batch(_b8_prompts(g) * 2, man["speakers"] * 2, [man["language"]] * 16)
+        assert rc == 0
+        codes = m.last_codes_batch()
+        for s in range(16):
+            b = s % 8
+            _codes_equal(codes[s], g["codes"][b], f"bench batch-16 slot {s} {env}")
+            _audio_close(audio[s][-1920:], g["audio_last"][b], f"slot {s} last frame")
+    finally:
+        m.close()
+
+
 def _eos_slot_check(codes, audio, g, man, b, what):
     n = int(g["stop_step"][b])
     _codes_equal(codes, g["codes"][b, :n], f"{what}: slot {b} codes up to the reference's stop")
