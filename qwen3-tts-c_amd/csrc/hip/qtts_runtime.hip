@@ -124,7 +124,7 @@ struct qtts_dev {
     bool bsplit = true;      // QTTS_HIP_BSPLIT=0: batch O / down projections without split-K
     int bself_min = 9;       // batch split-K producers reduce their own partials from this many rows up
     int bkz_max = 0;         // QTTS_HIP_BKZ_MAX: cap on the batch split-K columns (0: 2 up to 8 rows, else 4)
-    bool bkz_wide = true;    // QTTS_HIP_BKZ_WIDE=0: above 8 rows, no extra split-K columns for > 2048-wide slices (bsplit_kz)
+    int bkz_wide = 1;        // QTTS_HIP_BKZ_WIDE=0: above 8 rows, no extra split-K columns for > 2048-wide slices (bsplit_kz); 2: from 2 rows, up to 4 columns
     float *x_st = nullptr, *qkv_s = nullptr, *att_s = nullptr, *h_s = nullptr, *logits_s = nullptr;
     float *kc = nullptr, *vc = nullptr, *kcs = nullptr, *vcs = nullptr;
     int *codes = nullptr, *counts = nullptr, *n_gen = nullptr, *stopped = nullptr, *cur_row = nullptr;
@@ -447,7 +447,7 @@ extern "C" qtts_dev_t *qtts_dev_create(const qtts_dims_t *dims, int device) {
     const char *bk = getenv("QTTS_HIP_BKZ_MAX");
     if (bk) dv->bkz_max = atoi(bk) < 1 ? 1 : atoi(bk) > 4 ? 4 : atoi(bk);
     const char *bw = getenv("QTTS_HIP_BKZ_WIDE");
-    dv->bkz_wide = !(bw && !atoi(bw));
+    dv->bkz_wide = bw ? atoi(bw) : 1;
     const char *bm = getenv("QTTS_HIP_BSELF_MIN");
     if (bm) dv->bself_min = atoi(bm);
     const char *ad = getenv("QTTS_HIP_ATTN_DEFER");
@@ -974,8 +974,10 @@ static int bsplit_kz(const qtts_dev *dv, int R, int C) {
     // over the 160 KB of LDS, and the launch fell back to k_gemvm (17.5 us at
     // batch 16 against 10.1 us for batch 8's k_gemvb); more columns keep the
     // slices at <= 4 steps a wave
-    if (dv->nrun > 8 && dv->bkz_wide)
-        while (2 * kz <= cap && C / kz > 2048 && C % (64 * kz) == 0) kz *= 2;
+    if ((dv->nrun > 8 && dv->bkz_wide) || dv->bkz_wide == 2) {
+        const int wcap = dv->bkz_wide == 2 ? 4 : cap;
+        while (2 * kz <= wcap && C / kz > 2048 && C % (64 * kz) == 0) kz *= 2;
+    }
     while (kz > 1 && C % (32 * kz)) kz /= 2;
     return kz > 1 ? kz : 0;
 }
