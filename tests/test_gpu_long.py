@@ -290,13 +290,14 @@ def test_hd128_attention_switch_paths_vs_reference(gpu, monkeypatch, env, frames
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}])
+@pytest.mark.parametrize("env", [{}, {"QTTS_HIP_GEMVB": "0"}, {"QTTS_HIP_BKZ_WIDE": "2"}])
 def test_c4_bench_workload_batch8_vs_reference(gpu, monkeypatch, env):
     """C4's per-GPU bench workload itself (`bench.py --batch 8`, rank 0): p128
     seeds 1234-1241, speaker aiden, seed 42, default sampling, the whole 128
     frames -- decoded as ONE lock-step batch, every slot's 128 x 16 codes
     bit-exact against its own reference run (long_17b_b8bench.npz), audio
-    against the reference's samples.  Also on the staged-plane batch GEMV."""
+    against the reference's samples.  Also on the staged-plane batch GEMV,
+    and with the talker's down projection on 4 split-K columns (BKZ_WIDE=2)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = np.load(os.path.join(GOLDEN, "long_17b_b8bench.npz"))
